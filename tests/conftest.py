@@ -1,0 +1,82 @@
+"""Shared pytest configuration.
+
+Markers:
+  gpu -- needs an MI355X (runs through the HIP C-ABI); everything else runs on CPU.
+"""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+GOLDEN = REPO / "tests" / "golden"
+for p in (str(REPO), str(REPO / "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD MI355X GPU (HIP path)")
+
+
+def load_cases(name):
+    """Load tests/golden/<name>.npz as {case: {field: array}}."""
+    z = np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
+    cases = {}
+    for key in z.files:
+        if "/" not in key:
+            continue
+        case, field = key.split("/", 1)
+        cases.setdefault(case, {})[field] = z[key]
+    return cases, z
+
+
+def load_run(name):
+    z = np.load(GOLDEN / f"run_{name}.npz", allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+RUN_FIXTURES = sorted(p.stem[4:] for p in GOLDEN.glob("run_*.npz") if p.stem != "run_real_stand10")
+
+# k parity is pinnable only where the reference's own FRMSD curve separates the best k
+# from the runner-up by more than rounding noise (SURVEY.md §7 "k-collapse").
+K_GAP_PIN = 1e-9
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import ficp_oracle
+    ficp_oracle.build()
+    return ficp_oracle
+
+
+def pinned_prefix(gap, frmsd, scale):
+    """Number of leading NN/fraction calls of a reference trace whose k is pinned.
+
+    A call is pinned when the reference's own FRMSD curve separates the best k from the
+    runner-up by more than K_GAP_PIN (relative) AND the FRMSD itself is above rounding
+    level for the coordinates (exact synthetic data collapses to ~1e-15 residuals and
+    k=1): past the first unpinned call, trajectories may legitimately
+    differ in k while the final XY still agree within 1e-6."""
+    gap = np.asarray(gap)
+    frmsd = np.asarray(frmsd)
+    ok = (gap > K_GAP_PIN) & (frmsd > 1e-9 * scale)
+    return len(ok) if ok.all() else int(np.argmin(ok))
+
+
+def assert_T_close(T, Tref, pts, atol_R=1e-9, atol_xy=1e-6, msg=""):
+    """Compare rigid transforms the way the north star states parity: R within atol_R
+    and the transform's action on the plot's own points within atol_xy (abs).  With
+    geo-referenced coordinates (~6.5e6 m) the raw translation t = ct - R cs amplifies
+    ULP differences of R by |cs|, so it is compared through its action instead."""
+    T = np.asarray(T).reshape(-1, 3, 3)
+    Tref = np.asarray(Tref).reshape(-1, 3, 3)
+    assert T.shape == Tref.shape, (T.shape, Tref.shape, msg)
+    xy = np.asarray(pts)[:, :2]
+    for i in range(len(T)):
+        np.testing.assert_allclose(T[i, :2, :2], Tref[i, :2, :2], atol=atol_R, rtol=0, err_msg=f"{msg} R[{i}]")
+        a = xy @ T[i, :2, :2].T + T[i, :2, 2]
+        b = xy @ Tref[i, :2, :2].T + Tref[i, :2, 2]
+        np.testing.assert_allclose(a, b, atol=atol_xy, rtol=0, err_msg=f"{msg} T[{i}] action")

@@ -1,0 +1,118 @@
+"""Pin the CPU oracle (oracle/ficp_oracle.c) to the reference's golden vectors.
+
+The vectors were produced by the reference ficp.py (tests/golden/make_golden.py);
+the oracle is trusted as the HIP path's checker only because these pass.
+"""
+import numpy as np
+import pytest
+
+from conftest import K_GAP_PIN, RUN_FIXTURES, load_cases, load_run, pinned_prefix, assert_T_close
+
+
+@pytest.mark.parametrize("method", ["brute", "kdtree"])
+def test_nn_bit_exact(oracle, method):
+    cases, _ = load_cases("nn")
+    assert cases
+    for name, c in cases.items():
+        md = int(c["md"])
+        idx, dist, d2 = oracle.nn(c["src"], c["tgt"], md, method=method, nthreads=4)
+        np.testing.assert_array_equal(idx, c["idx"], err_msg=name)
+        assert np.array_equal(dist.view(np.uint64), c["dist"].view(np.uint64)), name
+
+
+def test_nn_facade_returns_all_target_columns(oracle):
+    cases, _ = load_cases("nn")
+    c = cases["d4_unit"]
+    icp = oracle.OracleFICP(c["src"], c["tgt"])
+    corr, dist = icp.find_correspondences(icp.source, icp.target)
+    assert corr.shape == (len(c["src"]), 4)
+    np.testing.assert_array_equal(corr, c["tgt"][c["idx"]])
+
+
+def test_optimal_fraction(oracle):
+    cases, _ = load_cases("frac")
+    for name, c in cases.items():
+        lam = float(c["lambda"])
+        for literal in (False, True):
+            frac, k, fr = oracle.optimal_fraction(c["src"], c["corr"], c["dist"], len(c["src"]), int(c["md"]),
+                                                  lam, literal=literal)
+            if float(c["gap"]) > K_GAP_PIN:
+                assert k == int(c["k"]), (name, k, int(c["k"]))
+                assert frac == float(c["frac"])
+            np.testing.assert_allclose(fr, float(c["frmsd"]), rtol=1e-12, err_msg=name)
+
+
+def test_fit(oracle):
+    cases, _ = load_cases("fit")
+    for name, c in cases.items():
+        T = oracle.fit_rigid2d(c["src"], c["tgt"], bool(c["allow_reflection"]))
+        scale = 1.0 + np.abs(c["src"][:, :2]).max()
+        np.testing.assert_allclose(T[:2, :2], c["T"][:2, :2], atol=1e-12, err_msg=name)
+        np.testing.assert_allclose(T[:2, 2], c["T"][:2, 2], atol=1e-12 * scale, err_msg=name)
+        np.testing.assert_array_equal(T[2], [0.0, 0.0, 1.0])
+
+
+def test_apply_bit_exact(oracle):
+    cases, _ = load_cases("apply")
+    for name, c in cases.items():
+        out = oracle.apply_xy(c["pts"], c["T"])
+        assert np.array_equal(out.view(np.uint64), c["out"].view(np.uint64)), name
+
+
+@pytest.mark.parametrize("name", RUN_FIXTURES)
+def test_run_trace(oracle, name):
+    r = load_run(name)
+    final, tr = oracle.run(r["src"], r["tgt"], threshold=float(r["kwargs_threshold"]),
+                           max_iterations=int(r["kwargs_max_iterations"]), trace_idx=True)
+    # final XY within 1e-6 abs (north star), every other column bit-identical
+    np.testing.assert_allclose(final[:, :2], r["final"][:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(final[:, 2:], r["final"][:, 2:])
+    scale = 1.0 + np.abs(r["src"][:, :2]).max()
+    first = pinned_prefix(r["gap"], r["frmsd"], scale)
+    np.testing.assert_array_equal(tr["k"][:first], r["k"][:first])
+    np.testing.assert_array_equal(tr["lam"][:first], r["lam"][:first])
+    np.testing.assert_array_equal(tr["idx"][:first], r["idx"][:first])
+    if first == len(r["k"]):
+        # the whole trajectory is pinned: same number of calls, fits within tolerance
+        assert tr["n_calls"] == len(r["k"])
+        assert_T_close(tr["T"], r["T"], r["src"], msg=name)
+    else:
+        nf = min(first, len(r["T"]))
+        assert_T_close(tr["T"][:nf], r["T"][:nf], r["src"], msg=name)
+
+
+def test_real_stand10(oracle):
+    z = np.load(__import__("conftest").GOLDEN / "run_real_stand10.npz")
+    tgt = z["tgt"]
+    for pid in z["plot_ids"]:
+        src = z[f"{pid}/src"]
+        final, tr = oracle.run(src, tgt, trace_idx=True)
+        np.testing.assert_allclose(final, z[f"{pid}/final"], atol=1e-6, rtol=0, err_msg=str(pid))
+        gap = z[f"{pid}/gap"]
+        if np.all(gap > K_GAP_PIN):
+            np.testing.assert_array_equal(tr["k"], z[f"{pid}/k"])
+            np.testing.assert_array_equal(tr["idx"], z[f"{pid}/idx"])
+
+
+def test_empty_contracts(oracle):
+    cases, _ = load_cases("empty")
+    from ficp_oracle import OracleFICP
+    import coregistrationgame_amd.synth as synth
+    a = OracleFICP(np.empty((0, 3)), synth.make_cloud(n=5, seed=42)).run()
+    assert tuple(a.shape) == tuple(cases["empty_source"]["shape"])
+    icp = OracleFICP(synth.make_cloud(n=4, seed=24), np.empty((0, 3)))
+    corr, d = icp.find_correspondences(icp.source, icp.target)
+    frac, k = icp.find_optimal_fraction(corr, d)
+    assert tuple(corr.shape) == tuple(cases["empty_target"]["corr_shape"])
+    assert d.size == int(cases["empty_target"]["dist_size"])
+    assert (frac, k) == (float(cases["empty_target"]["frac"]), int(cases["empty_target"]["k"]))
+
+
+def test_oracle_kdtree_equals_brute_large(oracle):
+    """Independent NN algorithms agree bit-for-bit on a larger geo-referenced plot."""
+    from coregistrationgame_amd import synth
+    p = synth.make_plot(20000, 20000, 0.7, seed=5, md=3)
+    a = oracle.nn(p.source, p.target, 3, "kdtree", nthreads=8)
+    b = oracle.nn(p.source, p.target, 3, "brute", nthreads=8)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])

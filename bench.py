@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: FICP iterations/s at 1M trees x 1M CHM stems (BASELINE.json metric).
+
+One "step" = one complete FractionalICP.run() (ficp.py:149-154: two FRMSD stages to
+convergence) of one synthetic C3 plot whose layers are already resident in HBM:
+static-layer grid build + copy of the pristine source + the device-resident ICP.
+`value` = ICP loop bodies (fit -> apply -> NN -> sort -> FRMSD scan; ficp.py:132-145)
+completed per second over all ranks; the two initial NN+selection passes per run are
+inside the timed region but not counted as iterations.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank co-registers its own
+independent 1M x 1M plot (seed 1_000_000 + rank) -- plots shard with no data-path
+collective ("scaling": "weak"); torch.distributed only provides the barrier and the
+max-over-ranks time.
+
+Other workloads (not the default bench line): --workload c2 (100k x 100k, f=0.8, exactly
+50 loop bodies), --workload batch (C4 plots of 10k x 10k, dealt over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+from coregistrationgame_amd import _lib, synth  # noqa: E402
+
+METRIC = "FICP iterations/sec (and correspondences/sec) at 1M×1M points, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+WORKLOADS = {
+    # name: (n, m, f, seed0, md, threshold, max_iterations, description)
+    "c3": (1_000_000, 1_000_000, 0.6, 1_000_000, 3, 1e-6, 1000,
+           "C3: 1M trees vs 1M CHM stems, f=0.6, md=3, run() to convergence (threshold 1e-6)"),
+    "c2": (100_000, 100_000, 0.8, 100_000, 3, float("-inf"), 25,
+           "C2: 100k trees vs 100k CHM stems, f=0.8, md=3, exactly 2x25 loop bodies"),
+}
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+class DevArray:
+    """A device buffer owned through libficp (no torch types at the boundary)."""
+
+    def __init__(self, ctx: _lib.Context, host: np.ndarray):
+        host = np.ascontiguousarray(host, dtype=np.float64)
+        self.ctx, self.n = ctx, host.size
+        p = _lib.C.c_void_p()
+        _lib._check(_lib.lib().ficp_dev_alloc(ctx.h, host.nbytes, _lib.C.byref(p)))
+        self.ptr = p.value
+        _lib._check(_lib.lib().ficp_memcpy_h2d(ctx.h, _lib.C.c_void_p(self.ptr), host.ctypes.data_as(_lib.C.c_void_p),
+                                               host.nbytes))
+
+    def copy_from(self, other: "DevArray"):
+        _lib._check(_lib.lib().ficp_memcpy_d2d(self.ctx.h, _lib.C.c_void_p(self.ptr), _lib.C.c_void_p(other.ptr),
+                                               8 * self.n))
+
+    def free(self):
+        _lib.lib().ficp_dev_free(self.ctx.h, _lib.C.c_void_p(self.ptr))
+
+
+def nn_bytes_per_launch(n, m, md):
+    """Algorithmic HBM bytes of one fused apply+NN launch: per tree read md
+    coordinates, write the moved XY (16 B), write idx (4) + dist (8); read the CHM layer
+    once (8*md per stem) -- SURVEY.md §8(d)'s NN + apply terms."""
+    return n * (8 * md + 16 + 12) + m * 8 * md
+
+
+def cpu_baseline(plot, threads):
+    """The pinned C oracle (oracle/ficp_oracle.c, kind "port") on the same C3 plot: static
+    kd-tree + O(N) fraction scan, 2 stages x 2 loop bodies (threshold -inf), timed on
+    this host's cores.  Bounded sample; the reference ficp.py itself would need ~5.5 h per
+    iteration at 1M (O(N^2) scan)."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import ficp_oracle
+    ficp_oracle.build()
+    t0 = time.perf_counter()
+    _, tr = ficp_oracle.run(plot.source, plot.target, threshold=float("-inf"), max_iterations=2,
+                            nthreads=threads, trace=True)
+    dt = time.perf_counter() - t0
+    return {"value": tr["n_fits"] / dt, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": f"C3 plot (1M x 1M, md=3): 2 stages x 2 loop bodies ({tr['n_calls']} NN calls, "
+                      f"{tr['n_fits']} fits) in {dt:.2f} s; kd-tree built once, O(N) FRMSD scan, "
+                      f"{threads} OpenMP threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--nn-mode", default="grid", choices=["auto", "brute", "grid"])
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n, m, f, seed0, md, thr, max_it, desc = WORKLOADS[args.workload]
+    plot = synth.make_plot(n, m, f, seed0 + rank, md=md)
+    ctx = _lib.Context(local, {"auto": 0, "brute": 1, "grid": 2}[args.nn_mode])
+    cols = [plot.source[:, j] for j in range(md)]
+    tcols = [plot.target[:, j] for j in range(md)]
+    src0 = [DevArray(ctx, c) for c in cols]          # pristine source, resident
+    src = [DevArray(ctx, c) for c in cols]           # working copy (x, y move)
+    tgt = [DevArray(ctx, c) for c in tcols]
+    lam = [3.0, 0.95 if md == 3 else 1.3]
+
+    def step():
+        src[0].copy_from(src0[0])
+        src[1].copy_from(src0[1])
+        ctx.set_target_device(tgt[0].ptr, tgt[1].ptr, tgt[2].ptr if md == 3 else 0, m, md)
+        return ctx.run_device(src[0].ptr, src[1].ptr, src[2].ptr if md == 3 else 0, n, lam, thr, max_it)
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.profile_report()  # drop warmup records
+    ctx.profile_enable(_lib.PROF_NN)
+    barrier()
+    t0 = time.perf_counter()
+    fits = calls = 0
+    for _ in range(args.steps):
+        st = step()
+        fits += st["n_fits"]
+        calls += st["n_nn_calls"]
+    barrier()
+    dt = time.perf_counter() - t0
+    ctx.profile_enable(0)
+    prof = json.loads(ctx.profile_report())
+
+    tot = np.array([dt, fits, calls], dtype=np.float64)
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        c = torch.tensor([float(fits), float(calls)], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        tot = np.array([t.item(), c[0].item(), c[1].item()])
+    dt_max, fits_all, calls_all = tot
+
+    if rank == 0:
+        nn = prof.get("nn_grid") or prof.get("nn_brute") or {"count": 0, "ms": 0.0}
+        avg_ms = nn["ms"] / max(nn["count"], 1)
+        bytes_launch = nn_bytes_per_launch(n, m, md)
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": fits_all / dt_max,
+            "unit": "iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * dt_max / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": f"synthetic (SURVEY.md §8(d) generator, seed {seed0}+rank, geo-referenced)",
+            "config": {"workload": desc, "n_trees": n, "n_chm": m, "inlier_fraction": f, "match_dims": md,
+                       "plots_per_rank": 1, "parallelism": f"{world} independent plots (1 per GPU)",
+                       "nn": args.nn_mode},
+            "iterations_per_step": fits_all / args.steps / world,
+            "nn_calls_per_step": calls_all / args.steps / world,
+            "correspondences_per_s": calls_all * n / dt_max,
+            "roofline": {"bound": "hbm", "kernel": "nn_grid (fused apply + exact 1-NN)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "avg_launch_us": avg_ms * 1e3, "launches": nn["count"],
+                         "algorithmic_bytes_per_launch": bytes_launch},
+            "kernel_ms": prof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(plot, threads)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+
+    for a in src0 + src + tgt:
+        a.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

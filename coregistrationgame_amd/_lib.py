@@ -1,0 +1,306 @@
+"""ctypes binding of libficp.so (include/ficp.h).
+
+The HIP library is the only compute path: if it is missing, or no GPU is visible,
+every entry point raises -- there is no CPU fallback in the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libficp.so"
+CSRC = PKG / "csrc"
+HEADER = PKG.parent / "include" / "ficp.h"
+
+FICP_OK = 0
+FICP_EINVAL = -1
+FICP_EHIP = -2
+FICP_ENOMEM = -3
+FICP_ESTATE = -4
+FICP_ENODEV = -5
+
+NN_AUTO, NN_BRUTE, NN_GRID = 0, 1, 2
+PROF_NN, PROF_SORT, PROF_FRAC, PROF_FIT, PROF_GRID = 1, 2, 4, 8, 16
+
+_dp = C.POINTER(C.c_double)
+_ip32 = C.POINTER(C.c_int32)
+_ip64 = C.POINTER(C.c_int64)
+_i64 = C.c_int64
+_i32 = C.c_int32
+_vp = C.c_void_p
+
+
+class FicpError(RuntimeError):
+    pass
+
+
+class Stats(C.Structure):
+    """struct ficp_stats (include/ficp.h)."""
+    _fields_ = [
+        ("n_nn_calls", C.c_int32), ("n_fits", C.c_int32), ("iters", C.c_int32 * 2),
+        ("k_last", C.c_int64), ("frmsd_last", C.c_double * 2), ("T_total", C.c_double * 9),
+        ("gpu_ms", C.c_double), ("max_trace", C.c_int32), ("_pad", C.c_int32),
+        ("trace_k", _ip64), ("trace_frmsd", _dp), ("trace_lambda", _dp), ("trace_T", _dp),
+        ("trace_idx", _ip32),
+    ]
+
+
+def header_symbols() -> list[str]:
+    """Every entry point declared in include/ficp.h."""
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(ficp_[a-z0-9_]+)\s*\(", txt)))
+
+
+def build(force: bool = False) -> Path:
+    """Compile libficp.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    env = dict(os.environ)
+    cmd = ["make", "-C", str(CSRC), "-j8"]
+    if force:
+        subprocess.run(["make", "-C", str(CSRC), "clean"], check=True, env=env)
+    subprocess.run(cmd, check=True, env=env)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Load libficp.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise FicpError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                        " or `make -C coregistrationgame_amd/csrc` (no CPU fallback exists)")
+    L = C.CDLL(str(LIB_PATH))
+    sig = {
+        "ficp_version": ([], C.c_int),
+        "ficp_last_error": ([], C.c_char_p),
+        "ficp_device_count": ([C.POINTER(C.c_int)], C.c_int),
+        "ficp_create": ([C.c_int, C.POINTER(_vp)], C.c_int),
+        "ficp_destroy": ([_vp], None),
+        "ficp_set_nn_mode": ([_vp, _i32], C.c_int),
+        "ficp_profile_enable": ([_vp, _i32], C.c_int),
+        "ficp_profile_report": ([_vp, C.c_char_p, _i64], C.c_int),
+        "ficp_set_target": ([_vp, _dp, _i64, _i64, _i32], C.c_int),
+        "ficp_set_target_device": ([_vp, _vp, _vp, _vp, _i64, _i32], C.c_int),
+        "ficp_nn": ([_vp, _dp, _i64, _i64, _ip32, _dp], C.c_int),
+        "ficp_optimal_fraction": ([_vp, _dp, _i64, _dp, _i64, _dp, _i64, _i64, _i32, C.c_double,
+                                   _dp, _ip64], C.c_int),
+        "ficp_frmsd": ([_vp, _dp, _i64, _dp, _i64, _i64, _i64, _i32, C.c_double, C.c_double, _dp],
+                       C.c_int),
+        "ficp_argsort": ([_vp, _dp, _i64, _ip64], C.c_int),
+        "ficp_fit_rigid2d": ([_vp, _dp, _i64, _dp, _i64, _i64, _i32, _dp], C.c_int),
+        "ficp_apply_xy": ([_vp, _dp, _i64, _i64, _dp, _dp], C.c_int),
+        "ficp_run": ([_vp, _dp, _i64, _i64, _i32, _dp, C.c_double, _i32, _i32, C.POINTER(Stats)],
+                     C.c_int),
+        "ficp_run_device": ([_vp, _vp, _vp, _vp, _i64, _i32, _dp, C.c_double, _i32, _i32,
+                             C.POINTER(Stats)], C.c_int),
+        "ficp_dev_alloc": ([_vp, _i64, C.POINTER(_vp)], C.c_int),
+        "ficp_dev_free": ([_vp, _vp], C.c_int),
+        "ficp_memcpy_h2d": ([_vp, _vp, _vp, _i64], C.c_int),
+        "ficp_memcpy_d2h": ([_vp, _vp, _vp, _i64], C.c_int),
+        "ficp_memcpy_d2d": ([_vp, _vp, _vp, _i64], C.c_int),
+        "ficp_synchronize": ([_vp], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != FICP_OK:
+        msg = lib().ficp_last_error().decode(errors="replace")
+        if rc == FICP_EINVAL:
+            raise ValueError(msg)
+        raise FicpError(f"libficp error {rc}: {msg}")
+
+
+def _p(a, t=_dp):
+    return a.ctypes.data_as(t)
+
+
+def _rows(a) -> np.ndarray:
+    """C-contiguous float64 2-D view/copy (the boundary's row-major layout)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if a.ndim == 1:
+        a = a.reshape(-1, 1)
+    return a
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib().ficp_device_count(C.byref(n))
+    if rc != FICP_OK:
+        return 0
+    return n.value
+
+
+def default_device() -> int:
+    for var in ("FICP_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(var, "").strip():
+            return int(os.environ[var])
+    return 0
+
+
+class Context:
+    """One libficp context (one HIP stream on one device, resident CHM layer)."""
+
+    def __init__(self, device: int | None = None, nn_mode: int = NN_AUTO):
+        self.device = default_device() if device is None else int(device)
+        h = _vp()
+        _check(lib().ficp_create(self.device, C.byref(h)))
+        self.h = h
+        self.md = None
+        self.m = 0
+        if nn_mode:
+            self.set_nn_mode(nn_mode)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ficp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_nn_mode(self, mode: int):
+        _check(lib().ficp_set_nn_mode(self.h, int(mode)))
+
+    def profile_enable(self, mask: int):
+        _check(lib().ficp_profile_enable(self.h, int(mask)))
+
+    def profile_report(self) -> str:
+        buf = C.create_string_buffer(1 << 16)
+        _check(lib().ficp_profile_report(self.h, buf, len(buf)))
+        return buf.value.decode()
+
+    # ---- target
+    def set_target(self, tgt, md: int):
+        t = _rows(tgt)
+        _check(lib().ficp_set_target(self.h, _p(t), len(t), t.shape[1], int(md)))
+        self.md, self.m = int(md), len(t)
+
+    def set_target_device(self, x_ptr: int, y_ptr: int, z_ptr: int, m: int, md: int):
+        _check(lib().ficp_set_target_device(self.h, _vp(x_ptr), _vp(y_ptr), _vp(z_ptr or 0), int(m), int(md)))
+        self.md, self.m = int(md), int(m)
+
+    # ---- hot-path operations
+    def nn(self, src):
+        s = _rows(src)
+        n = len(s)
+        idx = np.zeros(n, np.int32)
+        dist = np.zeros(n, np.float64)
+        _check(lib().ficp_nn(self.h, _p(s), n, s.shape[1], _p(idx, _ip32), _p(dist)))
+        return idx, dist
+
+    def optimal_fraction(self, src, corr, dist, n_source: int, md: int, lam: float):
+        s, c = _rows(src), _rows(corr)
+        d = np.ascontiguousarray(dist, dtype=np.float64).ravel()
+        frac = C.c_double()
+        k = C.c_int64()
+        _check(lib().ficp_optimal_fraction(self.h, _p(s), s.shape[1], _p(c), c.shape[1], _p(d), len(d),
+                                           int(n_source), int(md), float(lam), C.byref(frac), C.byref(k)))
+        return frac.value, k.value
+
+    def frmsd(self, src, corr, num_elements: int, md: int, fraction: float, lam: float):
+        s, c = _rows(src), _rows(corr)
+        out = C.c_double()
+        _check(lib().ficp_frmsd(self.h, _p(s), s.shape[1], _p(c), c.shape[1], len(s), int(num_elements),
+                                int(md), float(fraction), float(lam), C.byref(out)))
+        return out.value
+
+    def argsort(self, d):
+        d = np.ascontiguousarray(d, dtype=np.float64).ravel()
+        order = np.zeros(len(d), np.int64)
+        _check(lib().ficp_argsort(self.h, _p(d), len(d), _p(order, _ip64)))
+        return order
+
+    def fit_rigid2d(self, src, tgt, allow_reflection: bool):
+        s, t = _rows(src), _rows(tgt)
+        T = np.zeros(9)
+        _check(lib().ficp_fit_rigid2d(self.h, _p(s), s.shape[1], _p(t), t.shape[1], len(s),
+                                      int(bool(allow_reflection)), _p(T)))
+        return T.reshape(3, 3)
+
+    def apply_xy(self, pts, T):
+        p = _rows(pts)
+        T = np.ascontiguousarray(T, dtype=np.float64).reshape(9)
+        out = np.zeros((len(p), 2))
+        _check(lib().ficp_apply_xy(self.h, _p(p), len(p), p.shape[1], _p(T), _p(out)))
+        return out
+
+    def run(self, src_inout: np.ndarray, lambdas, threshold: float, max_iterations: int,
+            allow_reflection: bool, trace: bool = False, trace_idx: bool = False, max_trace: int = 4096):
+        """Runs the stages in place on a C-contiguous float64 (n, ld) array."""
+        assert src_inout.dtype == np.float64 and src_inout.flags.c_contiguous and src_inout.ndim == 2
+        lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+        st, keep = _make_stats(len(src_inout), trace, trace_idx, max_trace)
+        _check(lib().ficp_run(self.h, _p(src_inout), len(src_inout), src_inout.shape[1], len(lam), _p(lam),
+                              float(threshold), int(max_iterations), int(bool(allow_reflection)), C.byref(st)))
+        return _stats_dict(st, keep, len(src_inout))
+
+    def run_device(self, x_ptr: int, y_ptr: int, z_ptr: int, n: int, lambdas, threshold: float,
+                   max_iterations: int, allow_reflection: bool = False):
+        lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+        st, keep = _make_stats(n, False, False, 0)
+        _check(lib().ficp_run_device(self.h, _vp(x_ptr), _vp(y_ptr), _vp(z_ptr or 0), int(n), len(lam), _p(lam),
+                                     float(threshold), int(max_iterations), int(bool(allow_reflection)),
+                                     C.byref(st)))
+        return _stats_dict(st, keep, n)
+
+    def synchronize(self):
+        _check(lib().ficp_synchronize(self.h))
+
+
+def _make_stats(n, trace, trace_idx, max_trace):
+    st = Stats()
+    keep = {}
+    if trace:
+        st.max_trace = max_trace
+        keep["k"] = np.zeros(max_trace, np.int64)
+        keep["frmsd"] = np.zeros(max_trace)
+        keep["lam"] = np.zeros(max_trace)
+        keep["T"] = np.zeros(max_trace * 9)
+        st.trace_k, st.trace_frmsd = _p(keep["k"], _ip64), _p(keep["frmsd"])
+        st.trace_lambda, st.trace_T = _p(keep["lam"]), _p(keep["T"])
+        if trace_idx:
+            keep["idx"] = np.zeros((max_trace, n), np.int32)
+            st.trace_idx = _p(keep["idx"], _ip32)
+    return st, keep
+
+
+def _stats_dict(st, keep, n):
+    nc = st.n_nn_calls
+    nf = st.n_fits
+    out = dict(n_nn_calls=nc, n_fits=nf, iters=(st.iters[0], st.iters[1]), k_last=st.k_last,
+               frmsd_last=(st.frmsd_last[0], st.frmsd_last[1]),
+               T_total=np.array(st.T_total[:]).reshape(3, 3), gpu_ms=st.gpu_ms)
+    if keep:
+        m = st.max_trace
+        out["k"] = keep["k"][:min(nc, m)].copy()
+        out["frmsd"] = keep["frmsd"][:min(nc, m)].copy()
+        out["lam"] = keep["lam"][:min(nc, m)].copy()
+        out["T"] = keep["T"][:min(nf, m) * 9].reshape(-1, 3, 3).copy()
+        if "idx" in keep:
+            out["idx"] = keep["idx"][:min(nc, m)].copy()
+    return out

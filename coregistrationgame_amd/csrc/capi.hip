@@ -1,0 +1,753 @@
+// capi.hip -- the C ABI of include/ficp.h: context, buffers, the ICP driver loop.
+//
+// The loop is the reference's _iterate (ficp.py:122-147) with every array operation on
+// the device; per iteration the host reads back one small IterState (k, FRMSD, T) to
+// take the convergence decision `current - new <= threshold` (ficp.py:142).
+#include "../../include/ficp.h"
+#include "ficp_internal.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <cmath>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <vector>
+
+using namespace ficp;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(FICP_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+
+#define CHK(expr)                  \
+    do {                           \
+        int r_ = (expr);           \
+        if (r_ != FICP_OK) return r_; \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return FICP_OK;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(FICP_ENOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        cap = want;
+        return FICP_OK;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T *as() const {
+        return (T *)p;
+    }
+};
+
+enum ProfClass { P_NN = 1, P_SORT = 2, P_FRAC = 4, P_FIT = 8, P_GRID = 16, P_MISC = 32 };
+
+struct ProfRec {
+    const char *name;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct ficp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int nn_mode = 0;
+
+    // target (CHM layer)
+    bool has_target = false;
+    int64_t m = 0;
+    int md = 2;
+    DevBuf tx, ty, tz;
+    bool grid_ready = false;
+    DevBuf cell_of, counts, cell_start, fill, pts, scan_tmp, mm_part, mm_out;
+    GridView gv{};
+    int64_t ncells = 0;
+    double pivot_x = 0.0, pivot_y = 0.0;
+
+    // source + per-call buffers
+    DevBuf sx, sy, sz, idx, dist, r, key, val, order, sort_tmp, frac_tmp, fit_tmp, bd2, bidx;
+    DevBuf stage, stage2, cx, cy, cz, state_dev;
+    IterState *h_state = nullptr;  // pinned
+
+    // profiling
+    int prof_mask = 0;
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> ev_pool;
+    std::map<std::string, std::pair<int64_t, double>> prof_acc;
+
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+hipEvent_t ev_get(ficp_ctx *c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+}
+
+struct ProfScope {
+    ficp_ctx *c;
+    const char *name;
+    hipEvent_t a = nullptr;
+    ProfScope(ficp_ctx *c_, int cls, const char *n) : c(c_), name(n) {
+        if (c->prof_mask & cls) {
+            a = ev_get(c);
+            hipEventRecord(a, c->stream);
+        }
+    }
+    ~ProfScope() {
+        if (a) {
+            hipEvent_t b = ev_get(c);
+            hipEventRecord(b, c->stream);
+            c->recs.push_back({name, a, b});
+        }
+    }
+};
+
+int set_device(ficp_ctx *c) {
+    HIPCHK(hipSetDevice(c->device));
+    return FICP_OK;
+}
+
+int sync(ficp_ctx *c) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FICP_OK;
+}
+
+// host (n x ld) rows -> device SoA columns (first ncols)
+int upload_rows(ficp_ctx *c, const double *rows, int64_t n, int64_t ld, int ncols, DevBuf &c0,
+                DevBuf &c1, DevBuf *c2) {
+    CHK(c0.ensure(n * 8));
+    CHK(c1.ensure(n * 8));
+    if (c2) CHK(c2->ensure(n * 8));
+    if (n == 0) return FICP_OK;
+    CHK(c->stage.ensure(n * ld * 8));
+    HIPCHK(hipMemcpyAsync(c->stage.p, rows, n * ld * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_deinterleave(c->stage.as<double>(), n, ld, ncols, c0.as<double>(),
+                               c1.as<double>(), c2 ? c2->as<double>() : nullptr, c->stream));
+    return FICP_OK;
+}
+
+int ensure_grid(ficp_ctx *c) {
+    if (c->grid_ready) return FICP_OK;
+    const int64_t m = c->m;
+    ProfScope ps(c, P_GRID, "grid_build");
+    // 1. bounding box
+    CHK(c->mm_part.ensure(1024 * 4 * 8));
+    CHK(c->mm_out.ensure(4 * 8));
+    HIPCHK(launch_minmax2(c->tx.as<double>(), c->ty.as<double>(), m, c->mm_part.as<double>(),
+                          c->mm_out.as<double>(), c->stream));
+    double bb[4];
+    HIPCHK(hipMemcpyAsync(bb, c->mm_out.p, sizeof bb, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    const double x0 = bb[0], x1 = bb[1], y0 = bb[2], y1 = bb[3];
+    if (!(std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1)))
+        return fail(FICP_EINVAL, "target coordinates must be finite");
+    // 2. geometry: about kPerCell stems per cell
+    const double kPerCell = 2.0;
+    const double sxr = x1 - x0, syr = y1 - y0;
+    double h;
+    if (m <= 1 || (sxr <= 0.0 && syr <= 0.0)) h = 1.0;
+    else if (sxr > 0.0 && syr > 0.0) h = sqrt(sxr * syr * kPerCell / (double)m);
+    else h = std::max(sxr, syr) * kPerCell / (double)m;
+    if (!(h > 0.0)) h = 1.0;
+    int64_t gx, gy;
+    for (;;) {
+        gx = (int64_t)floor(sxr / h) + 1;
+        gy = (int64_t)floor(syr / h) + 1;
+        if (gx * gy <= 4 * m + 64 && gx < (1 << 24) && gy < (1 << 24)) break;
+        h *= 1.5;
+    }
+    c->ncells = gx * gy;
+    GridView g{};
+    g.x0 = x0;
+    g.y0 = y0;
+    g.h = h;
+    g.inv_h = 1.0 / h;
+    g.gx = (int)gx;
+    g.gy = (int)gy;
+    g.margin = 64.0 * 2.220446049250313e-16 * (fabs(x0) + fabs(y0) + sxr + syr + h);
+    c->pivot_x = x0 + 0.5 * sxr;
+    c->pivot_y = y0 + 0.5 * syr;
+    // 3. counting sort of the stems by cell
+    CHK(c->cell_of.ensure(m * 4));
+    CHK(c->counts.ensure((c->ncells + 1) * 4));
+    CHK(c->fill.ensure((c->ncells + 1) * 4));
+    CHK(c->cell_start.ensure((c->ncells + 1) * 4));
+    CHK(c->pts.ensure(m * sizeof(TPt)));
+    CHK(c->scan_tmp.ensure(scan_tmp_elems(c->ncells) * 4 + 64));
+    HIPCHK(hipMemsetAsync(c->counts.p, 0, (c->ncells + 1) * 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->fill.p, 0, (c->ncells + 1) * 4, c->stream));
+    HIPCHK(launch_grid_count(c->tx.as<double>(), c->ty.as<double>(), m, g.x0, g.y0, g.inv_h, g.gx,
+                             g.gy, c->cell_of.as<int32_t>(), c->counts.as<int32_t>(), c->stream));
+    HIPCHK(launch_scan_i32(c->counts.as<int32_t>(), c->cell_start.as<int32_t>(), c->ncells,
+                           c->scan_tmp.as<int32_t>(), c->stream));
+    HIPCHK(launch_grid_scatter(c->tx.as<double>(), c->ty.as<double>(),
+                               c->md == 3 ? c->tz.as<double>() : nullptr, m,
+                               c->cell_of.as<int32_t>(), c->cell_start.as<int32_t>(),
+                               c->fill.as<int32_t>(), c->pts.as<TPt>(), c->stream));
+    HIPCHK(launch_grid_sort_cells(c->pts.as<TPt>(), c->cell_start.as<int32_t>(), c->ncells,
+                                  c->stream));
+    g.pts = c->pts.as<TPt>();
+    g.cell_start = c->cell_start.as<int32_t>();
+    c->gv = g;
+    c->grid_ready = true;
+    return FICP_OK;
+}
+
+bool use_grid(ficp_ctx *c, int64_t n) {
+    if (c->nn_mode == 1) return false;
+    if (c->nn_mode == 2) return true;
+    return (double)n * (double)c->m > 4.0e6;
+}
+
+int ensure_work(ficp_ctx *c, int64_t n) {
+    CHK(c->idx.ensure(n * 4));
+    CHK(c->dist.ensure(n * 8));
+    CHK(c->r.ensure(n * 8));
+    CHK(c->key.ensure(n * 8));
+    CHK(c->val.ensure(n * 4));
+    CHK(c->order.ensure(n * 4));
+    CHK(c->sort_tmp.ensure(sort_tmp_bytes(n)));
+    CHK(c->frac_tmp.ensure(frac_tmp_bytes(n)));
+    CHK(c->fit_tmp.ensure(fit_tmp_bytes(n)));
+    CHK(c->state_dev.ensure(sizeof(IterState)));
+    return FICP_OK;
+}
+
+// NN of the device source (sx, sy, sz) against the target; optional pending transform.
+int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
+            bool want_keys) {
+    NNArgs a{};
+    a.sx = sx;
+    a.sy = sy;
+    a.sz = sz;
+    a.n = n;
+    a.T = T;
+    a.skip = nullptr;
+    a.idx = c->idx.as<int32_t>();
+    a.dist = c->dist.as<double>();
+    a.r = c->r.as<double>();
+    a.key = want_keys ? c->key.as<unsigned long long>() : nullptr;
+    a.val = want_keys ? c->val.as<uint32_t>() : nullptr;
+    if (use_grid(c, n)) {
+        CHK(ensure_grid(c));
+        ProfScope ps(c, P_NN, "nn_grid");
+        HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream));
+    } else {
+        const int64_t nch = brute_chunk_count(n, c->m);
+        if (nch > 1) {
+            CHK(c->bd2.ensure(nch * n * 8));
+            CHK(c->bidx.ensure(nch * n * 4));
+        }
+        ProfScope ps(c, P_NN, "nn_brute");
+        HIPCHK(launch_nn_brute(a, c->tx.as<double>(), c->ty.as<double>(),
+                               c->md == 3 ? c->tz.as<double>() : nullptr, c->m, c->md,
+                               c->bd2.as<double>(), c->bidx.as<int32_t>(), c->stream));
+    }
+    return FICP_OK;
+}
+
+int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam) {
+    {
+        ProfScope ps(c, P_SORT, "sort");
+        HIPCHK(launch_sort_pairs(c->key.as<unsigned long long>(), c->val.as<uint32_t>(), n,
+                                 c->order.as<uint32_t>(), c->sort_tmp.p, nullptr, c->stream));
+    }
+    {
+        ProfScope ps(c, P_FRAC, "fraction");
+        HIPCHK(launch_fraction(c->order.as<uint32_t>(), c->r.as<double>(), n, N, lam,
+                               c->frac_tmp.p, c->state_dev.as<IterState>(), nullptr, c->stream));
+    }
+    return FICP_OK;
+}
+
+int read_state(ficp_ctx *c) {
+    HIPCHK(hipMemcpyAsync(c->h_state, c->state_dev.p, sizeof(IterState), hipMemcpyDeviceToHost,
+                          c->stream));
+    return sync(c);
+}
+
+void mat3_mul(const double A[9], const double B[9], double C[9]) {
+    double R[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            R[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    memcpy(C, R, sizeof R);
+}
+
+int trace_call(ficp_ctx *c, ficp_stats *st, int64_t n, double lam) {
+    if (!st) return FICP_OK;
+    const int32_t call = st->n_nn_calls;
+    st->n_nn_calls++;
+    st->k_last = c->h_state->k;
+    if (call >= st->max_trace) return FICP_OK;
+    if (st->trace_k) st->trace_k[call] = c->h_state->k;
+    if (st->trace_frmsd) st->trace_frmsd[call] = c->h_state->frmsd;
+    if (st->trace_lambda) st->trace_lambda[call] = lam;
+    if (st->trace_idx && n > 0) {
+        HIPCHK(hipMemcpyAsync(st->trace_idx + (int64_t)call * n, c->idx.p, n * 4,
+                              hipMemcpyDeviceToHost, c->stream));
+        CHK(sync(c));
+    }
+    return FICP_OK;
+}
+
+// the device-resident ICP: stages of ficp.py:122-147
+int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, int32_t nstages,
+             const double *lambdas, double threshold, int32_t max_iter, int32_t allow_refl,
+             ficp_stats *st) {
+    if (st) {
+        st->n_nn_calls = 0;
+        st->n_fits = 0;
+        st->iters[0] = st->iters[1] = 0;
+        st->k_last = 0;
+        st->frmsd_last[0] = st->frmsd_last[1] = INFINITY;
+        for (int e = 0; e < 9; ++e) st->T_total[e] = (e % 4 == 0) ? 1.0 : 0.0;
+        st->gpu_ms = 0.0;
+    }
+    if (n == 0 || c->m == 0) return FICP_OK;  // ficp.py:66-68 + 125-126: nothing moves
+    if (n > 0x7fffffff) return fail(FICP_EINVAL, "n too large");
+    CHK(ensure_work(c, n));
+    IterState *dst = c->state_dev.as<IterState>();
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    for (int s = 0; s < nstages; ++s) {
+        const double lam = lambdas[s];
+        CHK(nn_call(c, sx, sy, sz, n, nullptr, true));
+        CHK(sort_and_select(c, n, n, lam));
+        CHK(read_state(c));
+        CHK(trace_call(c, st, n, lam));
+        if (c->h_state->k == 0) continue;
+        double cur = c->h_state->frmsd;
+        if (st) st->frmsd_last[s < 2 ? s : 1] = cur;
+        int it = 0;
+        while (it < max_iter) {
+            {
+                ProfScope ps(c, P_FIT, "fit");
+                HIPCHK(launch_fit(c->order.as<uint32_t>(), sx, sy, c->idx.as<int32_t>(),
+                                  c->tx.as<double>(), c->ty.as<double>(), n, c->pivot_x,
+                                  c->pivot_y, allow_refl, c->fit_tmp.p, dst, nullptr, c->stream));
+            }
+            CHK(nn_call(c, sx, sy, sz, n, dst->T, true));
+            CHK(sort_and_select(c, n, n, lam));
+            CHK(read_state(c));
+            if (st) {
+                if (st->trace_T && st->n_fits < st->max_trace)
+                    memcpy(st->trace_T + 9 * st->n_fits, c->h_state->T, 9 * sizeof(double));
+                st->n_fits++;
+                mat3_mul(c->h_state->T, st->T_total, st->T_total);
+            }
+            CHK(trace_call(c, st, n, lam));
+            const double nw = c->h_state->frmsd;
+            if (st) st->frmsd_last[s < 2 ? s : 1] = nw;
+            if (cur - nw <= threshold) break;  // ficp.py:142 (transform already applied)
+            cur = nw;
+            ++it;
+        }
+        if (st && s < 2) st->iters[s] = it;
+    }
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    CHK(sync(c));
+    if (st) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        st->gpu_ms = ms;
+    }
+    return FICP_OK;
+}
+
+int check_ctx(ficp_ctx *c) {
+    if (!c) return fail(FICP_EINVAL, "null context");
+    return set_device(c);
+}
+
+int check_md(int32_t md) {
+    if (md != 2 && md != 3) return fail(FICP_EINVAL, "md must be 2 or 3 (got %d)", md);
+    return FICP_OK;
+}
+
+}  // namespace
+
+// ===================================================================== C ABI
+extern "C" {
+
+int ficp_version(void) { return 100; }
+
+const char *ficp_last_error(void) { return g_err.c_str(); }
+
+int ficp_device_count(int *count) {
+    if (!count) return fail(FICP_EINVAL, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(FICP_ENODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return FICP_OK;
+}
+
+int ficp_create(int device, ficp_ctx **out) {
+    if (!out) return fail(FICP_EINVAL, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(FICP_ENODEV, "no HIP device");
+    if (device < 0 || device >= n) return fail(FICP_EINVAL, "device %d out of range [0,%d)", device, n);
+    ficp_ctx *c = new ficp_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_state, sizeof(IterState), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(FICP_EHIP, "context setup: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return FICP_OK;
+}
+
+void ficp_destroy(ficp_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->tx, &c->ty, &c->tz, &c->cell_of, &c->counts, &c->cell_start,
+                      &c->fill, &c->pts, &c->scan_tmp, &c->mm_part, &c->mm_out, &c->sx,
+                      &c->sy, &c->sz, &c->idx, &c->dist, &c->r, &c->key, &c->val, &c->order,
+                      &c->sort_tmp, &c->frac_tmp, &c->fit_tmp, &c->bd2, &c->bidx, &c->stage,
+                      &c->stage2, &c->cx, &c->cy, &c->cz, &c->state_dev};
+    for (DevBuf *b : bufs) b->release();
+    for (auto &r : c->recs) {
+        hipEventDestroy(r.a);
+        hipEventDestroy(r.b);
+    }
+    for (auto e : c->ev_pool) hipEventDestroy(e);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->h_state) hipHostFree(c->h_state);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int ficp_set_nn_mode(ficp_ctx *c, int32_t mode) {
+    if (!c) return fail(FICP_EINVAL, "null context");
+    if (mode < 0 || mode > 2) return fail(FICP_EINVAL, "nn mode must be 0, 1 or 2");
+    c->nn_mode = mode;
+    return FICP_OK;
+}
+
+int ficp_profile_enable(ficp_ctx *c, int32_t mask) {
+    if (!c) return fail(FICP_EINVAL, "null context");
+    c->prof_mask = mask;
+    return FICP_OK;
+}
+
+int ficp_profile_report(ficp_ctx *c, char *buf, int64_t buflen) {
+    CHK(check_ctx(c));
+    CHK(sync(c));
+    for (auto &r : c->recs) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, r.a, r.b);
+        auto &acc = c->prof_acc[r.name];
+        acc.first += 1;
+        acc.second += ms;
+        c->ev_pool.push_back(r.a);
+        c->ev_pool.push_back(r.b);
+    }
+    c->recs.clear();
+    std::string s = "{";
+    bool first = true;
+    for (auto &kv : c->prof_acc) {
+        char item[256];
+        snprintf(item, sizeof item, "%s\"%s\": {\"count\": %lld, \"ms\": %.6f}", first ? "" : ", ",
+                 kv.first.c_str(), (long long)kv.second.first, kv.second.second);
+        s += item;
+        first = false;
+    }
+    s += "}";
+    c->prof_acc.clear();
+    if (!buf || buflen <= 0) return fail(FICP_EINVAL, "null buffer");
+    if ((int64_t)s.size() + 1 > buflen) return fail(FICP_EINVAL, "buffer too small (%zu)", s.size() + 1);
+    memcpy(buf, s.c_str(), s.size() + 1);
+    return FICP_OK;
+}
+
+int ficp_set_target(ficp_ctx *c, const double *tgt, int64_t m, int64_t ld, int32_t md) {
+    CHK(check_ctx(c));
+    CHK(check_md(md));
+    if (m < 0 || (m > 0 && (!tgt || ld < md))) return fail(FICP_EINVAL, "bad target shape");
+    if (m > 0x7fffffff) return fail(FICP_EINVAL, "target too large");
+    c->has_target = true;
+    c->grid_ready = false;
+    c->m = m;
+    c->md = md;
+    CHK(upload_rows(c, tgt, m, ld, md, c->tx, c->ty, &c->tz));
+    return sync(c);
+}
+
+int ficp_set_target_device(ficp_ctx *c, const double *x, const double *y, const double *z,
+                           int64_t m, int32_t md) {
+    CHK(check_ctx(c));
+    CHK(check_md(md));
+    if (m < 0 || (m > 0 && (!x || !y || (md == 3 && !z)))) return fail(FICP_EINVAL, "bad target");
+    if (m > 0x7fffffff) return fail(FICP_EINVAL, "target too large");
+    c->has_target = true;
+    c->grid_ready = false;
+    c->m = m;
+    c->md = md;
+    CHK(c->tx.ensure(m * 8));
+    CHK(c->ty.ensure(m * 8));
+    CHK(c->tz.ensure(m * 8));
+    if (m > 0) {
+        HIPCHK(hipMemcpyAsync(c->tx.p, x, m * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->ty.p, y, m * 8, hipMemcpyDeviceToDevice, c->stream));
+        if (md == 3) HIPCHK(hipMemcpyAsync(c->tz.p, z, m * 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+    return FICP_OK;  // stream-ordered; the grid is built on first use
+}
+
+int ficp_nn(ficp_ctx *c, const double *src, int64_t n, int64_t ld, int32_t *idx, double *dist) {
+    CHK(check_ctx(c));
+    if (!c->has_target) return fail(FICP_ESTATE, "no target set");
+    if (n < 0 || (n > 0 && (!src || !idx || !dist || ld < c->md))) return fail(FICP_EINVAL, "bad source");
+    if (n == 0 || c->m == 0) return FICP_OK;
+    CHK(upload_rows(c, src, n, ld, c->md, c->sx, c->sy, &c->sz));
+    CHK(ensure_work(c, n));
+    CHK(nn_call(c, c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(), n, nullptr, false));
+    HIPCHK(hipMemcpyAsync(idx, c->idx.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(dist, c->dist.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    return sync(c);
+}
+
+int ficp_optimal_fraction(ficp_ctx *c, const double *src, int64_t lds, const double *corr,
+                          int64_t ldc, const double *dist, int64_t n, int64_t n_source,
+                          int32_t md, double lambda_val, double *frac, int64_t *k) {
+    CHK(check_ctx(c));
+    CHK(check_md(md));
+    if (!frac || !k) return fail(FICP_EINVAL, "null output");
+    *frac = 0.0;
+    *k = 0;
+    if (n_source == 0 || n == 0) return FICP_OK;  // ficp.py:76-77
+    if (n < 0 || n_source < 0 || !src || !corr || !dist || lds < md || ldc < md)
+        return fail(FICP_EINVAL, "bad arguments");
+    if (n > 0x7fffffff) return fail(FICP_EINVAL, "n too large");
+    CHK(ensure_work(c, n));
+    CHK(upload_rows(c, src, n, lds, md, c->sx, c->sy, &c->sz));
+    CHK(upload_rows(c, corr, n, ldc, md, c->cx, c->cy, &c->cz));
+    CHK(c->stage2.ensure(n * 8));
+    HIPCHK(hipMemcpyAsync(c->stage2.p, dist, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_residuals(c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(),
+                            c->cx.as<double>(), c->cy.as<double>(), c->cz.as<double>(), n, md,
+                            c->r.as<double>(), c->stream));
+    HIPCHK(launch_keys_from_doubles(c->stage2.as<double>(), n, c->key.as<unsigned long long>(),
+                                    c->val.as<uint32_t>(), c->stream));
+    CHK(sort_and_select(c, n, n_source, lambda_val));
+    CHK(read_state(c));
+    *k = c->h_state->k;
+    *frac = c->h_state->frac;
+    return FICP_OK;
+}
+
+int ficp_frmsd(ficp_ctx *c, const double *src, int64_t lds, const double *corr, int64_t ldc,
+               int64_t rows, int64_t num_elements, int32_t md, double fraction,
+               double lambda_val, double *out) {
+    CHK(check_ctx(c));
+    CHK(check_md(md));
+    if (!out) return fail(FICP_EINVAL, "null output");
+    if (num_elements == 0) {  // ficp.py:56-57
+        *out = INFINITY;
+        return FICP_OK;
+    }
+    const int64_t k = rows;
+    if (k < 0 || (k > 0 && (!src || !corr || lds < md || ldc < md)))
+        return fail(FICP_EINVAL, "bad arguments");
+    CHK(upload_rows(c, src, k, lds, md, c->sx, c->sy, &c->sz));
+    CHK(upload_rows(c, corr, k, ldc, md, c->cx, c->cy, &c->cz));
+    CHK(c->fit_tmp.ensure(std::max<int64_t>(fit_tmp_bytes(k), 4096)));
+    CHK(c->stage2.ensure(64));
+    HIPCHK(launch_sum_sq_diff(c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(),
+                              c->cx.as<double>(), c->cy.as<double>(), c->cz.as<double>(), k, md,
+                              c->fit_tmp.p, c->stage2.as<double>(), c->stream));
+    double S = 0.0;
+    HIPCHK(hipMemcpyAsync(&S, c->stage2.p, 8, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    *out = (1.0 / pow(fraction, lambda_val)) * sqrt(S / (double)num_elements);  // ficp.py:59-60
+    return FICP_OK;
+}
+
+int ficp_argsort(ficp_ctx *c, const double *d, int64_t n, int64_t *order) {
+    CHK(check_ctx(c));
+    if (n < 0 || (n > 0 && (!d || !order))) return fail(FICP_EINVAL, "bad arguments");
+    if (n == 0) return FICP_OK;
+    if (n > 0x7fffffff) return fail(FICP_EINVAL, "n too large");
+    CHK(ensure_work(c, n));
+    CHK(c->stage2.ensure(n * 8));
+    HIPCHK(hipMemcpyAsync(c->stage2.p, d, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_keys_from_doubles(c->stage2.as<double>(), n, c->key.as<unsigned long long>(),
+                                    c->val.as<uint32_t>(), c->stream));
+    HIPCHK(launch_sort_pairs(c->key.as<unsigned long long>(), c->val.as<uint32_t>(), n,
+                             c->order.as<uint32_t>(), c->sort_tmp.p, nullptr, c->stream));
+    std::vector<uint32_t> tmp((size_t)n);
+    HIPCHK(hipMemcpyAsync(tmp.data(), c->order.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    for (int64_t i = 0; i < n; ++i) order[i] = tmp[(size_t)i];
+    return FICP_OK;
+}
+
+int ficp_fit_rigid2d(ficp_ctx *c, const double *src, int64_t lds, const double *tgt,
+                     int64_t ldt, int64_t k, int32_t allow_reflection, double T[9]) {
+    CHK(check_ctx(c));
+    if (!T || k <= 0 || !src || !tgt || lds < 2 || ldt < 2)
+        return fail(FICP_EINVAL, "bad arguments (k must be >= 1)");
+    CHK(upload_rows(c, src, k, lds, 2, c->sx, c->sy, nullptr));
+    CHK(upload_rows(c, tgt, k, ldt, 2, c->cx, c->cy, nullptr));
+    CHK(c->fit_tmp.ensure(fit_tmp_bytes(k)));
+    CHK(c->state_dev.ensure(sizeof(IterState)));
+    // pivot: the first source point keeps the sums well conditioned for any offset
+    double p[2] = {0.0, 0.0};
+    HIPCHK(hipMemcpyAsync(p, c->stage.p, 16, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    HIPCHK(launch_fit(nullptr, c->sx.as<double>(), c->sy.as<double>(), nullptr,
+                      c->cx.as<double>(), c->cy.as<double>(), k, p[0], p[1], allow_reflection,
+                      c->fit_tmp.p, c->state_dev.as<IterState>(), nullptr, c->stream));
+    CHK(read_state(c));
+    memcpy(T, c->h_state->T, 9 * sizeof(double));
+    return FICP_OK;
+}
+
+int ficp_apply_xy(ficp_ctx *c, const double *pts, int64_t n, int64_t ld, const double T[9],
+                  double *out_xy) {
+    CHK(check_ctx(c));
+    if (n < 0 || (n > 0 && (!pts || !out_xy || ld < 2)) || !T) return fail(FICP_EINVAL, "bad arguments");
+    if (n == 0) return FICP_OK;
+    CHK(upload_rows(c, pts, n, ld, 2, c->sx, c->sy, nullptr));
+    CHK(c->stage2.ensure(std::max<int64_t>(n * 16, 128)));
+    CHK(c->state_dev.ensure(sizeof(IterState)));
+    double *dT = c->state_dev.as<IterState>()->T;
+    HIPCHK(hipMemcpyAsync(dT, T, 9 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_apply_xy(c->sx.as<double>(), c->sy.as<double>(), n, dT, c->stream));
+    HIPCHK(launch_interleave_xy(c->sx.as<double>(), c->sy.as<double>(), n, c->stage2.as<double>(),
+                                c->stream));
+    HIPCHK(hipMemcpyAsync(out_xy, c->stage2.p, n * 16, hipMemcpyDeviceToHost, c->stream));
+    return sync(c);
+}
+
+int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
+             const double *lambdas, double threshold, int32_t max_iterations,
+             int32_t allow_reflection, ficp_stats *stats) {
+    CHK(check_ctx(c));
+    if (!c->has_target) return fail(FICP_ESTATE, "no target set");
+    if (n < 0 || (n > 0 && (!src || ld < c->md)) || nstages < 0 || (nstages > 0 && !lambdas))
+        return fail(FICP_EINVAL, "bad arguments");
+    if (n == 0 || c->m == 0) return run_core(c, nullptr, nullptr, nullptr, 0, nstages, lambdas,
+                                             threshold, max_iterations, allow_reflection, stats);
+    CHK(upload_rows(c, src, n, ld, c->md, c->sx, c->sy, &c->sz));
+    CHK(run_core(c, c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(), n, nstages,
+                 lambdas, threshold, max_iterations, allow_reflection, stats));
+    CHK(c->stage2.ensure(n * 16));
+    HIPCHK(launch_interleave_xy(c->sx.as<double>(), c->sy.as<double>(), n, c->stage2.as<double>(),
+                                c->stream));
+    std::vector<double> xy((size_t)n * 2);
+    HIPCHK(hipMemcpyAsync(xy.data(), c->stage2.p, n * 16, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    for (int64_t i = 0; i < n; ++i) {  // columns 0,1 only; every other column untouched
+        src[i * ld] = xy[2 * i];
+        src[i * ld + 1] = xy[2 * i + 1];
+    }
+    return FICP_OK;
+}
+
+int ficp_run_device(ficp_ctx *c, double *x, double *y, const double *z, int64_t n,
+                    int32_t nstages, const double *lambdas, double threshold,
+                    int32_t max_iterations, int32_t allow_reflection, ficp_stats *stats) {
+    CHK(check_ctx(c));
+    if (!c->has_target) return fail(FICP_ESTATE, "no target set");
+    if (n < 0 || (n > 0 && (!x || !y || (c->md == 3 && !z))) || nstages < 0 ||
+        (nstages > 0 && !lambdas))
+        return fail(FICP_EINVAL, "bad arguments");
+    return run_core(c, x, y, z, n, nstages, lambdas, threshold, max_iterations, allow_reflection,
+                    stats);
+}
+
+int ficp_dev_alloc(ficp_ctx *c, int64_t bytes, void **ptr) {
+    CHK(check_ctx(c));
+    if (!ptr || bytes < 0) return fail(FICP_EINVAL, "bad arguments");
+    HIPCHK(hipMalloc(ptr, std::max<int64_t>(bytes, 1)));
+    return FICP_OK;
+}
+
+int ficp_dev_free(ficp_ctx *c, void *ptr) {
+    CHK(check_ctx(c));
+    HIPCHK(hipFree(ptr));
+    return FICP_OK;
+}
+
+int ficp_memcpy_h2d(ficp_ctx *c, void *dst, const void *src, int64_t bytes) {
+    CHK(check_ctx(c));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return sync(c);
+}
+
+int ficp_memcpy_d2h(ficp_ctx *c, void *dst, const void *src, int64_t bytes) {
+    CHK(check_ctx(c));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return sync(c);
+}
+
+int ficp_memcpy_d2d(ficp_ctx *c, void *dst, const void *src, int64_t bytes) {
+    CHK(check_ctx(c));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return FICP_OK;
+}
+
+int ficp_synchronize(ficp_ctx *c) {
+    CHK(check_ctx(c));
+    return sync(c);
+}
+
+}  // extern "C"

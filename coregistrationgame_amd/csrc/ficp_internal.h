@@ -1,0 +1,121 @@
+// ficp_internal.h -- shared types and kernel launchers of libficp (gfx950 only).
+//
+// Device data layout:
+//   source  : SoA fp64 x[n], y[n], z[n] (z only when md == 3); x,y updated in place
+//   target  : SoA fp64 tx[m], ty[m], tz[m] (original order, for corr gathers) and a
+//             uniform XY grid: cell_start[ncells+1] + TPt pts[m] (cell-sorted AoS,
+//             32 B per stem = two dwordx4 loads per candidate)
+//   per call: idx[n] int32, dist[n] fp64, r[n] fp64 (= d^2), key[n] u64 (ordered
+//             bits of dist), sorted val[n] (source index in selection order)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ficp {
+
+constexpr int kWave = 64;
+
+struct alignas(32) TPt {
+    double x, y, z;
+    long long idx;
+};
+
+// Everything an NN kernel needs to search the static CHM grid.
+struct GridView {
+    const TPt *pts;
+    const int32_t *cell_start;  // ncells + 1
+    double x0, y0, h, inv_h;
+    double margin;              // conservative slack for the ring lower bound (m)
+    int gx, gy;
+};
+
+// Per-launch NN arguments.
+struct NNArgs {
+    double *sx;                 // source x (updated in place when T != nullptr)
+    double *sy;
+    const double *sz;
+    int64_t n;
+    const double *T;            // pending 3x3 transform to apply before the query, or null
+    const int *skip;            // device flag: kernel is a no-op when *skip != 0 (nullable)
+    int32_t *idx;               // out
+    double *dist;               // out (nullable)
+    double *r;                  // out: d^2 (nullable)
+    unsigned long long *key;    // out: order-preserving bits of dist (nullable)
+    uint32_t *val;              // out: identity payload for the sort (nullable)
+};
+
+// Device-resident state of one ICP stage (written by kernels, read back per iteration).
+struct alignas(16) IterState {
+    double T[9];           // last fit
+    double pad0;
+    double frac;           // last fraction
+    double frmsd;          // FRMSD at k
+    long long k;           // selected k
+    long long n_src;       // N
+    double csx, csy, ctx, cty;  // centroids of the last fit (relative to the pivot)
+    double H[4];
+    int done;              // set by the fit/scan kernels when nothing is left to do
+    int pad1;
+};
+
+// ----------------------------------------------------------------- launchers
+// grid build (k_grid_nn.hip)
+hipError_t launch_minmax2(const double *x, const double *y, int64_t m, double *partials,
+                          double *out4, hipStream_t s);
+hipError_t launch_grid_count(const double *x, const double *y, int64_t m, double x0, double y0,
+                             double inv_h, int gx, int gy, int32_t *cell_of, int32_t *counts,
+                             hipStream_t s);
+hipError_t launch_grid_scatter(const double *x, const double *y, const double *z, int64_t m,
+                               const int32_t *cell_of, const int32_t *cell_start,
+                               int32_t *fill, TPt *pts, hipStream_t s);
+hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t ncells,
+                                  hipStream_t s);
+hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s);
+int64_t brute_chunk_count(int64_t n, int64_t m);  // target chunks of the brute kernel
+hipError_t launch_nn_brute(const NNArgs &a, const double *tx, const double *ty,
+                           const double *tz, int64_t m, int md, double *part_d2,
+                           int32_t *part_idx, hipStream_t s);
+hipError_t launch_deinterleave(const double *rows, int64_t n, int64_t ld, int ncols,
+                               double *c0, double *c1, double *c2, hipStream_t s);
+hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, double *out_xy,
+                                hipStream_t s);
+
+// scans / sort (k_sort.hip)
+// Exclusive scan of n int32 (out may alias in); out[n] = total. tmp >= scan_tmp_elems(n).
+int64_t scan_tmp_elems(int64_t n);
+hipError_t launch_scan_i32(const int32_t *in, int32_t *out, int64_t n, int32_t *tmp,
+                           hipStream_t s);
+// Stable sort of (key, val) pairs by 64-bit key.  Sorts by the top 32 key bits with a
+// stable LSD radix sort, then orders every run of equal top bits by the full key.
+// Outputs val_out (and key_out).  Scratch sized by sort_tmp_bytes(n).
+int64_t sort_tmp_bytes(int64_t n);
+hipError_t launch_sort_pairs(const unsigned long long *key, const uint32_t *val_in, int64_t n,
+                             uint32_t *val_out, void *tmp, const int *skip, hipStream_t s);
+hipError_t launch_keys_from_doubles(const double *d, int64_t n, unsigned long long *key,
+                                    uint32_t *val, hipStream_t s);
+
+// selection + fit + apply (k_select_fit.hip)
+int64_t frac_tmp_bytes(int64_t n);
+// r_i = sum_md (src_i - corr_i)^2 on SoA inputs
+hipError_t launch_residuals(const double *sx, const double *sy, const double *sz,
+                            const double *cx, const double *cy, const double *cz, int64_t n,
+                            int md, double *r, hipStream_t s);
+// argmin_k FRMSD(k) over the sorted order -> st->k, st->frac, st->frmsd
+hipError_t launch_fraction(const uint32_t *order, const double *r, int64_t n, int64_t n_src,
+                           double lambda_val, void *tmp, IterState *st, const int *skip,
+                           hipStream_t s);
+// fit on the first st->k entries of `order` (or the first kfixed rows when order == null):
+// src point i = (sx[i], sy[i]), its partner = (tx[j], ty[j]) with j = idx ? idx[i] : i.
+int64_t fit_tmp_bytes(int64_t n);
+hipError_t launch_fit(const uint32_t *order, const double *sx, const double *sy,
+                      const int32_t *idx, const double *tx, const double *ty, int64_t kfixed,
+                      double px, double py, int allow_reflection, void *tmp, IterState *st,
+                      const int *skip, hipStream_t s);
+hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hipStream_t s);
+hipError_t launch_sum_sq_diff(const double *sx, const double *sy, const double *sz,
+                              const double *cx, const double *cy, const double *cz, int64_t k,
+                              int md, void *tmp, double *out, hipStream_t s);
+hipError_t launch_gather_xy(const int32_t *idx, const double *tx, const double *ty, int64_t n,
+                            double *ox, double *oy, hipStream_t s);
+
+}  // namespace ficp

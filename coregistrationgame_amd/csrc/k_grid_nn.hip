@@ -1,0 +1,468 @@
+// k_grid_nn.hip -- exact 1-NN correspondence search of the tree layer against the
+// static CHM layer (replaces cKDTree(target).query(source, k=1), ficp.py:65-71).
+//
+// Parity rule (probe-verified against cKDTree): squared distance
+// d2 = ((0 + dx*dx) + dy*dy) + dz*dz in fp64 with NO FMA contraction (this TU is built
+// with -ffp-contract=off; `0 + x` is the identity for x >= 0), argmin over d2, exact ties
+// to the lowest target index, dist = sqrt(d2).
+//
+// Two exact searches:
+//  * k_nn_grid  -- the CHM layer is binned once into a uniform XY grid (cell-sorted AoS,
+//    32 B per stem); a query scans square rings of cells around its own cell until a
+//    conservative lower bound on the distance to everything outside the scanned block
+//    exceeds the best d2.  Work per query is O(stems near the query), HBM/L2 bound.
+//  * k_nn_brute -- LDS-tiled all-pairs scan (target tiles of 256 stems staged in LDS and
+//    read as broadcasts, QPT queries per lane held in registers), fp64-VALU bound; used
+//    for small layers and as an independent cross-check of the grid kernel.
+#include "ficp_internal.h"
+
+#include <math.h>
+
+#include <algorithm>
+
+namespace ficp {
+
+namespace {
+
+__device__ __forceinline__ unsigned long long ordkey(double v) {
+    unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+
+__device__ __forceinline__ int cell_coord(double v, double v0, double inv_h, int g) {
+    double f = (v - v0) * inv_h;
+    if (!(f >= 0.0)) return 0;           // also catches NaN
+    if (f >= (double)(g - 1)) return g - 1;
+    return (int)f;
+}
+
+template <int MD>
+__device__ __forceinline__ double sq_dist(double qx, double qy, double qz, double px, double py,
+                                          double pz) {
+    double dx = qx - px;
+    double dy = qy - py;
+    double s = dx * dx;  // == 0 + dx*dx exactly
+    s = s + dy * dy;
+    if (MD == 3) {
+        double dz = qz - pz;
+        s = s + dz * dz;
+    }
+    return s;
+}
+
+template <int MD>
+__device__ __forceinline__ void scan_pts(const TPt *__restrict__ pts, int p0, int p1, double qx,
+                                         double qy, double qz, double &best, int &bi) {
+    for (int p = p0; p < p1; ++p) {
+        const double4 a = *reinterpret_cast<const double4 *>(pts + p);
+        double s = sq_dist<MD>(qx, qy, qz, a.x, a.y, a.z);
+        int id = (int)__double_as_longlong(a.w);
+        bool b = (s < best) | ((s == best) & (id < bi));
+        best = b ? s : best;
+        bi = b ? id : bi;
+    }
+}
+
+template <int MD>
+__device__ __forceinline__ void grid_query(const GridView &g, double qx, double qy, double qz,
+                                           double &best, int &bi) {
+    const int cx = cell_coord(qx, g.x0, g.inv_h, g.gx);
+    const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
+    const double mq = g.margin + 1e-15 * (fabs(qx) + fabs(qy));
+    for (int r = 0;; ++r) {
+        const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
+        const int ylo = max(ya, 0), yhi = min(yb, g.gy - 1);
+        const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);
+        for (int yy = ylo; yy <= yhi; ++yy) {
+            const double by0 = g.y0 + (double)yy * g.h;
+            const double by1 = by0 + g.h;
+            const double gyap = fmax(fmax(by0 - qy, qy - by1), 0.0) - mq;
+            if (gyap > 0.0 && gyap * gyap > best) continue;
+            const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+            if (yy == ya || yy == yb) {
+                scan_pts<MD>(g.pts, row[xlo], row[xhi + 1], qx, qy, qz, best, bi);
+            } else {
+                if (xa >= 0) {
+                    const double gx0 = qx - (g.x0 + (double)(xa + 1) * g.h) - mq;
+                    if (!(gx0 > 0.0 && gx0 * gx0 > best))
+                        scan_pts<MD>(g.pts, row[xa], row[xa + 1], qx, qy, qz, best, bi);
+                }
+                if (xb < g.gx) {
+                    const double gx1 = (g.x0 + (double)xb * g.h) - qx - mq;
+                    if (!(gx1 > 0.0 && gx1 * gx1 > best))
+                        scan_pts<MD>(g.pts, row[xb], row[xb + 1], qx, qy, qz, best, bi);
+                }
+            }
+        }
+        // lower bound on the distance from q to any cell outside the scanned block
+        double lb = INFINITY;
+        if (xa > 0) lb = fmin(lb, qx - (g.x0 + (double)xa * g.h));
+        if (xb < g.gx - 1) lb = fmin(lb, (g.x0 + (double)(xb + 1) * g.h) - qx);
+        if (ya > 0) lb = fmin(lb, qy - (g.y0 + (double)ya * g.h));
+        if (yb < g.gy - 1) lb = fmin(lb, (g.y0 + (double)(yb + 1) * g.h) - qy);
+        if (lb == INFINITY) break;  // the block already covers the whole grid
+        lb -= mq;
+        if (lb > 0.0 && lb * lb > best) break;
+    }
+}
+
+__device__ __forceinline__ void apply_T(const double *__restrict__ T, double &x, double &y) {
+    // numpy's ([x, y, 1] @ T.T)[:, :2] through OpenBLAS dgemm (ficp.py:117):
+    // fma(y, T01, x*T00) + T02 -- pinned bit-exactly by tests/golden/apply.npz
+    const double nx = __fma_rn(y, T[1], x * T[0]) + T[2];
+    const double ny = __fma_rn(y, T[4], x * T[3]) + T[5];
+    x = nx;
+    y = ny;
+}
+
+__device__ __forceinline__ void write_out(const NNArgs &a, int64_t i, double best, int bi) {
+    a.idx[i] = bi;
+    const double d = sqrt(best);
+    if (a.dist) a.dist[i] = d;
+    if (a.r) a.r[i] = best;
+    if (a.key) a.key[i] = ordkey(d);
+    if (a.val) a.val[i] = (uint32_t)i;
+}
+
+template <int MD, bool APPLY>
+__global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
+    if (a.skip && *a.skip) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    double qx = a.sx[i], qy = a.sy[i];
+    if (APPLY) {
+        apply_T(a.T, qx, qy);
+        a.sx[i] = qx;
+        a.sy[i] = qy;
+    }
+    const double qz = (MD == 3) ? a.sz[i] : 0.0;
+    double best = INFINITY;
+    int bi = 0x7fffffff;
+    grid_query<MD>(g, qx, qy, qz, best, bi);
+    write_out(a, i, best, bi);
+}
+
+constexpr int kTile = 256;
+
+// blockIdx.y = target chunk; one chunk -> final outputs, several -> partials then merge
+template <int MD, int QPT>
+__global__ __launch_bounds__(256) void k_nn_brute(NNArgs a, const double *__restrict__ tx,
+                                                  const double *__restrict__ ty,
+                                                  const double *__restrict__ tz, int64_t m,
+                                                  int64_t chunk, double *part_d2,
+                                                  int32_t *part_idx) {
+    if (a.skip && *a.skip) return;
+    __shared__ double s_x[kTile], s_y[kTile], s_z[kTile];
+    const int64_t base = (int64_t)blockIdx.x * (256 * QPT) + threadIdx.x;
+    double qx[QPT], qy[QPT], qz[QPT], best[QPT];
+    int bi[QPT];
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+        const int64_t i = base + q * 256;
+        const bool ok = i < a.n;
+        qx[q] = ok ? a.sx[i] : 0.0;
+        qy[q] = ok ? a.sy[i] : 0.0;
+        qz[q] = (ok && MD == 3) ? a.sz[i] : 0.0;
+        best[q] = INFINITY;
+        bi[q] = 0x7fffffff;
+    }
+    const int64_t j0 = (int64_t)blockIdx.y * chunk;
+    const int64_t j1 = min(m, j0 + chunk);
+    for (int64_t t0 = j0; t0 < j1; t0 += kTile) {
+        const int cnt = (int)min((int64_t)kTile, j1 - t0);
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            s_x[threadIdx.x] = tx[t0 + threadIdx.x];
+            s_y[threadIdx.x] = ty[t0 + threadIdx.x];
+            if (MD == 3) s_z[threadIdx.x] = tz[t0 + threadIdx.x];
+        }
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+            const double px = s_x[j], py = s_y[j];
+            const double pz = (MD == 3) ? s_z[j] : 0.0;
+            const int id = (int)(t0 + j);
+#pragma unroll
+            for (int q = 0; q < QPT; ++q) {
+                const double s = sq_dist<MD>(qx[q], qy[q], qz[q], px, py, pz);
+                const bool b = s < best[q];  // ascending j: strict < keeps the lowest index
+                best[q] = b ? s : best[q];
+                bi[q] = b ? id : bi[q];
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+        const int64_t i = base + q * 256;
+        if (i >= a.n) continue;
+        if (gridDim.y == 1) {
+            write_out(a, i, best[q], bi[q]);
+        } else {
+            part_d2[(int64_t)blockIdx.y * a.n + i] = best[q];
+            part_idx[(int64_t)blockIdx.y * a.n + i] = bi[q];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_nn_merge(NNArgs a, int nchunks, const double *part_d2,
+                                                  const int32_t *part_idx) {
+    if (a.skip && *a.skip) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    double best = INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = 0; c < nchunks; ++c) {  // chunks ascend in index: strict < keeps the lowest
+        const double s = part_d2[(int64_t)c * a.n + i];
+        const int id = part_idx[(int64_t)c * a.n + i];
+        if (s < best || (s == best && id < bi)) {
+            best = s;
+            bi = id;
+        }
+    }
+    write_out(a, i, best, bi);
+}
+
+__global__ __launch_bounds__(256) void k_apply_inplace(double *x, double *y, int64_t n,
+                                                       const double *T, const int *skip) {
+    if (skip && *skip) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double qx = x[i], qy = y[i];
+    apply_T(T, qx, qy);
+    x[i] = qx;
+    y[i] = qy;
+}
+
+// ---------------------------------------------------------------- grid build
+__global__ __launch_bounds__(256) void k_minmax2_partial(const double *x, const double *y,
+                                                         int64_t m, double *partials) {
+    __shared__ double s[4][256];
+    double a0 = INFINITY, a1 = -INFINITY, b0 = INFINITY, b1 = -INFINITY;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (int64_t)gridDim.x * 256) {
+        const double vx = x[i], vy = y[i];
+        a0 = fmin(a0, vx);
+        a1 = fmax(a1, vx);
+        b0 = fmin(b0, vy);
+        b1 = fmax(b1, vy);
+    }
+    s[0][threadIdx.x] = a0;
+    s[1][threadIdx.x] = a1;
+    s[2][threadIdx.x] = b0;
+    s[3][threadIdx.x] = b1;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            s[0][threadIdx.x] = fmin(s[0][threadIdx.x], s[0][threadIdx.x + w]);
+            s[1][threadIdx.x] = fmax(s[1][threadIdx.x], s[1][threadIdx.x + w]);
+            s[2][threadIdx.x] = fmin(s[2][threadIdx.x], s[2][threadIdx.x + w]);
+            s[3][threadIdx.x] = fmax(s[3][threadIdx.x], s[3][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 4) partials[blockIdx.x * 4 + threadIdx.x] = s[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void k_minmax2_final(const double *partials, int nb, double *out4) {
+    __shared__ double s[4][256];
+    double a0 = INFINITY, a1 = -INFINITY, b0 = INFINITY, b1 = -INFINITY;
+    for (int b = threadIdx.x; b < nb; b += 256) {
+        a0 = fmin(a0, partials[4 * b]);
+        a1 = fmax(a1, partials[4 * b + 1]);
+        b0 = fmin(b0, partials[4 * b + 2]);
+        b1 = fmax(b1, partials[4 * b + 3]);
+    }
+    s[0][threadIdx.x] = a0;
+    s[1][threadIdx.x] = a1;
+    s[2][threadIdx.x] = b0;
+    s[3][threadIdx.x] = b1;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            s[0][threadIdx.x] = fmin(s[0][threadIdx.x], s[0][threadIdx.x + w]);
+            s[1][threadIdx.x] = fmax(s[1][threadIdx.x], s[1][threadIdx.x + w]);
+            s[2][threadIdx.x] = fmin(s[2][threadIdx.x], s[2][threadIdx.x + w]);
+            s[3][threadIdx.x] = fmax(s[3][threadIdx.x], s[3][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 4) out4[threadIdx.x] = s[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void k_grid_count(const double *x, const double *y, int64_t m,
+                                                    double x0, double y0, double inv_h, int gx,
+                                                    int gy, int32_t *cell_of, int32_t *counts) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int cx = cell_coord(x[i], x0, inv_h, gx);
+    const int cy = cell_coord(y[i], y0, inv_h, gy);
+    const int c = cy * gx + cx;
+    cell_of[i] = c;
+    atomicAdd(&counts[c], 1);
+}
+
+__global__ __launch_bounds__(256) void k_grid_scatter(const double *x, const double *y,
+                                                      const double *z, int64_t m,
+                                                      const int32_t *cell_of,
+                                                      const int32_t *cell_start, int32_t *fill,
+                                                      TPt *pts) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int c = cell_of[i];
+    const int pos = cell_start[c] + atomicAdd(&fill[c], 1);
+    double4 v;
+    v.x = x[i];
+    v.y = y[i];
+    v.z = z ? z[i] : 0.0;
+    v.w = __longlong_as_double((long long)i);
+    *reinterpret_cast<double4 *>(pts + pos) = v;
+}
+
+// Order each cell's stems by index so the grid layout is deterministic (results are
+// deterministic regardless: ties are resolved by index explicitly).
+__global__ __launch_bounds__(256) void k_grid_sort_cells(TPt *pts, const int32_t *cell_start,
+                                                         int64_t ncells) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    const int p0 = cell_start[c], p1 = cell_start[c + 1];
+    if (p1 - p0 > 64) return;  // only small cells; large ones keep arrival order
+    for (int a = p0 + 1; a < p1; ++a) {
+        const TPt v = pts[a];
+        int b = a - 1;
+        while (b >= p0 && pts[b].idx > v.idx) {
+            pts[b + 1] = pts[b];
+            --b;
+        }
+        pts[b + 1] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_deinterleave(const double *rows, int64_t n, int64_t ld,
+                                                      int ncols, double *c0, double *c1,
+                                                      double *c2) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double *r = rows + i * ld;
+    c0[i] = r[0];
+    if (ncols > 1) c1[i] = r[1];
+    if (ncols > 2 && c2) c2[i] = r[2];
+}
+
+__global__ __launch_bounds__(256) void k_interleave_xy(const double *x, const double *y, int64_t n,
+                                                       double *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[2 * i] = x[i];
+    out[2 * i + 1] = y[i];
+}
+
+inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+hipError_t launch_minmax2(const double *x, const double *y, int64_t m, double *partials,
+                          double *out4, hipStream_t s) {
+    int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (m + 255) / 256));
+    hipLaunchKernelGGL(k_minmax2_partial, dim3(nb), dim3(256), 0, s, x, y, m, partials);
+    hipLaunchKernelGGL(k_minmax2_final, dim3(1), dim3(256), 0, s, partials, nb, out4);
+    return hipGetLastError();
+}
+
+hipError_t launch_grid_count(const double *x, const double *y, int64_t m, double x0, double y0,
+                             double inv_h, int gx, int gy, int32_t *cell_of, int32_t *counts,
+                             hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_grid_count, dim3(nblk(m)), dim3(256), 0, s, x, y, m, x0, y0, inv_h, gx,
+                       gy, cell_of, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_grid_scatter(const double *x, const double *y, const double *z, int64_t m,
+                               const int32_t *cell_of, const int32_t *cell_start, int32_t *fill,
+                               TPt *pts, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_grid_scatter, dim3(nblk(m)), dim3(256), 0, s, x, y, z, m, cell_of,
+                       cell_start, fill, pts);
+    return hipGetLastError();
+}
+
+hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t ncells,
+                                  hipStream_t s) {
+    hipLaunchKernelGGL(k_grid_sort_cells, dim3(nblk(ncells)), dim3(256), 0, s, pts, cell_start,
+                       ncells);
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    dim3 grid(nblk(a.n)), blk(256);
+    if (md == 3) {
+        if (a.T) hipLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, a, g);
+        else hipLaunchKernelGGL((k_nn_grid<3, false>), grid, blk, 0, s, a, g);
+    } else {
+        if (a.T) hipLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, a, g);
+        else hipLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, a, g);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_brute(const NNArgs &a0, const double *tx, const double *ty,
+                           const double *tz, int64_t m, int md, double *part_d2,
+                           int32_t *part_idx, hipStream_t s) {
+    if (a0.n == 0 || m == 0) return hipSuccess;
+    NNArgs a = a0;
+    if (a.T) {  // apply first: with several target chunks every chunk reads the moved source
+        hipLaunchKernelGGL(k_apply_inplace, dim3(nblk(a.n)), dim3(256), 0, s, a.sx, a.sy, a.n,
+                           a.T, a.skip);
+        a.T = nullptr;
+    }
+    constexpr int QPT = 2;
+    const int64_t qblocks = (a.n + 256 * QPT - 1) / (256 * QPT);
+    const int64_t nchunks = brute_chunk_count(a.n, m);
+    const int64_t chunk = ((m + nchunks - 1) / nchunks + kTile - 1) / kTile * kTile;
+    const int64_t nch = (m + chunk - 1) / chunk;
+    dim3 grid((unsigned)qblocks, (unsigned)nch), blk(256);
+    if (md == 3)
+        hipLaunchKernelGGL((k_nn_brute<3, QPT>), grid, blk, 0, s, a, tx, ty, tz, m, chunk,
+                           part_d2, part_idx);
+    else
+        hipLaunchKernelGGL((k_nn_brute<2, QPT>), grid, blk, 0, s, a, tx, ty, tz, m, chunk,
+                           part_d2, part_idx);
+    if (nch > 1)
+        hipLaunchKernelGGL(k_nn_merge, dim3(nblk(a.n)), dim3(256), 0, s, a, (int)nch, part_d2,
+                           part_idx);
+    return hipGetLastError();
+}
+
+// target chunks for the brute kernel: enough workgroups to fill 256 CUs
+int64_t brute_chunk_count(int64_t n, int64_t m) {
+    const int64_t qblocks = (n + 511) / 512;
+    int64_t c = (2048 + qblocks - 1) / qblocks;
+    const int64_t maxc = (m + kTile - 1) / kTile;
+    if (c > maxc) c = maxc;
+    if (c > 64) c = 64;
+    if (c < 1) c = 1;
+    return c;
+}
+
+hipError_t launch_deinterleave(const double *rows, int64_t n, int64_t ld, int ncols, double *c0,
+                               double *c1, double *c2, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_deinterleave, dim3(nblk(n)), dim3(256), 0, s, rows, n, ld, ncols, c0, c1,
+                       c2);
+    return hipGetLastError();
+}
+
+hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, double *out_xy,
+                                hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_interleave_xy, dim3(nblk(n)), dim3(256), 0, s, x, y, n, out_xy);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_apply_inplace, dim3(nblk(n)), dim3(256), 0, s, x, y, n, T,
+                       (const int *)nullptr);
+    return hipGetLastError();
+}
+
+}  // namespace ficp

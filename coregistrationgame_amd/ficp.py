@@ -1,0 +1,176 @@
+"""`FractionalICP` -- the reference's class surface (ficp.py:5-154) over the MI355X engine.
+
+Drop-in for `from ficp import FractionalICP` in the Join caller (app.py:20, 658-661) and
+the reference tests (tests/test_ficp.py:9, tests/test_rigid_2d_operations.py:8): same
+constructor keywords and defaults, same attributes (source, target, match_dims,
+lambda_val, threshold, max_iterations, allow_reflection), same public methods with the
+same argument meaning, return values, empty-input behaviour and ValueError text.
+
+Every array operation runs in libficp.so (HIP kernels for gfx950) through ctypes:
+  run() / _iterate()            -> ficp_run: the whole two-stage ICP stays on the device;
+                                   one small state read back per iteration
+  find_correspondences          -> ficp_nn (exact 1-NN, cKDTree-identical)
+  find_optimal_fraction         -> ficp_optimal_fraction (device sort + prefix scan)
+  get_n_first_elements          -> ficp_argsort (stable device sort)
+  frmsd                         -> ficp_frmsd
+  compute_optimal_transform_2d  -> ficp_fit_rigid2d
+  apply_transform_2d_xy_only    -> ficp_apply_xy
+There is no CPU fallback: without the library or a GPU the methods raise.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+
+
+class FractionalICP:
+    def __init__(
+        self,
+        source,
+        target,
+        lambda_val=3.0,
+        threshold=1e-6,
+        max_iterations=1000,
+        allow_reflection=False,
+        *,
+        device=None,
+        nn_mode="auto",
+    ):
+        """
+        Fractional ICP (rigid 2D only), as ficp.py:6-44:
+          * correspondences / FRMSD in 3D when both layers have >= 3 columns, else 2D;
+          * rigid planar transform (rotation + XY translation, no scaling);
+          * applied to XY only; Z and extra columns are left unchanged.
+
+        Extra keyword-only options of this engine: ``device`` (GPU ordinal; default
+        $FICP_DEVICE, $LOCAL_RANK or 0) and ``nn_mode`` ("auto", "brute", "grid").
+        """
+        self.source = np.array(source, dtype=float)
+        self.target = np.array(target, dtype=float)
+
+        if self.source.ndim != 2 or self.target.ndim != 2:
+            raise ValueError("source and target must be 2D arrays (N, D).")
+
+        self.match_dims = 3 if (self.source.shape[1] >= 3 and self.target.shape[1] >= 3) else 2
+        self.lambda_val = lambda_val
+        self.threshold = threshold
+        self.max_iterations = max_iterations
+        self.allow_reflection = allow_reflection
+        self.device = device
+        self.nn_mode = {"auto": _lib.NN_AUTO, "brute": _lib.NN_BRUTE, "grid": _lib.NN_GRID}[nn_mode]
+        self.last_stats = None
+        self._ctx = None
+
+    # ----------------- engine context -----------------
+    def _context(self) -> _lib.Context:
+        if self._ctx is None:
+            self._ctx = _lib.Context(self.device, self.nn_mode)
+        return self._ctx
+
+    def close(self):
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None
+
+    # ----------------- helpers (ficp.py:47-51) -----------------
+    def _xy(self, pts):
+        return np.ascontiguousarray(pts[:, :2])
+
+    def _xyz_or_xy(self, pts):
+        return np.ascontiguousarray(pts[:, :self.match_dims])
+
+    # ----------------- FRMSD & matching -----------------
+    def frmsd(self, fraction, num_elements, subset_source, corresponding_targets):
+        """Fractional RMSD in XYZ (or XY if no Z) -- ficp.py:54-60."""
+        if num_elements == 0:
+            return float("inf")
+        a = self._xyz_or_xy(np.asarray(subset_source, dtype=float))
+        b = self._xyz_or_xy(np.asarray(corresponding_targets, dtype=float))
+        if a.shape != b.shape:
+            raise ValueError(f"operands could not be broadcast together with shapes {a.shape} {b.shape}")
+        return self._context().frmsd(a, b, num_elements, self.match_dims, fraction, self.lambda_val)
+
+    def get_n_first_elements(self, num_elements, distances):
+        """argsort(distances)[:num_elements] -- ficp.py:62-63 (stable: ties by index)."""
+        d = np.asarray(distances, dtype=float).ravel()
+        if d.size == 0:
+            return np.zeros(0, dtype=np.intp)
+        return self._context().argsort(d)[:num_elements].astype(np.intp, copy=False)
+
+    def find_correspondences(self, source, target):
+        """Exact 1-NN of every source row in the target -- ficp.py:65-71.
+
+        Uses the instance's match_dims (fixed in the constructor), returns
+        (target[idx] with all target columns, distances)."""
+        if len(target) == 0 or len(source) == 0:
+            empty_corr = np.empty((0, target.shape[1]))
+            return empty_corr, np.array([])
+        md = self.match_dims
+        ctx = self._context()
+        ctx.set_target(np.asarray(target, dtype=float)[:, :md], md)
+        idx, dist = ctx.nn(np.asarray(source, dtype=float)[:, :md])
+        return target[idx], dist
+
+    def find_optimal_fraction(self, corresponding_targets, distances):
+        """Subset size minimising FRMSD -- ficp.py:73-86 (one device sort + prefix scan
+        instead of the reference's O(N^2) loop; same first-minimum rule)."""
+        N = len(self.source)
+        if N == 0 or len(distances) == 0:
+            return 0.0, 0
+        d = np.asarray(distances, dtype=float).ravel()
+        n = len(d)
+        if n > N:
+            raise IndexError(f"index {N} is out of bounds for axis 0 with size {N}")
+        md = self.match_dims
+        src = self._xyz_or_xy(self.source[:n])
+        corr = self._xyz_or_xy(np.asarray(corresponding_targets, dtype=float)[:n])
+        frac, k = self._context().optimal_fraction(src, corr, d, N, md, self.lambda_val)
+        return frac, k
+
+    # ----------------- rigid 2D transform -----------------
+    def compute_optimal_transform_2d(self, source_subset, target_subset):
+        """2D rigid transform (rotation + translation) -- ficp.py:89-110."""
+        X = self._xy(np.asarray(source_subset, dtype=float))
+        Y = self._xy(np.asarray(target_subset, dtype=float))
+        if len(X) != len(Y):
+            raise ValueError(f"matmul: size mismatch {len(X)} vs {len(Y)}")
+        if len(X) == 0:
+            # mean of nothing: the reference's centroids are NaN and H = 0 -> R = I
+            T = np.eye(3)
+            T[:2, 2] = np.nan
+            return T
+        return self._context().fit_rigid2d(X, Y, self.allow_reflection)
+
+    def apply_transform_2d_xy_only(self, points, T):
+        """Apply a 2D rigid transform to XY only -- ficp.py:112-119."""
+        out = points.copy()
+        if len(points) == 0:
+            return out
+        xy_t = self._context().apply_xy(np.asarray(points, dtype=float)[:, :2], np.asarray(T, dtype=float))
+        out[:, :2] = xy_t
+        return out
+
+    # ----------------- ICP loop -----------------
+    def _stages(self, lambdas, trace=False, trace_idx=False):
+        src = np.array(self.source, dtype=np.float64, order="C", copy=True)
+        if len(src) == 0 or len(self.target) == 0:
+            self.last_stats = dict(n_nn_calls=0, n_fits=0, iters=(0, 0))
+            return self.source
+        ctx = self._context()
+        ctx.set_target(self._xyz_or_xy(self.target), self.match_dims)
+        self.last_stats = ctx.run(src, lambdas, self.threshold, self.max_iterations, self.allow_reflection,
+                                  trace=trace, trace_idx=trace_idx)
+        self.source = src
+        return self.source
+
+    def _iterate(self, trace=False, trace_idx=False):
+        """One FRMSD-ICP stage with the current lambda -- ficp.py:122-147."""
+        return self._stages([self.lambda_val], trace, trace_idx)
+
+    def run(self, trace=False, trace_idx=False):
+        """Two-stage Fractional ICP (rigid only) -- ficp.py:149-154."""
+        lam2 = 0.95 if self.match_dims == 3 else 1.3
+        self._stages([self.lambda_val, lam2], trace, trace_idx)
+        self.lambda_val = lam2
+        return self.source

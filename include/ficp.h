@@ -1,0 +1,127 @@
+/*
+ * ficp.h -- C ABI of the MI355X-native Fractional ICP engine (libficp.so).
+ *
+ * Drop-in boundary: the reference has no native boundary of its own; its
+ * interface is the Python class `FractionalICP` (ficp.py:5-154), imported by
+ * the Join caller (app.py:20, app.py:658-660) and by the tests
+ * (tests/test_ficp.py:9, tests/test_rigid_2d_operations.py:8).  The Python
+ * facade coregistrationgame_amd/ficp.py keeps that class surface and binds
+ * these entry points with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Host arrays are row-major C-contiguous fp64 with a leading dimension `ld`
+ *    (columns); only the first `md` columns (2 or 3) are read, only columns 0,1
+ *    are ever written.  The library never keeps a host pointer after a call
+ *    returns.
+ *  - `*_device` entry points take SoA device pointers (x[], y[], z[]) on the
+ *    context's device; they are the "inputs already resident in HBM" path.
+ *  - Return value: FICP_OK (0) or a negative FICP_E* code; ficp_last_error()
+ *    returns a thread-local message for the last failure.
+ *  - A context is not thread-safe; distinct contexts are independent.  All
+ *    work of a context runs on one HIP stream of its device.
+ *  - Parity rules: squared distance ((0+dx^2)+dy^2)+dz^2 in
+ *    fp64 without FMA contraction, argmin on it, dist = sqrt; exact ties go to
+ *    the lowest target index; selection order = stable sort of dist.
+ */
+#ifndef FICP_H
+#define FICP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FICP_OK 0
+#define FICP_EINVAL (-1)  /* bad argument (shape, md, null pointer)          */
+#define FICP_EHIP (-2)    /* HIP runtime error                                */
+#define FICP_ENOMEM (-3)  /* device allocation failed                         */
+#define FICP_ESTATE (-4)  /* call order (e.g. no target set)                  */
+#define FICP_ENODEV (-5)  /* no usable GPU                                    */
+
+typedef struct ficp_ctx ficp_ctx;
+
+/* Per-run statistics and optional traces (caller-owned arrays, nullable). */
+typedef struct ficp_stats {
+    int32_t n_nn_calls;      /* out: NN correspondence calls (both stages)            */
+    int32_t n_fits;          /* out: fits applied = ICP loop bodies (ficp.py:132-145) */
+    int32_t iters[2];        /* out: loop bodies per stage                            */
+    int64_t k_last;          /* out: k of the last fraction call                      */
+    double frmsd_last[2];    /* out: last FRMSD of each stage                         */
+    double T_total[9];       /* out: composite transform of the whole run (row-major) */
+    double gpu_ms;           /* out: wall time of the run on the device stream        */
+    int32_t max_trace;       /* in : capacity of the trace arrays (NN calls)          */
+    int32_t _pad;
+    int64_t *trace_k;        /* [max_trace]      k per NN/fraction call               */
+    double *trace_frmsd;     /* [max_trace]      FRMSD at that k                      */
+    double *trace_lambda;    /* [max_trace]      lambda in force                      */
+    double *trace_T;         /* [max_trace * 9]  fits, in order                       */
+    int32_t *trace_idx;      /* [max_trace * n]  NN target index per call             */
+} ficp_stats;
+
+/* --- library / context ------------------------------------------------- */
+int ficp_version(void);                       /* ABI version, e.g. 100 */
+const char *ficp_last_error(void);
+int ficp_device_count(int *count);
+int ficp_create(int device, ficp_ctx **out);
+void ficp_destroy(ficp_ctx *ctx);
+/* NN algorithm: 0 = auto, 1 = brute force (LDS-tiled), 2 = uniform grid. */
+int ficp_set_nn_mode(ficp_ctx *ctx, int32_t mode);
+/* Kernel timing with HIP events on the context stream: mask bit per kernel class
+   (1 = nn, 2 = sort, 4 = scan/fraction, 8 = fit, 16 = grid build); 0 = off. */
+int ficp_profile_enable(ficp_ctx *ctx, int32_t mask);
+/* JSON {"kernel": {"count": c, "ms": total}, ...} of the timings so far; resets them. */
+int ficp_profile_report(ficp_ctx *ctx, char *buf, int64_t buflen);
+
+/* --- static CHM layer (target) ----------------------------------------- */
+/* Replaces the per-call cKDTree(target) of ficp.py:69: uploads the target once and
+   builds its uniform grid; reused by every later NN call of this context. */
+int ficp_set_target(ficp_ctx *ctx, const double *tgt, int64_t m, int64_t ld, int32_t md);
+int ficp_set_target_device(ficp_ctx *ctx, const double *x, const double *y, const double *z,
+                           int64_t m, int32_t md);
+
+/* --- the hot-path operations (ficp.py method each replaces) -------------- */
+/* find_correspondences (ficp.py:65-71): idx[i], dist[i] of the exact 1-NN of src row i. */
+int ficp_nn(ficp_ctx *ctx, const double *src, int64_t n, int64_t ld, int32_t *idx, double *dist);
+/* find_optimal_fraction (ficp.py:73-86): n rows of src/corr/dist, N = len(self.source). */
+int ficp_optimal_fraction(ficp_ctx *ctx, const double *src, int64_t lds, const double *corr,
+                          int64_t ldc, const double *dist, int64_t n, int64_t n_source,
+                          int32_t md, double lambda_val, double *frac, int64_t *k);
+/* frmsd (ficp.py:54-60): squared differences summed over `rows` rows, divided by
+   num_elements; +inf when num_elements == 0. */
+int ficp_frmsd(ficp_ctx *ctx, const double *src, int64_t lds, const double *corr, int64_t ldc,
+               int64_t rows, int64_t num_elements, int32_t md, double fraction,
+               double lambda_val, double *out);
+/* argsort (ficp.py:63,78): stable order of d (ties by index). */
+int ficp_argsort(ficp_ctx *ctx, const double *d, int64_t n, int64_t *order);
+/* compute_optimal_transform_2d (ficp.py:89-110) on k pairs (XY columns). */
+int ficp_fit_rigid2d(ficp_ctx *ctx, const double *src, int64_t lds, const double *tgt,
+                     int64_t ldt, int64_t k, int32_t allow_reflection, double T[9]);
+/* apply_transform_2d_xy_only (ficp.py:112-119): writes the new XY to out_xy (n x 2). */
+int ficp_apply_xy(ficp_ctx *ctx, const double *pts, int64_t n, int64_t ld, const double T[9],
+                  double *out_xy);
+
+/* --- the whole ICP ---------------------------------------------------- */
+/* _iterate (ficp.py:122-147) for `nstages` stages with lambdas[s]; run()
+   (ficp.py:149-154) is nstages = 2 with {lambda_val, 0.95 if md == 3 else 1.3}.
+   src (n x ld, host) columns 0,1 are updated in place; md from ficp_set_target. */
+int ficp_run(ficp_ctx *ctx, double *src, int64_t n, int64_t ld, int32_t nstages,
+             const double *lambdas, double threshold, int32_t max_iterations,
+             int32_t allow_reflection, ficp_stats *stats);
+/* Same on device-resident SoA source; x, y updated in place. */
+int ficp_run_device(ficp_ctx *ctx, double *x, double *y, const double *z, int64_t n,
+                    int32_t nstages, const double *lambdas, double threshold,
+                    int32_t max_iterations, int32_t allow_reflection, ficp_stats *stats);
+
+/* --- device memory helpers (for callers without their own allocator) ---- */
+int ficp_dev_alloc(ficp_ctx *ctx, int64_t bytes, void **ptr);
+int ficp_dev_free(ficp_ctx *ctx, void *ptr);
+int ficp_memcpy_h2d(ficp_ctx *ctx, void *dst, const void *src, int64_t bytes);
+int ficp_memcpy_d2h(ficp_ctx *ctx, void *dst, const void *src, int64_t bytes);
+int ficp_memcpy_d2d(ficp_ctx *ctx, void *dst, const void *src, int64_t bytes);
+int ficp_synchronize(ficp_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FICP_H */

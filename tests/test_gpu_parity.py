@@ -171,7 +171,7 @@ def test_fit_golden(ctx):
     cases, _ = load_cases("fit")
     for name, c in cases.items():
         T = ctx.fit_rigid2d(c["src"][:, :2], c["tgt"][:, :2], bool(c["allow_reflection"]))
-        assert_T_close(T, c["T"], c["src"], atol_R=1e-12, atol_xy=1e-9, msg=name)
+        assert_T_close(T, c["T"], c["src"], atol_R=1e-12, atol_xy=1e-7, msg=name)
         np.testing.assert_array_equal(T[2], [0.0, 0.0, 1.0])
 
 

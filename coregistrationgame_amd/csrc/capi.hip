@@ -104,6 +104,9 @@ struct ficp_ctx {
 
     // source + per-call buffers
     DevBuf sx, sy, sz, idx, dist, r, key, val, order, sort_tmp, frac_tmp, fit_tmp, bd2, bidx;
+    DevBuf ccx, ccy, rs;  // correspondence XY per source point; r in selection order
+    bool bbox_ready = false;
+    double bb[4] = {0, 0, 0, 0};
     DevBuf stage, stage2, cx, cy, cz, state_dev;
     IterState *h_state = nullptr;  // pinned
 
@@ -172,21 +175,31 @@ int upload_rows(ficp_ctx *c, const double *rows, int64_t n, int64_t ld, int ncol
     return FICP_OK;
 }
 
+// bounding box of the CHM layer (grid geometry and the fit's pivot), once per target
+int ensure_bbox(ficp_ctx *c) {
+    if (c->bbox_ready) return FICP_OK;
+    CHK(c->mm_part.ensure(1024 * 4 * 8));
+    CHK(c->mm_out.ensure(4 * 8));
+    HIPCHK(launch_minmax2(c->tx.as<double>(), c->ty.as<double>(), c->m, c->mm_part.as<double>(),
+                          c->mm_out.as<double>(), c->stream));
+    HIPCHK(hipMemcpyAsync(c->bb, c->mm_out.p, sizeof c->bb, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    const double *bb = c->bb;
+    if (!(std::isfinite(bb[0]) && std::isfinite(bb[1]) && std::isfinite(bb[2]) && std::isfinite(bb[3])))
+        return fail(FICP_EINVAL, "target coordinates must be finite");
+    c->pivot_x = bb[0] + 0.5 * (bb[1] - bb[0]);
+    c->pivot_y = bb[2] + 0.5 * (bb[3] - bb[2]);
+    c->bbox_ready = true;
+    return FICP_OK;
+}
+
 int ensure_grid(ficp_ctx *c) {
     if (c->grid_ready) return FICP_OK;
     const int64_t m = c->m;
     ProfScope ps(c, P_GRID, "grid_build");
     // 1. bounding box
-    CHK(c->mm_part.ensure(1024 * 4 * 8));
-    CHK(c->mm_out.ensure(4 * 8));
-    HIPCHK(launch_minmax2(c->tx.as<double>(), c->ty.as<double>(), m, c->mm_part.as<double>(),
-                          c->mm_out.as<double>(), c->stream));
-    double bb[4];
-    HIPCHK(hipMemcpyAsync(bb, c->mm_out.p, sizeof bb, hipMemcpyDeviceToHost, c->stream));
-    CHK(sync(c));
-    const double x0 = bb[0], x1 = bb[1], y0 = bb[2], y1 = bb[3];
-    if (!(std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1)))
-        return fail(FICP_EINVAL, "target coordinates must be finite");
+    CHK(ensure_bbox(c));
+    const double x0 = c->bb[0], x1 = c->bb[1], y0 = c->bb[2], y1 = c->bb[3];
     // 2. geometry: about kPerCell stems per cell
     const double kPerCell = 2.0;
     const double sxr = x1 - x0, syr = y1 - y0;
@@ -211,8 +224,6 @@ int ensure_grid(ficp_ctx *c) {
     g.gx = (int)gx;
     g.gy = (int)gy;
     g.margin = 64.0 * 2.220446049250313e-16 * (fabs(x0) + fabs(y0) + sxr + syr + h);
-    c->pivot_x = x0 + 0.5 * sxr;
-    c->pivot_y = y0 + 0.5 * syr;
     // 3. counting sort of the stems by cell
     CHK(c->cell_of.ensure(m * 4));
     CHK(c->counts.ensure((c->ncells + 1) * 4));
@@ -256,6 +267,9 @@ int ensure_work(ficp_ctx *c, int64_t n) {
     CHK(c->frac_tmp.ensure(frac_tmp_bytes(n)));
     CHK(c->fit_tmp.ensure(fit_tmp_bytes(n)));
     CHK(c->state_dev.ensure(sizeof(IterState)));
+    CHK(c->ccx.ensure(n * 8));
+    CHK(c->ccy.ensure(n * 8));
+    CHK(c->rs.ensure(n * 8));
     return FICP_OK;
 }
 
@@ -274,6 +288,10 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.r = c->r.as<double>();
     a.key = want_keys ? c->key.as<unsigned long long>() : nullptr;
     a.val = want_keys ? c->val.as<uint32_t>() : nullptr;
+    a.cx = want_keys ? c->ccx.as<double>() : nullptr;
+    a.cy = want_keys ? c->ccy.as<double>() : nullptr;
+    a.tx = c->tx.as<double>();
+    a.ty = c->ty.as<double>();
     if (use_grid(c, n)) {
         CHK(ensure_grid(c));
         ProfScope ps(c, P_NN, "nn_grid");
@@ -296,12 +314,13 @@ int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam) {
     {
         ProfScope ps(c, P_SORT, "sort");
         HIPCHK(launch_sort_pairs(c->key.as<unsigned long long>(), c->val.as<uint32_t>(), n,
-                                 c->order.as<uint32_t>(), c->sort_tmp.p, nullptr, c->stream));
+                                 c->order.as<uint32_t>(), c->r.as<double>(), c->rs.as<double>(),
+                                 c->sort_tmp.p, nullptr, c->stream));
     }
     {
         ProfScope ps(c, P_FRAC, "fraction");
-        HIPCHK(launch_fraction(c->order.as<uint32_t>(), c->r.as<double>(), n, N, lam,
-                               c->frac_tmp.p, c->state_dev.as<IterState>(), nullptr, c->stream));
+        HIPCHK(launch_fraction(c->rs.as<double>(), n, N, lam, c->frac_tmp.p,
+                               c->state_dev.as<IterState>(), nullptr, c->stream));
     }
     return FICP_OK;
 }
@@ -353,7 +372,10 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     if (n == 0 || c->m == 0) return FICP_OK;  // ficp.py:66-68 + 125-126: nothing moves
     if (n > 0x7fffffff) return fail(FICP_EINVAL, "n too large");
     CHK(ensure_work(c, n));
+    CHK(ensure_bbox(c));
     IterState *dst = c->state_dev.as<IterState>();
+    FitIn fa{sx, sy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
+             c->order.as<uint32_t>(), n, c->pivot_x, c->pivot_y, dst};
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     for (int s = 0; s < nstages; ++s) {
         const double lam = lambdas[s];
@@ -368,9 +390,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         while (it < max_iter) {
             {
                 ProfScope ps(c, P_FIT, "fit");
-                HIPCHK(launch_fit(c->order.as<uint32_t>(), sx, sy, c->idx.as<int32_t>(),
-                                  c->tx.as<double>(), c->ty.as<double>(), n, c->pivot_x,
-                                  c->pivot_y, allow_refl, c->fit_tmp.p, dst, nullptr, c->stream));
+                HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, nullptr, c->stream));
             }
             CHK(nn_call(c, sx, sy, sz, n, dst->T, true));
             CHK(sort_and_select(c, n, n, lam));
@@ -460,7 +480,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->fill, &c->pts, &c->scan_tmp, &c->mm_part, &c->mm_out, &c->sx,
                       &c->sy, &c->sz, &c->idx, &c->dist, &c->r, &c->key, &c->val, &c->order,
                       &c->sort_tmp, &c->frac_tmp, &c->fit_tmp, &c->bd2, &c->bidx, &c->stage,
-                      &c->stage2, &c->cx, &c->cy, &c->cz, &c->state_dev};
+                      &c->stage2, &c->cx, &c->cy, &c->cz, &c->state_dev, &c->ccx, &c->ccy, &c->rs};
     for (DevBuf *b : bufs) b->release();
     for (auto &r : c->recs) {
         hipEventDestroy(r.a);
@@ -524,6 +544,7 @@ int ficp_set_target(ficp_ctx *c, const double *tgt, int64_t m, int64_t ld, int32
     if (m > 0x7fffffff) return fail(FICP_EINVAL, "target too large");
     c->has_target = true;
     c->grid_ready = false;
+    c->bbox_ready = false;
     c->m = m;
     c->md = md;
     CHK(upload_rows(c, tgt, m, ld, md, c->tx, c->ty, &c->tz));
@@ -538,6 +559,7 @@ int ficp_set_target_device(ficp_ctx *c, const double *x, const double *y, const 
     if (m > 0x7fffffff) return fail(FICP_EINVAL, "target too large");
     c->has_target = true;
     c->grid_ready = false;
+    c->bbox_ready = false;
     c->m = m;
     c->md = md;
     CHK(c->tx.ensure(m * 8));
@@ -631,7 +653,8 @@ int ficp_argsort(ficp_ctx *c, const double *d, int64_t n, int64_t *order) {
     HIPCHK(launch_keys_from_doubles(c->stage2.as<double>(), n, c->key.as<unsigned long long>(),
                                     c->val.as<uint32_t>(), c->stream));
     HIPCHK(launch_sort_pairs(c->key.as<unsigned long long>(), c->val.as<uint32_t>(), n,
-                             c->order.as<uint32_t>(), c->sort_tmp.p, nullptr, c->stream));
+                             c->order.as<uint32_t>(), nullptr, nullptr, c->sort_tmp.p, nullptr,
+                             c->stream));
     std::vector<uint32_t> tmp((size_t)n);
     HIPCHK(hipMemcpyAsync(tmp.data(), c->order.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));
@@ -650,11 +673,13 @@ int ficp_fit_rigid2d(ficp_ctx *c, const double *src, int64_t lds, const double *
     CHK(c->state_dev.ensure(sizeof(IterState)));
     // pivot: the first source point keeps the sums well conditioned for any offset
     double p[2] = {0.0, 0.0};
-    HIPCHK(hipMemcpyAsync(p, c->stage.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&p[0], c->sx.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&p[1], c->sy.p, 8, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));
-    HIPCHK(launch_fit(nullptr, c->sx.as<double>(), c->sy.as<double>(), nullptr,
-                      c->cx.as<double>(), c->cy.as<double>(), k, p[0], p[1], allow_reflection,
-                      c->fit_tmp.p, c->state_dev.as<IterState>(), nullptr, c->stream));
+    FitIn fa{c->sx.as<double>(), c->sy.as<double>(), c->cx.as<double>(), c->cy.as<double>(),
+             nullptr, nullptr, k, p[0], p[1], c->state_dev.as<IterState>()};
+    HIPCHK(launch_fit(fa, allow_reflection, c->fit_tmp.p, c->state_dev.as<IterState>(), nullptr,
+                      c->stream));
     CHK(read_state(c));
     memcpy(T, c->h_state->T, 9 * sizeof(double));
     return FICP_OK;

@@ -42,6 +42,10 @@ struct NNArgs {
     double *r;                  // out: d^2 (nullable)
     unsigned long long *key;    // out: order-preserving bits of dist (nullable)
     uint32_t *val;              // out: identity payload for the sort (nullable)
+    double *cx;                 // out: XY of the matched stem (nullable)
+    double *cy;
+    const double *tx;           // original-order CHM layer (brute path gathers cx, cy)
+    const double *ty;
 };
 
 // Device-resident state of one ICP stage (written by kernels, read back per iteration).
@@ -89,8 +93,10 @@ hipError_t launch_scan_i32(const int32_t *in, int32_t *out, int64_t n, int32_t *
 // stable LSD radix sort, then orders every run of equal top bits by the full key.
 // Outputs val_out (and key_out).  Scratch sized by sort_tmp_bytes(n).
 int64_t sort_tmp_bytes(int64_t n);
+// r_in/r_sorted (nullable): also emit r_sorted[j] = r_in[val_out[j]].
 hipError_t launch_sort_pairs(const unsigned long long *key, const uint32_t *val_in, int64_t n,
-                             uint32_t *val_out, void *tmp, const int *skip, hipStream_t s);
+                             uint32_t *val_out, const double *r_in, double *r_sorted, void *tmp,
+                             const int *skip, hipStream_t s);
 hipError_t launch_keys_from_doubles(const double *d, int64_t n, unsigned long long *key,
                                     uint32_t *val, hipStream_t s);
 
@@ -100,22 +106,26 @@ int64_t frac_tmp_bytes(int64_t n);
 hipError_t launch_residuals(const double *sx, const double *sy, const double *sz,
                             const double *cx, const double *cy, const double *cz, int64_t n,
                             int md, double *r, hipStream_t s);
-// argmin_k FRMSD(k) over the sorted order -> st->k, st->frac, st->frmsd
-hipError_t launch_fraction(const uint32_t *order, const double *r, int64_t n, int64_t n_src,
-                           double lambda_val, void *tmp, IterState *st, const int *skip,
-                           hipStream_t s);
-// fit on the first st->k entries of `order` (or the first kfixed rows when order == null):
-// src point i = (sx[i], sy[i]), its partner = (tx[j], ty[j]) with j = idx ? idx[i] : i.
+// argmin_k FRMSD(k) over r in selection order (rs) -> st->k, st->frac, st->frmsd
+hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double lambda_val,
+                           void *tmp, IterState *st, const int *skip, hipStream_t s);
+// Rigid fit of source (sx, sy) onto its correspondences (cx, cy).  With key != null the
+// selected rows are the first st->k entries of the stable order (order, key); with
+// key == null every one of the n rows is used.
+struct FitIn {
+    const double *sx, *sy, *cx, *cy;
+    const unsigned long long *key;
+    const uint32_t *order;
+    int64_t n;
+    double px, py;          // pivot subtracted before summation
+    const IterState *st;
+};
 int64_t fit_tmp_bytes(int64_t n);
-hipError_t launch_fit(const uint32_t *order, const double *sx, const double *sy,
-                      const int32_t *idx, const double *tx, const double *ty, int64_t kfixed,
-                      double px, double py, int allow_reflection, void *tmp, IterState *st,
+hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,
                       const int *skip, hipStream_t s);
 hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hipStream_t s);
 hipError_t launch_sum_sq_diff(const double *sx, const double *sy, const double *sz,
                               const double *cx, const double *cy, const double *cz, int64_t k,
                               int md, void *tmp, double *out, hipStream_t s);
-hipError_t launch_gather_xy(const int32_t *idx, const double *tx, const double *ty, int64_t n,
-                            double *ox, double *oy, hipStream_t s);
 
 }  // namespace ficp

@@ -52,7 +52,7 @@ __device__ __forceinline__ double sq_dist(double qx, double qy, double qz, doubl
 
 template <int MD>
 __device__ __forceinline__ void scan_pts(const TPt *__restrict__ pts, int p0, int p1, double qx,
-                                         double qy, double qz, double &best, int &bi) {
+                                         double qy, double qz, double &best, int &bi, int &bp) {
     for (int p = p0; p < p1; ++p) {
         const double4 a = *reinterpret_cast<const double4 *>(pts + p);
         double s = sq_dist<MD>(qx, qy, qz, a.x, a.y, a.z);
@@ -60,12 +60,13 @@ __device__ __forceinline__ void scan_pts(const TPt *__restrict__ pts, int p0, in
         bool b = (s < best) | ((s == best) & (id < bi));
         best = b ? s : best;
         bi = b ? id : bi;
+        bp = b ? p : bp;
     }
 }
 
 template <int MD>
 __device__ __forceinline__ void grid_query(const GridView &g, double qx, double qy, double qz,
-                                           double &best, int &bi) {
+                                           double &best, int &bi, int &bp) {
     const int cx = cell_coord(qx, g.x0, g.inv_h, g.gx);
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
     const double mq = g.margin + 1e-15 * (fabs(qx) + fabs(qy));
@@ -80,17 +81,17 @@ __device__ __forceinline__ void grid_query(const GridView &g, double qx, double 
             if (gyap > 0.0 && gyap * gyap > best) continue;
             const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
             if (yy == ya || yy == yb) {
-                scan_pts<MD>(g.pts, row[xlo], row[xhi + 1], qx, qy, qz, best, bi);
+                scan_pts<MD>(g.pts, row[xlo], row[xhi + 1], qx, qy, qz, best, bi, bp);
             } else {
                 if (xa >= 0) {
                     const double gx0 = qx - (g.x0 + (double)(xa + 1) * g.h) - mq;
                     if (!(gx0 > 0.0 && gx0 * gx0 > best))
-                        scan_pts<MD>(g.pts, row[xa], row[xa + 1], qx, qy, qz, best, bi);
+                        scan_pts<MD>(g.pts, row[xa], row[xa + 1], qx, qy, qz, best, bi, bp);
                 }
                 if (xb < g.gx) {
                     const double gx1 = (g.x0 + (double)xb * g.h) - qx - mq;
                     if (!(gx1 > 0.0 && gx1 * gx1 > best))
-                        scan_pts<MD>(g.pts, row[xb], row[xb + 1], qx, qy, qz, best, bi);
+                        scan_pts<MD>(g.pts, row[xb], row[xb + 1], qx, qy, qz, best, bi, bp);
                 }
             }
         }
@@ -117,6 +118,10 @@ __device__ __forceinline__ void apply_T(const double *__restrict__ T, double &x,
 
 __device__ __forceinline__ void write_out(const NNArgs &a, int64_t i, double best, int bi) {
     a.idx[i] = bi;
+    if (a.cx) {  // correspondence XY for the fit (gathered from the original layer)
+        a.cx[i] = a.tx[bi];
+        a.cy[i] = a.ty[bi];
+    }
     const double d = sqrt(best);
     if (a.dist) a.dist[i] = d;
     if (a.r) a.r[i] = best;
@@ -137,9 +142,16 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     }
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
     double best = INFINITY;
-    int bi = 0x7fffffff;
-    grid_query<MD>(g, qx, qy, qz, best, bi);
-    write_out(a, i, best, bi);
+    int bi = 0x7fffffff, bp = 0;
+    grid_query<MD>(g, qx, qy, qz, best, bi, bp);
+    if (a.cx) {  // correspondence XY straight from the grid record just scanned (L1/L2 hot)
+        const double2 c = *reinterpret_cast<const double2 *>(g.pts + bp);
+        a.cx[i] = c.x;
+        a.cy[i] = c.y;
+    }
+    NNArgs b = a;
+    b.cx = nullptr;
+    write_out(b, i, best, bi);
 }
 
 constexpr int kTile = 256;

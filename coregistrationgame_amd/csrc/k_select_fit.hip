@@ -3,18 +3,20 @@
 //
 // Fraction: the reference evaluates FRMSD(k) = (1.0 / (k/N)**lambda) * sqrt(S_k / k) for
 // every prefix k of argsort(dist), each with a fresh O(k) sum -> O(N^2) (ficp.py:80-85).
-// Here S_k is ONE prefix scan of r_(j) = sum_md (src - corr)^2 in the sorted order
-// (tile sums -> scan of tile sums -> per-tile scan fused with the FRMSD evaluation and
-// a first-minimum argmin), all deterministic (fixed reduction trees, no float atomics).
+// Here S_k is ONE prefix scan of r_(j) = sum_md (src - corr)^2 in selection order (the
+// sort already wrote r in that order, so every read is coalesced): tile sums -> scan of
+// the tile sums -> per-tile scan fused with the FRMSD evaluation and a first-minimum
+// argmin.  Deterministic: fixed reduction trees, no float atomics.
 //
-// Fit: two passes like the reference (centroids, then the 2x2 cross-covariance of the
-// centred pairs), reduced per tile and combined in a fixed order; coordinates are
-// shifted by a pivot (the CHM-layer centre) before summation so geo-referenced inputs
-// (~6.5e6 m) keep full precision.  R comes from the closed form of the 2x2 Kabsch
-// problem: rotation angle atan2(H01 - H10, H00 + H11) -- identical to the SVD path
-// R = Vt^T U^T with the det fix of ficp.py:101-103; with
-// allow_reflection the SVD path returns a reflection iff det(H) < 0, given here by the
-// angle atan2(H01 + H10, H00 - H11).
+// Fit: the selected set is {i : (key_i, i) <= (key_t, t)} with t = order[k-1] (the k-th
+// entry of the stable order), so the fit streams every source point in index order
+// (coalesced x, y, corr x, corr y, key) instead of gathering through the permutation.
+// One pass accumulates the 8 sums of the pivot-shifted pairs (pivot = CHM-layer centre,
+// so geo-referenced ~6.5e6 m coordinates keep their precision); H = sum s't'^T -
+// k cs' ct'^T.  R from the closed form of the 2x2 Kabsch problem: rotation angle
+// atan2(H01 - H10, H00 + H11), identical to the SVD path R = Vt^T U^T with the det fix
+// of ficp.py:101-103; with allow_reflection the SVD path returns a
+// reflection iff det(H) < 0, given by the angle atan2(H01 + H10, H00 - H11).
 #include "ficp_internal.h"
 
 #include <math.h>
@@ -26,7 +28,7 @@ namespace ficp {
 namespace {
 
 constexpr int FB = 256;
-constexpr int FI = 16;
+constexpr int FI = 4;
 constexpr int FTILE = FB * FI;
 
 __device__ __forceinline__ double block_sum_d(double v, double *s /*[256]*/) {
@@ -62,8 +64,8 @@ __device__ __forceinline__ double block_excl_scan_d(double v, double *s /*[2][25
 }
 
 __device__ __forceinline__ double frmsd_of(long long k, long long N, double S, double lam) {
-    const double frac = (double)k / (double)N;
-    return (1.0 / pow(frac, lam)) * sqrt(S / (double)k);
+    const double frac = (double)k / (double)N;  // k / N (ficp.py:81)
+    return (1.0 / pow(frac, lam)) * sqrt(S / (double)k);  // ficp.py:59-60
 }
 
 __device__ __forceinline__ bool better(double f, long long k, double bf, long long bk) {
@@ -87,16 +89,16 @@ __global__ __launch_bounds__(256) void k_residuals(const double *sx, const doubl
     r[i] = s;
 }
 
-// per tile: sum of r in sorted order
-__global__ __launch_bounds__(FB) void k_frac_tilesum(const uint32_t *order, const double *r,
-                                                     int64_t n, double *tsum, const int *skip) {
+// per tile: sum of r in selection order
+__global__ __launch_bounds__(FB) void k_frac_tilesum(const double *rs, int64_t n, double *tsum,
+                                                     const int *skip) {
     if (skip && *skip) return;
     __shared__ double s[256];
-    const int64_t j0 = (int64_t)blockIdx.x * FTILE + (int64_t)threadIdx.x * FI;
+    const int64_t j0 = (int64_t)blockIdx.x * FTILE + threadIdx.x;
     double acc = 0.0;
 #pragma unroll
-    for (int q = 0; q < FI; ++q)
-        if (j0 + q < n) acc = acc + r[order[j0 + q]];
+    for (int q = 0; q < FI; ++q)  // strided within the tile: coalesced; order fixed
+        if (j0 + q * FB < n) acc = acc + rs[j0 + q * FB];
     const double t = block_sum_d(acc, s);
     if (threadIdx.x == 0) tsum[blockIdx.x] = t;
 }
@@ -123,10 +125,9 @@ struct BestRec {
     long long k;
 };
 
-__global__ __launch_bounds__(FB) void k_frac_eval(const uint32_t *order, const double *r,
-                                                  int64_t n, int64_t N, double lam,
-                                                  const double *tpre, BestRec *tbest,
-                                                  const int *skip) {
+__global__ __launch_bounds__(FB) void k_frac_eval(const double *rs, int64_t n, int64_t N,
+                                                  double lam, const double *tpre,
+                                                  BestRec *tbest, const int *skip) {
     if (skip && *skip) return;
     __shared__ double s[512];
     __shared__ double s_f[256];
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(FB) void k_frac_eval(const uint32_t *order, const d
     double acc = 0.0;
 #pragma unroll
     for (int q = 0; q < FI; ++q) {
-        v[q] = (j0 + q < n) ? r[order[j0 + q]] : 0.0;
+        v[q] = (j0 + q < n) ? rs[j0 + q] : 0.0;
         acc = acc + v[q];
     }
     double S = tpre[blockIdx.x] + block_excl_scan_d(acc, s);
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(FB) void k_frac_eval(const uint32_t *order, const d
             S = S + v[q];
             const long long k = j + 1;
             const double f = frmsd_of(k, N, S, lam);
-            if (f < bf) {  // ascending k: strict < keeps the first minimum
+            if (f < bf) {  // ascending k: strict < keeps the first minimum (ficp.py:84)
                 bf = f;
                 bk = k;
             }
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256) void k_frac_final(const BestRec *tbest, int nb
                 bk = N;
             }
         }
-        if (bk == 0x7fffffffffffffffLL) {  // every FRMSD was NaN/inf: reference keeps (0.0, 0)
+        if (bk == 0x7fffffffffffffffLL) {  // every FRMSD was NaN: reference keeps (0.0, 0)
             st->k = 0;
             st->frac = 0.0;
             st->frmsd = INFINITY;
@@ -224,123 +225,78 @@ __global__ __launch_bounds__(256) void k_frac_final(const BestRec *tbest, int nb
 }
 
 // ------------------------------------------------------------------------- fit
-struct FitIn {
-    const uint32_t *order;  // selection order (null: rows 0..k-1)
-    const double *sx, *sy;
-    const int32_t *idx;     // partner index (null: same row)
-    const double *tx, *ty;
-    int64_t kfixed;         // k when order == null
-    double px, py;          // pivot
-    const IterState *st;
-};
-
-__device__ __forceinline__ int64_t fit_k(const FitIn &a) { return a.order ? (int64_t)a.st->k : a.kfixed; }
-
-__device__ __forceinline__ void fit_pair(const FitIn &a, int64_t j, double &xs, double &ys,
-                                         double &xt, double &yt) {
-    const int64_t i = a.order ? (int64_t)a.order[j] : j;
-    const int64_t m = a.idx ? (int64_t)a.idx[i] : i;
-    xs = a.sx[i] - a.px;
-    ys = a.sy[i] - a.py;
-    xt = a.tx[m] - a.px;
-    yt = a.ty[m] - a.py;
+__device__ __forceinline__ bool fit_threshold(const FitIn &a, unsigned long long &tk,
+                                              int64_t &ti) {
+    if (!a.key) return true;  // every row selected
+    const long long k = a.st->k;
+    if (k <= 0) {
+        tk = 0;
+        ti = -1;
+        return false;
+    }
+    ti = (int64_t)a.order[k - 1];
+    tk = a.key[ti];
+    return false;
 }
 
-__global__ __launch_bounds__(FB) void k_fit_pass1(FitIn a, double *part, const int *skip) {
+__global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, const int *skip) {
     if (skip && *skip) return;
     __shared__ double s[256];
-    const int64_t k = fit_k(a);
-    const int64_t j0 = (int64_t)blockIdx.x * FTILE + (int64_t)threadIdx.x * FI;
-    double c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    unsigned long long tk = 0;
+    int64_t ti = 0;
+    const bool all = fit_threshold(a, tk, ti);
+    const int64_t i0 = (int64_t)blockIdx.x * FTILE + threadIdx.x;
+    double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
     for (int q = 0; q < FI; ++q) {
-        const int64_t j = j0 + q;
-        if (j < k) {
-            double xs, ys, xt, yt;
-            fit_pair(a, j, xs, ys, xt, yt);
-            c0 = c0 + xs;
-            c1 = c1 + ys;
-            c2 = c2 + xt;
-            c3 = c3 + yt;
+        const int64_t i = i0 + q * FB;
+        if (i < a.n) {
+            bool sel = all;
+            if (!all) {
+                const unsigned long long ki = a.key[i];
+                sel = ki < tk || (ki == tk && i <= ti);
+            }
+            if (sel) {
+                const double xs = a.sx[i] - a.px, ys = a.sy[i] - a.py;
+                const double xt = a.cx[i] - a.px, yt = a.cy[i] - a.py;
+                c[0] = c[0] + xs;
+                c[1] = c[1] + ys;
+                c[2] = c[2] + xt;
+                c[3] = c[3] + yt;
+                c[4] = c[4] + xs * xt;
+                c[5] = c[5] + xs * yt;
+                c[6] = c[6] + ys * xt;
+                c[7] = c[7] + ys * yt;
+            }
         }
     }
-    c0 = block_sum_d(c0, s);
-    c1 = block_sum_d(c1, s);
-    c2 = block_sum_d(c2, s);
-    c3 = block_sum_d(c3, s);
-    if (threadIdx.x == 0) {
-        part[4 * blockIdx.x + 0] = c0;
-        part[4 * blockIdx.x + 1] = c1;
-        part[4 * blockIdx.x + 2] = c2;
-        part[4 * blockIdx.x + 3] = c3;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const double t = block_sum_d(c[e], s);
+        if (threadIdx.x == 0) part[8 * blockIdx.x + e] = t;
     }
 }
 
-// identical fixed-order reduction of the pass-1 partials in every block that needs it
-__device__ __forceinline__ void fit_centroids(const double *part, int nb, int64_t k, double *s,
-                                              double c[4]) {
-    for (int e = 0; e < 4; ++e) {
-        double acc = 0.0;
-        for (int b = threadIdx.x; b < nb; b += 256) acc = acc + part[4 * b + e];
-        c[e] = block_sum_d(acc, s) / (double)k;
-    }
-}
-
-__global__ __launch_bounds__(FB) void k_fit_pass2(FitIn a, const double *part1, int nb,
-                                                  double *part2, const int *skip) {
+__global__ __launch_bounds__(256) void k_fit_final(FitIn a, const double *part, int nb,
+                                                   int allow_refl, IterState *st,
+                                                   const int *skip) {
     if (skip && *skip) return;
     __shared__ double s[256];
-    const int64_t k = fit_k(a);
-    const int64_t j0b = (int64_t)blockIdx.x * FTILE;
-    if (j0b >= k) {
-        if (threadIdx.x < 4) part2[4 * blockIdx.x + threadIdx.x] = 0.0;
-        return;
-    }
-    double c[4];
-    fit_centroids(part1, nb, k, s, c);
-    const int64_t j0 = j0b + (int64_t)threadIdx.x * FI;
-    double h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    for (int q = 0; q < FI; ++q) {
-        const int64_t j = j0 + q;
-        if (j < k) {
-            double xs, ys, xt, yt;
-            fit_pair(a, j, xs, ys, xt, yt);
-            xs = xs - c[0];
-            ys = ys - c[1];
-            xt = xt - c[2];
-            yt = yt - c[3];
-            h0 = h0 + xs * xt;
-            h1 = h1 + xs * yt;
-            h2 = h2 + ys * xt;
-            h3 = h3 + ys * yt;
-        }
-    }
-    h0 = block_sum_d(h0, s);
-    h1 = block_sum_d(h1, s);
-    h2 = block_sum_d(h2, s);
-    h3 = block_sum_d(h3, s);
-    if (threadIdx.x == 0) {
-        part2[4 * blockIdx.x + 0] = h0;
-        part2[4 * blockIdx.x + 1] = h1;
-        part2[4 * blockIdx.x + 2] = h2;
-        part2[4 * blockIdx.x + 3] = h3;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_fit_final(FitIn a, const double *part1,
-                                                   const double *part2, int nb, int allow_refl,
-                                                   IterState *st, const int *skip) {
-    if (skip && *skip) return;
-    __shared__ double s[256];
-    const int64_t k = fit_k(a);
-    double c[4];
-    fit_centroids(part1, nb, k, s, c);
-    double H[4];
-    for (int e = 0; e < 4; ++e) {
+    double c[8];
+    for (int e = 0; e < 8; ++e) {
         double acc = 0.0;
-        for (int b = threadIdx.x; b < nb; b += 256) acc = acc + part2[4 * b + e];
-        H[e] = block_sum_d(acc, s);
+        for (int b = threadIdx.x; b < nb; b += 256) acc = acc + part[8 * b + e];
+        c[e] = block_sum_d(acc, s);
     }
     if (threadIdx.x != 0) return;
+    const double k = a.key ? (double)a.st->k : (double)a.n;
+    // centroids of the pivot-shifted pairs, then H = sum s't'^T - k cs' ct'^T
+    const double csx = c[0] / k, csy = c[1] / k, ctx = c[2] / k, cty = c[3] / k;
+    double H[4];
+    H[0] = c[4] - c[0] * ctx;
+    H[1] = c[5] - c[0] * cty;
+    H[2] = c[6] - c[1] * ctx;
+    H[3] = c[7] - c[1] * cty;
     double R00, R01, R10, R11;
     const double det = H[0] * H[3] - H[1] * H[2];
     if (allow_refl && det < 0.0) {
@@ -366,23 +322,21 @@ __global__ __launch_bounds__(256) void k_fit_final(FitIn a, const double *part1,
         R11 = cc;
     }
     // centroids in world coordinates, t = ct - cs @ R^T (ficp.py:105)
-    const double csx = c[0] + a.px, csy = c[1] + a.py;
-    const double ctx = c[2] + a.px, cty = c[3] + a.py;
-    const double tx = ctx - (csx * R00 + csy * R01);
-    const double ty = cty - (csx * R10 + csy * R11);
+    const double wsx = csx + a.px, wsy = csy + a.py;
+    const double wtx = ctx + a.px, wty = cty + a.py;
     st->T[0] = R00;
     st->T[1] = R01;
-    st->T[2] = tx;
+    st->T[2] = wtx - (wsx * R00 + wsy * R01);
     st->T[3] = R10;
     st->T[4] = R11;
-    st->T[5] = ty;
+    st->T[5] = wty - (wsx * R10 + wsy * R11);
     st->T[6] = 0.0;
     st->T[7] = 0.0;
     st->T[8] = 1.0;
-    st->csx = c[0];
-    st->csy = c[1];
-    st->ctx = c[2];
-    st->cty = c[3];
+    st->csx = csx;
+    st->csy = csy;
+    st->ctx = ctx;
+    st->cty = cty;
     for (int e = 0; e < 4; ++e) st->H[e] = H[e];
 }
 
@@ -392,10 +346,10 @@ __global__ __launch_bounds__(256) void k_ssd_partial(const double *sx, const dou
                                                      const double *cy, const double *cz,
                                                      int64_t k, int md, double *part) {
     __shared__ double s[256];
-    const int64_t j0 = (int64_t)blockIdx.x * FTILE + (int64_t)threadIdx.x * FI;
+    const int64_t i0 = (int64_t)blockIdx.x * FTILE + threadIdx.x;
     double acc = 0.0;
     for (int q = 0; q < FI; ++q) {
-        const int64_t i = j0 + q;
+        const int64_t i = i0 + q * FB;
         if (i < k) {
             const double dx = sx[i] - cx[i], dy = sy[i] - cy[i];
             double r = dx * dx;
@@ -419,16 +373,6 @@ __global__ __launch_bounds__(256) void k_ssd_final(const double *part, int nb, d
     if (threadIdx.x == 0) *out = acc;
 }
 
-__global__ __launch_bounds__(256) void k_gather_xy(const int32_t *idx, const double *tx,
-                                                   const double *ty, int64_t n, double *ox,
-                                                   double *oy) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int j = idx[i];
-    ox[i] = tx[j];
-    oy[i] = ty[j];
-}
-
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
@@ -448,18 +392,18 @@ hipError_t launch_residuals(const double *sx, const double *sy, const double *sz
     return hipGetLastError();
 }
 
-hipError_t launch_fraction(const uint32_t *order, const double *r, int64_t n, int64_t n_src,
-                           double lam, void *tmp, IterState *st, const int *skip, hipStream_t s) {
+hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double lam, void *tmp,
+                           IterState *st, const int *skip, hipStream_t s) {
     const int nb = (int)((n + FTILE - 1) / FTILE);
     char *p = (char *)tmp;
     double *tsum = (double *)p;
     p += align_up((int64_t)(nb + 2) * 8, 256);
     BestRec *tbest = (BestRec *)p;
     if (nb > 0) {
-        hipLaunchKernelGGL(k_frac_tilesum, dim3(nb), dim3(FB), 0, s, order, r, n, tsum, skip);
+        hipLaunchKernelGGL(k_frac_tilesum, dim3(nb), dim3(FB), 0, s, rs, n, tsum, skip);
         hipLaunchKernelGGL(k_frac_tilescan, dim3(1), dim3(256), 0, s, tsum, nb, skip);
-        hipLaunchKernelGGL(k_frac_eval, dim3(nb), dim3(FB), 0, s, order, r, n, n_src, lam, tsum,
-                           tbest, skip);
+        hipLaunchKernelGGL(k_frac_eval, dim3(nb), dim3(FB), 0, s, rs, n, n_src, lam, tsum, tbest,
+                           skip);
     }
     hipLaunchKernelGGL(k_frac_final, dim3(1), dim3(256), 0, s, tbest, nb, tsum, n, n_src, lam, st,
                        skip);
@@ -468,24 +412,16 @@ hipError_t launch_fraction(const uint32_t *order, const double *r, int64_t n, in
 
 int64_t fit_tmp_bytes(int64_t n) {
     const int64_t nb = (n + FTILE - 1) / FTILE + 1;
-    return 2 * align_up(nb * 4 * 8, 256);
+    return align_up(nb * 8 * 8, 256);
 }
 
-hipError_t launch_fit(const uint32_t *order, const double *sx, const double *sy,
-                      const int32_t *idx, const double *tx, const double *ty, int64_t n,
-                      double px, double py, int allow_reflection, void *tmp, IterState *st,
+hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,
                       const int *skip, hipStream_t s) {
-    // n = number of rows available (grid size); the kernels read k from st when order != null
-    const int nb = (int)std::max<int64_t>(1, (n + FTILE - 1) / FTILE);
-    char *p = (char *)tmp;
-    double *part1 = (double *)p;
-    p += align_up((int64_t)nb * 4 * 8, 256);
-    double *part2 = (double *)p;
-    FitIn a{order, sx, sy, idx, tx, ty, n, px, py, st};
-    hipLaunchKernelGGL(k_fit_pass1, dim3(nb), dim3(FB), 0, s, a, part1, skip);
-    hipLaunchKernelGGL(k_fit_pass2, dim3(nb), dim3(FB), 0, s, a, part1, nb, part2, skip);
-    hipLaunchKernelGGL(k_fit_final, dim3(1), dim3(256), 0, s, a, part1, part2, nb,
-                       allow_reflection, st, skip);
+    const int nb = (int)std::max<int64_t>(1, (a.n + FTILE - 1) / FTILE);
+    double *part = (double *)tmp;
+    hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FB), 0, s, a, part, skip);
+    hipLaunchKernelGGL(k_fit_final, dim3(1), dim3(256), 0, s, a, part, nb, allow_reflection, st,
+                       skip);
     return hipGetLastError();
 }
 
@@ -497,13 +433,6 @@ hipError_t launch_sum_sq_diff(const double *sx, const double *sy, const double *
     hipLaunchKernelGGL(k_ssd_partial, dim3(nb), dim3(256), 0, s, sx, sy, sz, cx, cy, cz, k, md,
                        part);
     hipLaunchKernelGGL(k_ssd_final, dim3(1), dim3(256), 0, s, part, nb, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_gather_xy(const int32_t *idx, const double *tx, const double *ty, int64_t n,
-                            double *ox, double *oy, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gather_xy, dim3(nblk(n)), dim3(256), 0, s, idx, tx, ty, n, ox, oy);
     return hipGetLastError();
 }
 

@@ -97,6 +97,7 @@ __global__ __launch_bounds__(SB) void k_radix_scatter(const void *kin, const uin
                                                       const uint32_t *counts,
                                                       const uint32_t *rowtot, int nb,
                                                       uint32_t *kout, uint32_t *vout,
+                                                      const double *rin, double *rout,
                                                       const int *skip) {
     if (skip && *skip) return;
     __shared__ uint32_t s_k[STILE];
@@ -163,12 +164,14 @@ __global__ __launch_bounds__(SB) void k_radix_scatter(const void *kin, const uin
         const uint32_t g = s_base[d] + ((uint32_t)li - s_loc[d]);
         kout[g] = k;
         vout[g] = s_v[li];
+        if (rout) rout[g] = rin[s_v[li]];  // last pass: residuals in selection order
     }
 }
 
 // runs of equal top-32 bits: order by the full key (stable insertion sort by the run head)
 __global__ __launch_bounds__(256) void k_sort_fixup(const uint32_t *k32, uint32_t *val,
-                                                    const unsigned long long *key64, int64_t n,
+                                                    const unsigned long long *key64,
+                                                    const double *rin, double *rout, int64_t n,
                                                     const int *skip) {
     if (skip && *skip) return;
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -194,6 +197,8 @@ __global__ __launch_bounds__(256) void k_sort_fixup(const uint32_t *k32, uint32_
         }
         val[b + 1] = v;
     }
+    if (rout)
+        for (int64_t a = j; a < e; ++a) rout[a] = rin[val[a]];
 }
 
 __global__ __launch_bounds__(256) void k_keys_from_doubles(const double *d, int64_t n,
@@ -282,7 +287,8 @@ int64_t sort_tmp_bytes(int64_t n) {
 }
 
 hipError_t launch_sort_pairs(const unsigned long long *key, const uint32_t *val_in, int64_t n,
-                             uint32_t *val_out, void *tmp, const int *skip, hipStream_t s) {
+                             uint32_t *val_out, const double *r_in, double *r_sorted, void *tmp,
+                             const int *skip, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const int nb = (int)((n + STILE - 1) / STILE);
     char *p = (char *)tmp;
@@ -312,15 +318,19 @@ hipError_t launch_sort_pairs(const unsigned long long *key, const uint32_t *val_
         hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(SB), 0, s, counts, nb, rowtot, skip);
         if (pass == 0) {
             hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(SB), 0, s, kin, vin, n, shift,
-                               counts, rowtot, nb, kouts[pass], vouts[pass], skip);
+                               counts, rowtot, nb, kouts[pass], vouts[pass],
+                               (const double *)nullptr, (double *)nullptr, skip);
         } else {
             hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nb), dim3(SB), 0, s, kin, vin, n,
-                               shift, counts, rowtot, nb, kouts[pass], vouts[pass], skip);
+                               shift, counts, rowtot, nb, kouts[pass], vouts[pass],
+                               pass == 3 ? r_in : (const double *)nullptr,
+                               pass == 3 ? r_sorted : (double *)nullptr, skip);
         }
         kin = kouts[pass];
         vin = vouts[pass];
     }
-    hipLaunchKernelGGL(k_sort_fixup, dim3(nblk(n)), dim3(256), 0, s, kA, val_out, key, n, skip);
+    hipLaunchKernelGGL(k_sort_fixup, dim3(nblk(n)), dim3(256), 0, s, kA, val_out, key, r_in,
+                       r_sorted, n, skip);
     return hipGetLastError();
 }
 

@@ -9,11 +9,10 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
-
-#include <cmath>
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <string>
 #include <vector>
@@ -43,9 +42,9 @@ int fail(int code, const char *fmt, ...) {
                         __FILE__, __LINE__);                                               \
     } while (0)
 
-#define CHK(expr)                  \
-    do {                           \
-        int r_ = (expr);           \
+#define CHK(expr)                     \
+    do {                              \
+        int r_ = (expr);              \
         if (r_ != FICP_OK) return r_; \
     } while (0)
 
@@ -54,7 +53,7 @@ struct DevBuf {
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return FICP_OK;
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
         size_t want = std::max<size_t>(bytes, 256);
@@ -67,7 +66,7 @@ struct DevBuf {
         return FICP_OK;
     }
     void release() {
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
     }
@@ -96,17 +95,17 @@ struct ficp_ctx {
     int64_t m = 0;
     int md = 2;
     DevBuf tx, ty, tz;
-    bool grid_ready = false;
+    bool grid_ready = false, bbox_ready = false;
+    double bb[4] = {0, 0, 0, 0};
     DevBuf cell_of, counts, cell_start, fill, pts, scan_tmp, mm_part, mm_out;
     GridView gv{};
     int64_t ncells = 0;
     double pivot_x = 0.0, pivot_y = 0.0;
 
-    // source + per-call buffers
+    // per-call buffers (work order)
     DevBuf sx, sy, sz, idx, dist, r, key, val, order, sort_tmp, frac_tmp, fit_tmp, bd2, bidx;
-    DevBuf ccx, ccy, rs;  // correspondence XY per source point; r in selection order
-    bool bbox_ready = false;
-    double bb[4] = {0, 0, 0, 0};
+    DevBuf ccx, ccy, rs, range;      // matched XY, r in selection order, key range
+    DevBuf wx, wy, wz, worig, tidx;  // spatial work order of the source
     DevBuf stage, stage2, cx, cy, cz, state_dev;
     IterState *h_state = nullptr;  // pinned
 
@@ -128,7 +127,7 @@ hipEvent_t ev_get(ficp_ctx *c) {
         return e;
     }
     hipEvent_t e = nullptr;
-    hipEventCreate(&e);
+    (void)hipEventCreate(&e);
     return e;
 }
 
@@ -139,13 +138,13 @@ struct ProfScope {
     ProfScope(ficp_ctx *c_, int cls, const char *n) : c(c_), name(n) {
         if (c->prof_mask & cls) {
             a = ev_get(c);
-            hipEventRecord(a, c->stream);
+            (void)hipEventRecord(a, c->stream);
         }
     }
     ~ProfScope() {
         if (a) {
             hipEvent_t b = ev_get(c);
-            hipEventRecord(b, c->stream);
+            (void)hipEventRecord(b, c->stream);
             c->recs.push_back({name, a, b});
         }
     }
@@ -185,7 +184,8 @@ int ensure_bbox(ficp_ctx *c) {
     HIPCHK(hipMemcpyAsync(c->bb, c->mm_out.p, sizeof c->bb, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));
     const double *bb = c->bb;
-    if (!(std::isfinite(bb[0]) && std::isfinite(bb[1]) && std::isfinite(bb[2]) && std::isfinite(bb[3])))
+    if (!(std::isfinite(bb[0]) && std::isfinite(bb[1]) && std::isfinite(bb[2]) &&
+          std::isfinite(bb[3])))
         return fail(FICP_EINVAL, "target coordinates must be finite");
     c->pivot_x = bb[0] + 0.5 * (bb[1] - bb[0]);
     c->pivot_y = bb[2] + 0.5 * (bb[3] - bb[2]);
@@ -197,10 +197,9 @@ int ensure_grid(ficp_ctx *c) {
     if (c->grid_ready) return FICP_OK;
     const int64_t m = c->m;
     ProfScope ps(c, P_GRID, "grid_build");
-    // 1. bounding box
     CHK(ensure_bbox(c));
     const double x0 = c->bb[0], x1 = c->bb[1], y0 = c->bb[2], y1 = c->bb[3];
-    // 2. geometry: about kPerCell stems per cell
+    // geometry: about kPerCell stems per cell
     const double kPerCell = 2.0;
     const double sxr = x1 - x0, syr = y1 - y0;
     double h;
@@ -224,19 +223,20 @@ int ensure_grid(ficp_ctx *c) {
     g.gx = (int)gx;
     g.gy = (int)gy;
     g.margin = 64.0 * 2.220446049250313e-16 * (fabs(x0) + fabs(y0) + sxr + syr + h);
-    // 3. counting sort of the stems by cell
+    // counting sort of the stems by cell
     CHK(c->cell_of.ensure(m * 4));
     CHK(c->counts.ensure((c->ncells + 1) * 4));
     CHK(c->fill.ensure((c->ncells + 1) * 4));
     CHK(c->cell_start.ensure((c->ncells + 1) * 4));
     CHK(c->pts.ensure(m * sizeof(TPt)));
     CHK(c->scan_tmp.ensure(scan_tmp_elems(c->ncells) * 4 + 64));
-    HIPCHK(hipMemsetAsync(c->counts.p, 0, (c->ncells + 1) * 4, c->stream));
-    HIPCHK(hipMemsetAsync(c->fill.p, 0, (c->ncells + 1) * 4, c->stream));
+    // counts/fill are updated with atomics: reset them with atomics
+    HIPCHK(launch_atomic_zero32((uint32_t *)c->counts.p, c->ncells + 1, c->stream));
+    HIPCHK(launch_atomic_zero32((uint32_t *)c->fill.p, c->ncells + 1, c->stream));
     HIPCHK(launch_grid_count(c->tx.as<double>(), c->ty.as<double>(), m, g.x0, g.y0, g.inv_h, g.gx,
                              g.gy, c->cell_of.as<int32_t>(), c->counts.as<int32_t>(), c->stream));
     HIPCHK(launch_scan_i32(c->counts.as<int32_t>(), c->cell_start.as<int32_t>(), c->ncells,
-                           c->scan_tmp.as<int32_t>(), c->stream));
+                           c->scan_tmp.as<int32_t>(), true, c->stream));
     HIPCHK(launch_grid_scatter(c->tx.as<double>(), c->ty.as<double>(),
                                c->md == 3 ? c->tz.as<double>() : nullptr, m,
                                c->cell_of.as<int32_t>(), c->cell_start.as<int32_t>(),
@@ -270,10 +270,17 @@ int ensure_work(ficp_ctx *c, int64_t n) {
     CHK(c->ccx.ensure(n * 8));
     CHK(c->ccy.ensure(n * 8));
     CHK(c->rs.ensure(n * 8));
+    if (!c->range.p) {
+        CHK(c->range.ensure(64));
+        HIPCHK(launch_atomic_zero64(c->range.as<unsigned long long>(), 2, c->stream));
+    }
     return FICP_OK;
 }
 
+unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long long>(); }
+
 // NN of the device source (sx, sy, sz) against the target; optional pending transform.
+// With want_keys the sort inputs (key, range, r, matched XY) are produced too.
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
             bool want_keys) {
     NNArgs a{};
@@ -287,11 +294,12 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.dist = c->dist.as<double>();
     a.r = c->r.as<double>();
     a.key = want_keys ? c->key.as<unsigned long long>() : nullptr;
-    a.val = want_keys ? c->val.as<uint32_t>() : nullptr;
+    a.val = nullptr;
     a.cx = want_keys ? c->ccx.as<double>() : nullptr;
     a.cy = want_keys ? c->ccy.as<double>() : nullptr;
     a.tx = c->tx.as<double>();
     a.ty = c->ty.as<double>();
+    a.range = want_keys ? range_ptr(c) : nullptr;
     if (use_grid(c, n)) {
         CHK(ensure_grid(c));
         ProfScope ps(c, P_NN, "nn_grid");
@@ -310,12 +318,13 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     return FICP_OK;
 }
 
-int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam) {
+// sort (key, orig) of the last NN call, then the FRMSD fraction scan
+int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam, const uint32_t *orig) {
     {
         ProfScope ps(c, P_SORT, "sort");
-        HIPCHK(launch_sort_pairs(c->key.as<unsigned long long>(), c->val.as<uint32_t>(), n,
-                                 c->order.as<uint32_t>(), c->r.as<double>(), c->rs.as<double>(),
-                                 c->sort_tmp.p, nullptr, c->stream));
+        HIPCHK(launch_sort(c->key.as<unsigned long long>(), orig, n, range_ptr(c),
+                           c->order.as<uint32_t>(), c->r.as<double>(), c->rs.as<double>(),
+                           c->sort_tmp.p, nullptr, c->stream));
     }
     {
         ProfScope ps(c, P_FRAC, "fraction");
@@ -339,7 +348,7 @@ void mat3_mul(const double A[9], const double B[9], double C[9]) {
     memcpy(C, R, sizeof R);
 }
 
-int trace_call(ficp_ctx *c, ficp_stats *st, int64_t n, double lam) {
+int trace_call(ficp_ctx *c, ficp_stats *st, int64_t n, double lam, const uint32_t *worig) {
     if (!st) return FICP_OK;
     const int32_t call = st->n_nn_calls;
     st->n_nn_calls++;
@@ -349,10 +358,37 @@ int trace_call(ficp_ctx *c, ficp_stats *st, int64_t n, double lam) {
     if (st->trace_frmsd) st->trace_frmsd[call] = c->h_state->frmsd;
     if (st->trace_lambda) st->trace_lambda[call] = lam;
     if (st->trace_idx && n > 0) {
-        HIPCHK(hipMemcpyAsync(st->trace_idx + (int64_t)call * n, c->idx.p, n * 4,
+        const void *src = c->idx.p;
+        if (worig) {  // back to the caller's row order
+            CHK(c->tidx.ensure(n * 4));
+            HIPCHK(launch_scatter_i32(worig, c->idx.as<int32_t>(), n, c->tidx.as<int32_t>(),
+                                      c->stream));
+            src = c->tidx.p;
+        }
+        HIPCHK(hipMemcpyAsync(st->trace_idx + (int64_t)call * n, src, n * 4,
                               hipMemcpyDeviceToHost, c->stream));
         CHK(sync(c));
     }
+    return FICP_OK;
+}
+
+// Spatial work order: the source permuted into 8x8-cell supertile order of the CHM grid
+// (ties by index), so each wave's queries scan neighbouring cells.
+int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const double *sz,
+                     int64_t n) {
+    CHK(c->wx.ensure(n * 8));
+    CHK(c->wy.ensure(n * 8));
+    if (sz) CHK(c->wz.ensure(n * 8));
+    CHK(c->worig.ensure(n * 4));
+    ProfScope ps(c, P_MISC, "work_order");
+    HIPCHK(launch_src_cellkey(sx, sy, n, c->gv, c->key.as<unsigned long long>(), c->stream));
+    HIPCHK(launch_key_range(c->key.as<unsigned long long>(), n, range_ptr(c), c->stream));
+    HIPCHK(launch_sort(c->key.as<unsigned long long>(), nullptr, n, range_ptr(c),
+                       c->order.as<uint32_t>(), nullptr, nullptr, c->sort_tmp.p, nullptr,
+                       c->stream));
+    HIPCHK(launch_gather_work(c->order.as<uint32_t>(), sx, sy, sz, n, c->wx.as<double>(),
+                              c->wy.as<double>(), sz ? c->wz.as<double>() : nullptr,
+                              c->worig.as<uint32_t>(), c->stream));
     return FICP_OK;
 }
 
@@ -370,19 +406,32 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         st->gpu_ms = 0.0;
     }
     if (n == 0 || c->m == 0) return FICP_OK;  // ficp.py:66-68 + 125-126: nothing moves
-    if (n > 0x7fffffff) return fail(FICP_EINVAL, "n too large");
+    if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large (max 2^30 - 1)");
     CHK(ensure_work(c, n));
     CHK(ensure_bbox(c));
-    IterState *dst = c->state_dev.as<IterState>();
-    FitIn fa{sx, sy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
-             c->order.as<uint32_t>(), n, c->pivot_x, c->pivot_y, dst};
+    uint32_t *tflag = sort_timeout_flag(c->sort_tmp.p, n);
+    HIPCHK(launch_atomic_zero32(tflag, 1, c->stream));
     HIPCHK(hipEventRecord(c->ev0, c->stream));
+    double *wx = sx, *wy = sy;
+    const double *wz = sz;
+    const uint32_t *worig = nullptr;
+    if (use_grid(c, n)) {
+        CHK(ensure_grid(c));
+        CHK(build_work_order(c, sx, sy, sz, n));
+        wx = c->wx.as<double>();
+        wy = c->wy.as<double>();
+        wz = sz ? c->wz.as<double>() : nullptr;
+        worig = c->worig.as<uint32_t>();
+    }
+    IterState *dst = c->state_dev.as<IterState>();
+    FitIn fa{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
+             c->order.as<uint32_t>(), worig, n, c->pivot_x, c->pivot_y, dst};
     for (int s = 0; s < nstages; ++s) {
         const double lam = lambdas[s];
-        CHK(nn_call(c, sx, sy, sz, n, nullptr, true));
-        CHK(sort_and_select(c, n, n, lam));
+        CHK(nn_call(c, wx, wy, wz, n, nullptr, true));
+        CHK(sort_and_select(c, n, n, lam, worig));
         CHK(read_state(c));
-        CHK(trace_call(c, st, n, lam));
+        CHK(trace_call(c, st, n, lam, worig));
         if (c->h_state->k == 0) continue;
         double cur = c->h_state->frmsd;
         if (st) st->frmsd_last[s < 2 ? s : 1] = cur;
@@ -392,8 +441,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
                 ProfScope ps(c, P_FIT, "fit");
                 HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, nullptr, c->stream));
             }
-            CHK(nn_call(c, sx, sy, sz, n, dst->T, true));
-            CHK(sort_and_select(c, n, n, lam));
+            CHK(nn_call(c, wx, wy, wz, n, dst->T, true));
+            CHK(sort_and_select(c, n, n, lam, worig));
             CHK(read_state(c));
             if (st) {
                 if (st->trace_T && st->n_fits < st->max_trace)
@@ -401,7 +450,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
                 st->n_fits++;
                 mat3_mul(c->h_state->T, st->T_total, st->T_total);
             }
-            CHK(trace_call(c, st, n, lam));
+            CHK(trace_call(c, st, n, lam, worig));
             const double nw = c->h_state->frmsd;
             if (st) st->frmsd_last[s < 2 ? s : 1] = nw;
             if (cur - nw <= threshold) break;  // ficp.py:142 (transform already applied)
@@ -410,13 +459,17 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         }
         if (st && s < 2) st->iters[s] = it;
     }
+    if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     CHK(sync(c));
     if (st) {
         float ms = 0.f;
-        hipEventElapsedTime(&ms, c->ev0, c->ev1);
+        (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
         st->gpu_ms = ms;
     }
+    uint32_t tf = 0;
+    HIPCHK(hipMemcpy(&tf, tflag, 4, hipMemcpyDeviceToHost));
+    if (tf) return fail(FICP_EHIP, "residual sort look-back timed out (results invalid)");
     return FICP_OK;
 }
 
@@ -428,6 +481,14 @@ int check_ctx(ficp_ctx *c) {
 int check_md(int32_t md) {
     if (md != 2 && md != 3) return fail(FICP_EINVAL, "md must be 2 or 3 (got %d)", md);
     return FICP_OK;
+}
+
+void reset_target(ficp_ctx *c, int64_t m, int md) {
+    c->has_target = true;
+    c->grid_ready = false;
+    c->bbox_ready = false;
+    c->m = m;
+    c->md = md;
 }
 
 }  // namespace
@@ -456,12 +517,14 @@ int ficp_create(int device, ficp_ctx **out) {
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(FICP_ENODEV, "no HIP device");
-    if (device < 0 || device >= n) return fail(FICP_EINVAL, "device %d out of range [0,%d)", device, n);
+    if (device < 0 || device >= n)
+        return fail(FICP_EINVAL, "device %d out of range [0,%d)", device, n);
     ficp_ctx *c = new ficp_ctx();
     c->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_state, sizeof(IterState), hipHostMallocDefault);
+    if (e == hipSuccess)
+        e = hipHostMalloc((void **)&c->h_state, sizeof(IterState), hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e != hipSuccess) {
@@ -474,23 +537,26 @@ int ficp_create(int device, ficp_ctx **out) {
 
 void ficp_destroy(ficp_ctx *c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    DevBuf *bufs[] = {&c->tx, &c->ty, &c->tz, &c->cell_of, &c->counts, &c->cell_start,
-                      &c->fill, &c->pts, &c->scan_tmp, &c->mm_part, &c->mm_out, &c->sx,
-                      &c->sy, &c->sz, &c->idx, &c->dist, &c->r, &c->key, &c->val, &c->order,
-                      &c->sort_tmp, &c->frac_tmp, &c->fit_tmp, &c->bd2, &c->bidx, &c->stage,
-                      &c->stage2, &c->cx, &c->cy, &c->cz, &c->state_dev, &c->ccx, &c->ccy, &c->rs};
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->tx,     &c->ty,         &c->tz,       &c->cell_of,  &c->counts,
+                      &c->cell_start, &c->fill,   &c->pts,      &c->scan_tmp, &c->mm_part,
+                      &c->mm_out, &c->sx,         &c->sy,       &c->sz,       &c->idx,
+                      &c->dist,   &c->r,          &c->key,      &c->val,      &c->order,
+                      &c->sort_tmp, &c->frac_tmp, &c->fit_tmp,  &c->bd2,      &c->bidx,
+                      &c->ccx,    &c->ccy,        &c->rs,       &c->range,    &c->wx,
+                      &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
+                      &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev};
     for (DevBuf *b : bufs) b->release();
     for (auto &r : c->recs) {
-        hipEventDestroy(r.a);
-        hipEventDestroy(r.b);
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
     }
-    for (auto e : c->ev_pool) hipEventDestroy(e);
-    if (c->ev0) hipEventDestroy(c->ev0);
-    if (c->ev1) hipEventDestroy(c->ev1);
-    if (c->h_state) hipHostFree(c->h_state);
-    if (c->stream) hipStreamDestroy(c->stream);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -512,7 +578,7 @@ int ficp_profile_report(ficp_ctx *c, char *buf, int64_t buflen) {
     CHK(sync(c));
     for (auto &r : c->recs) {
         float ms = 0.f;
-        hipEventElapsedTime(&ms, r.a, r.b);
+        (void)hipEventElapsedTime(&ms, r.a, r.b);
         auto &acc = c->prof_acc[r.name];
         acc.first += 1;
         acc.second += ms;
@@ -532,7 +598,8 @@ int ficp_profile_report(ficp_ctx *c, char *buf, int64_t buflen) {
     s += "}";
     c->prof_acc.clear();
     if (!buf || buflen <= 0) return fail(FICP_EINVAL, "null buffer");
-    if ((int64_t)s.size() + 1 > buflen) return fail(FICP_EINVAL, "buffer too small (%zu)", s.size() + 1);
+    if ((int64_t)s.size() + 1 > buflen)
+        return fail(FICP_EINVAL, "buffer too small (%zu)", s.size() + 1);
     memcpy(buf, s.c_str(), s.size() + 1);
     return FICP_OK;
 }
@@ -542,11 +609,7 @@ int ficp_set_target(ficp_ctx *c, const double *tgt, int64_t m, int64_t ld, int32
     CHK(check_md(md));
     if (m < 0 || (m > 0 && (!tgt || ld < md))) return fail(FICP_EINVAL, "bad target shape");
     if (m > 0x7fffffff) return fail(FICP_EINVAL, "target too large");
-    c->has_target = true;
-    c->grid_ready = false;
-    c->bbox_ready = false;
-    c->m = m;
-    c->md = md;
+    reset_target(c, m, md);
     CHK(upload_rows(c, tgt, m, ld, md, c->tx, c->ty, &c->tz));
     return sync(c);
 }
@@ -555,20 +618,18 @@ int ficp_set_target_device(ficp_ctx *c, const double *x, const double *y, const 
                            int64_t m, int32_t md) {
     CHK(check_ctx(c));
     CHK(check_md(md));
-    if (m < 0 || (m > 0 && (!x || !y || (md == 3 && !z)))) return fail(FICP_EINVAL, "bad target");
+    if (m < 0 || (m > 0 && (!x || !y || (md == 3 && !z))))
+        return fail(FICP_EINVAL, "bad target");
     if (m > 0x7fffffff) return fail(FICP_EINVAL, "target too large");
-    c->has_target = true;
-    c->grid_ready = false;
-    c->bbox_ready = false;
-    c->m = m;
-    c->md = md;
+    reset_target(c, m, md);
     CHK(c->tx.ensure(m * 8));
     CHK(c->ty.ensure(m * 8));
     CHK(c->tz.ensure(m * 8));
     if (m > 0) {
         HIPCHK(hipMemcpyAsync(c->tx.p, x, m * 8, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->ty.p, y, m * 8, hipMemcpyDeviceToDevice, c->stream));
-        if (md == 3) HIPCHK(hipMemcpyAsync(c->tz.p, z, m * 8, hipMemcpyDeviceToDevice, c->stream));
+        if (md == 3)
+            HIPCHK(hipMemcpyAsync(c->tz.p, z, m * 8, hipMemcpyDeviceToDevice, c->stream));
     }
     return FICP_OK;  // stream-ordered; the grid is built on first use
 }
@@ -576,11 +637,13 @@ int ficp_set_target_device(ficp_ctx *c, const double *x, const double *y, const 
 int ficp_nn(ficp_ctx *c, const double *src, int64_t n, int64_t ld, int32_t *idx, double *dist) {
     CHK(check_ctx(c));
     if (!c->has_target) return fail(FICP_ESTATE, "no target set");
-    if (n < 0 || (n > 0 && (!src || !idx || !dist || ld < c->md))) return fail(FICP_EINVAL, "bad source");
+    if (n < 0 || (n > 0 && (!src || !idx || !dist || ld < c->md)))
+        return fail(FICP_EINVAL, "bad source");
     if (n == 0 || c->m == 0) return FICP_OK;
     CHK(upload_rows(c, src, n, ld, c->md, c->sx, c->sy, &c->sz));
     CHK(ensure_work(c, n));
-    CHK(nn_call(c, c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(), n, nullptr, false));
+    CHK(nn_call(c, c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(), n, nullptr,
+                false));
     HIPCHK(hipMemcpyAsync(idx, c->idx.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(dist, c->dist.p, n * 8, hipMemcpyDeviceToHost, c->stream));
     return sync(c);
@@ -597,7 +660,7 @@ int ficp_optimal_fraction(ficp_ctx *c, const double *src, int64_t lds, const dou
     if (n_source == 0 || n == 0) return FICP_OK;  // ficp.py:76-77
     if (n < 0 || n_source < 0 || !src || !corr || !dist || lds < md || ldc < md)
         return fail(FICP_EINVAL, "bad arguments");
-    if (n > 0x7fffffff) return fail(FICP_EINVAL, "n too large");
+    if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large");
     CHK(ensure_work(c, n));
     CHK(upload_rows(c, src, n, lds, md, c->sx, c->sy, &c->sz));
     CHK(upload_rows(c, corr, n, ldc, md, c->cx, c->cy, &c->cz));
@@ -607,8 +670,9 @@ int ficp_optimal_fraction(ficp_ctx *c, const double *src, int64_t lds, const dou
                             c->cx.as<double>(), c->cy.as<double>(), c->cz.as<double>(), n, md,
                             c->r.as<double>(), c->stream));
     HIPCHK(launch_keys_from_doubles(c->stage2.as<double>(), n, c->key.as<unsigned long long>(),
-                                    c->val.as<uint32_t>(), c->stream));
-    CHK(sort_and_select(c, n, n_source, lambda_val));
+                                    nullptr, c->stream));
+    HIPCHK(launch_key_range(c->key.as<unsigned long long>(), n, range_ptr(c), c->stream));
+    CHK(sort_and_select(c, n, n_source, lambda_val, nullptr));
     CHK(read_state(c));
     *k = c->h_state->k;
     *frac = c->h_state->frac;
@@ -646,18 +710,24 @@ int ficp_argsort(ficp_ctx *c, const double *d, int64_t n, int64_t *order) {
     CHK(check_ctx(c));
     if (n < 0 || (n > 0 && (!d || !order))) return fail(FICP_EINVAL, "bad arguments");
     if (n == 0) return FICP_OK;
-    if (n > 0x7fffffff) return fail(FICP_EINVAL, "n too large");
+    if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large");
     CHK(ensure_work(c, n));
     CHK(c->stage2.ensure(n * 8));
     HIPCHK(hipMemcpyAsync(c->stage2.p, d, n * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(launch_keys_from_doubles(c->stage2.as<double>(), n, c->key.as<unsigned long long>(),
-                                    c->val.as<uint32_t>(), c->stream));
-    HIPCHK(launch_sort_pairs(c->key.as<unsigned long long>(), c->val.as<uint32_t>(), n,
-                             c->order.as<uint32_t>(), nullptr, nullptr, c->sort_tmp.p, nullptr,
-                             c->stream));
+                                    nullptr, c->stream));
+    uint32_t *tflag = sort_timeout_flag(c->sort_tmp.p, n);
+    HIPCHK(launch_atomic_zero32(tflag, 1, c->stream));
+    HIPCHK(launch_key_range(c->key.as<unsigned long long>(), n, range_ptr(c), c->stream));
+    HIPCHK(launch_sort(c->key.as<unsigned long long>(), nullptr, n, range_ptr(c),
+                       c->order.as<uint32_t>(), nullptr, nullptr, c->sort_tmp.p, nullptr,
+                       c->stream));
+    uint32_t tf = 0;
+    HIPCHK(hipMemcpyAsync(&tf, tflag, 4, hipMemcpyDeviceToHost, c->stream));
     std::vector<uint32_t> tmp((size_t)n);
     HIPCHK(hipMemcpyAsync(tmp.data(), c->order.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));
+    if (tf) return fail(FICP_EHIP, "sort look-back timed out (results invalid)");
     for (int64_t i = 0; i < n; ++i) order[i] = tmp[(size_t)i];
     return FICP_OK;
 }
@@ -677,7 +747,7 @@ int ficp_fit_rigid2d(ficp_ctx *c, const double *src, int64_t lds, const double *
     HIPCHK(hipMemcpyAsync(&p[1], c->sy.p, 8, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));
     FitIn fa{c->sx.as<double>(), c->sy.as<double>(), c->cx.as<double>(), c->cy.as<double>(),
-             nullptr, nullptr, k, p[0], p[1], c->state_dev.as<IterState>()};
+             nullptr, nullptr, nullptr, k, p[0], p[1], c->state_dev.as<IterState>()};
     HIPCHK(launch_fit(fa, allow_reflection, c->fit_tmp.p, c->state_dev.as<IterState>(), nullptr,
                       c->stream));
     CHK(read_state(c));
@@ -688,7 +758,8 @@ int ficp_fit_rigid2d(ficp_ctx *c, const double *src, int64_t lds, const double *
 int ficp_apply_xy(ficp_ctx *c, const double *pts, int64_t n, int64_t ld, const double T[9],
                   double *out_xy) {
     CHK(check_ctx(c));
-    if (n < 0 || (n > 0 && (!pts || !out_xy || ld < 2)) || !T) return fail(FICP_EINVAL, "bad arguments");
+    if (n < 0 || (n > 0 && (!pts || !out_xy || ld < 2)) || !T)
+        return fail(FICP_EINVAL, "bad arguments");
     if (n == 0) return FICP_OK;
     CHK(upload_rows(c, pts, n, ld, 2, c->sx, c->sy, nullptr));
     CHK(c->stage2.ensure(std::max<int64_t>(n * 16, 128)));
@@ -709,11 +780,13 @@ int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
     if (!c->has_target) return fail(FICP_ESTATE, "no target set");
     if (n < 0 || (n > 0 && (!src || ld < c->md)) || nstages < 0 || (nstages > 0 && !lambdas))
         return fail(FICP_EINVAL, "bad arguments");
-    if (n == 0 || c->m == 0) return run_core(c, nullptr, nullptr, nullptr, 0, nstages, lambdas,
-                                             threshold, max_iterations, allow_reflection, stats);
+    if (n == 0 || c->m == 0)
+        return run_core(c, nullptr, nullptr, nullptr, 0, nstages, lambdas, threshold,
+                        max_iterations, allow_reflection, stats);
     CHK(upload_rows(c, src, n, ld, c->md, c->sx, c->sy, &c->sz));
-    CHK(run_core(c, c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(), n, nstages,
-                 lambdas, threshold, max_iterations, allow_reflection, stats));
+    CHK(run_core(c, c->sx.as<double>(), c->sy.as<double>(),
+                 c->md == 3 ? c->sz.as<double>() : nullptr, n, nstages, lambdas, threshold,
+                 max_iterations, allow_reflection, stats));
     CHK(c->stage2.ensure(n * 16));
     HIPCHK(launch_interleave_xy(c->sx.as<double>(), c->sy.as<double>(), n, c->stage2.as<double>(),
                                 c->stream));
@@ -735,8 +808,8 @@ int ficp_run_device(ficp_ctx *c, double *x, double *y, const double *z, int64_t 
     if (n < 0 || (n > 0 && (!x || !y || (c->md == 3 && !z))) || nstages < 0 ||
         (nstages > 0 && !lambdas))
         return fail(FICP_EINVAL, "bad arguments");
-    return run_core(c, x, y, z, n, nstages, lambdas, threshold, max_iterations, allow_reflection,
-                    stats);
+    return run_core(c, x, y, c->md == 3 ? z : nullptr, n, nstages, lambdas, threshold,
+                    max_iterations, allow_reflection, stats);
 }
 
 int ficp_dev_alloc(ficp_ctx *c, int64_t bytes, void **ptr) {

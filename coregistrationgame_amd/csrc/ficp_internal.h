@@ -15,6 +15,23 @@ namespace ficp {
 
 constexpr int kWave = 64;
 
+// order-preserving 64-bit key of a double (for d >= 0: the bits with the sign bit set)
+__device__ __forceinline__ unsigned long long ordkey(double v) {
+    unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+
+// wave-wide max of two u64 (all 64 lanes must be active)
+__device__ __forceinline__ void wave_range_reduce(unsigned long long &a, unsigned long long &b) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long xa = __shfl_xor(a, o, 64);
+        const unsigned long long xb = __shfl_xor(b, o, 64);
+        a = xa > a ? xa : a;
+        b = xb > b ? xb : b;
+    }
+}
+
 struct alignas(32) TPt {
     double x, y, z;
     long long idx;
@@ -46,6 +63,7 @@ struct NNArgs {
     double *cy;
     const double *tx;           // original-order CHM layer (brute path gathers cx, cy)
     const double *ty;
+    unsigned long long *range;  // out: key range {max(~key), max(key)} (atomics; nullable)
 };
 
 // Device-resident state of one ICP stage (written by kernels, read back per iteration).
@@ -83,20 +101,42 @@ hipError_t launch_deinterleave(const double *rows, int64_t n, int64_t ld, int nc
                                double *c0, double *c1, double *c2, hipStream_t s);
 hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, double *out_xy,
                                 hipStream_t s);
+// spatial work order of a source layer: key64 = (8x8-supertile cell order << 32) | i
+hipError_t launch_src_cellkey(const double *sx, const double *sy, int64_t n, const GridView &g,
+                              unsigned long long *key, hipStream_t s);
+// w*[p] = s*[perm[p]], worig[p] = perm[p]
+hipError_t launch_gather_work(const uint32_t *perm, const double *sx, const double *sy,
+                              const double *sz, int64_t n, double *wx, double *wy, double *wz,
+                              uint32_t *worig, hipStream_t s);
+// s*[worig[p]] = w*[p]
+hipError_t launch_scatter_xy(const uint32_t *worig, const double *wx, const double *wy, int64_t n,
+                             double *sx, double *sy, hipStream_t s);
+hipError_t launch_scatter_i32(const uint32_t *worig, const int32_t *w, int64_t n, int32_t *out,
+                              hipStream_t s);
 
 // scans / sort (k_sort.hip)
-// Exclusive scan of n int32 (out may alias in); out[n] = total. tmp >= scan_tmp_elems(n).
+// Exclusive scan of n int32; out[n] = total. tmp >= scan_tmp_elems(n).  atomic_in: the
+// input was accumulated with atomics and is read with atomic RMWs.
 int64_t scan_tmp_elems(int64_t n);
 hipError_t launch_scan_i32(const int32_t *in, int32_t *out, int64_t n, int32_t *tmp,
-                           hipStream_t s);
-// Stable sort of (key, val) pairs by 64-bit key.  Sorts by the top 32 key bits with a
-// stable LSD radix sort, then orders every run of equal top bits by the full key.
-// Outputs val_out (and key_out).  Scratch sized by sort_tmp_bytes(n).
+                           bool atomic_in, hipStream_t s);
+// Memory-model rule of this library: a word that any kernel updates with
+// device-scope atomics is reset with atomics (these kernels, never hipMemset or plain
+// stores) and read with atomic RMWs.
+hipError_t launch_atomic_zero32(uint32_t *p, int64_t n, hipStream_t s);
+hipError_t launch_atomic_zero64(unsigned long long *p, int64_t n, hipStream_t s);
+// Stable argsort: order[j] = position (0..n-1) of the j-th smallest (key64, orig) pair
+// (orig == null: orig = position).  range = {max(~key), max(key)} of the keys (from the
+// NN kernel or launch_key_range); the sort resets it to {0, 0}.  r/rs (nullable):
+// rs[j] = r[order[j]].  Scratch: sort_tmp_bytes(n).
 int64_t sort_tmp_bytes(int64_t n);
-// r_in/r_sorted (nullable): also emit r_sorted[j] = r_in[val_out[j]].
-hipError_t launch_sort_pairs(const unsigned long long *key, const uint32_t *val_in, int64_t n,
-                             uint32_t *val_out, const double *r_in, double *r_sorted, void *tmp,
-                             const int *skip, hipStream_t s);
+// sticky flag set when a look-back wait timed out (results of that sort are invalid)
+uint32_t *sort_timeout_flag(void *tmp, int64_t n);
+hipError_t launch_key_range(const unsigned long long *key, int64_t n, unsigned long long *range,
+                            hipStream_t s);
+hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, int64_t n,
+                       unsigned long long *range, uint32_t *order, const double *r, double *rs,
+                       void *tmp, const int *skip, hipStream_t s);
 hipError_t launch_keys_from_doubles(const double *d, int64_t n, unsigned long long *key,
                                     uint32_t *val, hipStream_t s);
 
@@ -116,6 +156,7 @@ struct FitIn {
     const double *sx, *sy, *cx, *cy;
     const unsigned long long *key;
     const uint32_t *order;
+    const uint32_t *orig;   // caller index of each position (tie order; null = identity)
     int64_t n;
     double px, py;          // pivot subtracted before summation
     const IterState *st;

@@ -10,10 +10,14 @@
 //  * k_nn_grid  -- the CHM layer is binned once into a uniform XY grid (cell-sorted AoS,
 //    32 B per stem); a query scans square rings of cells around its own cell until a
 //    conservative lower bound on the distance to everything outside the scanned block
-//    exceeds the best d2.  Work per query is O(stems near the query), HBM/L2 bound.
+//    exceeds the best d2.  Queries run in a spatial work order (8x8-cell supertiles) so
+//    the 64 lanes of a wave scan overlapping cells: their candidate loads coalesce and
+//    hit L1/L2 instead of 64 scattered cache lines.
 //  * k_nn_brute -- LDS-tiled all-pairs scan (target tiles of 256 stems staged in LDS and
 //    read as broadcasts, QPT queries per lane held in registers), fp64-VALU bound; used
 //    for small layers and as an independent cross-check of the grid kernel.
+// Both fuse the pending rigid transform of the previous fit (ficp.py:135) into the
+// source load, and write idx, dist, d2, the sort key, and the matched stem's XY.
 #include "ficp_internal.h"
 
 #include <math.h>
@@ -23,11 +27,6 @@
 namespace ficp {
 
 namespace {
-
-__device__ __forceinline__ unsigned long long ordkey(double v) {
-    unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
-}
 
 __device__ __forceinline__ int cell_coord(double v, double v0, double inv_h, int g) {
     double f = (v - v0) * inv_h;
@@ -116,42 +115,56 @@ __device__ __forceinline__ void apply_T(const double *__restrict__ T, double &x,
     y = ny;
 }
 
-__device__ __forceinline__ void write_out(const NNArgs &a, int64_t i, double best, int bi) {
+// per-point outputs; returns the sort key (for the wave's key-range reduction)
+__device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t i, double best,
+                                                        int bi) {
     a.idx[i] = bi;
-    if (a.cx) {  // correspondence XY for the fit (gathered from the original layer)
-        a.cx[i] = a.tx[bi];
-        a.cy[i] = a.ty[bi];
-    }
     const double d = sqrt(best);
+    const unsigned long long k = ordkey(d);
     if (a.dist) a.dist[i] = d;
     if (a.r) a.r[i] = best;
-    if (a.key) a.key[i] = ordkey(d);
+    if (a.key) a.key[i] = k;
     if (a.val) a.val[i] = (uint32_t)i;
+    return k;
+}
+
+// wave-level {max(~key), max(key)} folded into the global range (all lanes active)
+__device__ __forceinline__ void range_accumulate(unsigned long long *range, bool valid,
+                                                 unsigned long long kmin_c,
+                                                 unsigned long long kmax) {
+    unsigned long long a = valid ? kmin_c : 0ULL, b = valid ? kmax : 0ULL;
+    wave_range_reduce(a, b);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&range[0], a);
+        atomicMax(&range[1], b);
+    }
 }
 
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     if (a.skip && *a.skip) return;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    double qx = a.sx[i], qy = a.sy[i];
-    if (APPLY) {
-        apply_T(a.T, qx, qy);
-        a.sx[i] = qx;
-        a.sy[i] = qy;
+    const bool valid = i < a.n;
+    unsigned long long key = 0;
+    if (valid) {
+        double qx = a.sx[i], qy = a.sy[i];
+        if (APPLY) {
+            apply_T(a.T, qx, qy);
+            a.sx[i] = qx;
+            a.sy[i] = qy;
+        }
+        const double qz = (MD == 3) ? a.sz[i] : 0.0;
+        double best = INFINITY;
+        int bi = 0x7fffffff, bp = 0;
+        grid_query<MD>(g, qx, qy, qz, best, bi, bp);
+        if (a.cx) {  // correspondence XY straight from the grid record just scanned (cache hot)
+            const double2 c = *reinterpret_cast<const double2 *>(g.pts + bp);
+            a.cx[i] = c.x;
+            a.cy[i] = c.y;
+        }
+        key = write_out(a, i, best, bi);
     }
-    const double qz = (MD == 3) ? a.sz[i] : 0.0;
-    double best = INFINITY;
-    int bi = 0x7fffffff, bp = 0;
-    grid_query<MD>(g, qx, qy, qz, best, bi, bp);
-    if (a.cx) {  // correspondence XY straight from the grid record just scanned (L1/L2 hot)
-        const double2 c = *reinterpret_cast<const double2 *>(g.pts + bp);
-        a.cx[i] = c.x;
-        a.cy[i] = c.y;
-    }
-    NNArgs b = a;
-    b.cx = nullptr;
-    write_out(b, i, best, bi);
+    if (a.range) range_accumulate(a.range, valid, ~key, key);
 }
 
 constexpr int kTile = 256;
@@ -202,35 +215,53 @@ __global__ __launch_bounds__(256) void k_nn_brute(NNArgs a, const double *__rest
             }
         }
     }
+    unsigned long long kmin_c = 0, kmax = 0;
+    bool any = false;
 #pragma unroll
     for (int q = 0; q < QPT; ++q) {
         const int64_t i = base + q * 256;
         if (i >= a.n) continue;
         if (gridDim.y == 1) {
-            write_out(a, i, best[q], bi[q]);
+            const unsigned long long k = write_out(a, i, best[q], bi[q]);
+            if (a.cx) {
+                a.cx[i] = a.tx[bi[q]];
+                a.cy[i] = a.ty[bi[q]];
+            }
+            kmin_c = max(kmin_c, ~k);
+            kmax = max(kmax, k);
+            any = true;
         } else {
             part_d2[(int64_t)blockIdx.y * a.n + i] = best[q];
             part_idx[(int64_t)blockIdx.y * a.n + i] = bi[q];
         }
     }
+    if (gridDim.y == 1 && a.range) range_accumulate(a.range, any, kmin_c, kmax);
 }
 
 __global__ __launch_bounds__(256) void k_nn_merge(NNArgs a, int nchunks, const double *part_d2,
                                                   const int32_t *part_idx) {
     if (a.skip && *a.skip) return;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    double best = INFINITY;
-    int bi = 0x7fffffff;
-    for (int c = 0; c < nchunks; ++c) {  // chunks ascend in index: strict < keeps the lowest
-        const double s = part_d2[(int64_t)c * a.n + i];
-        const int id = part_idx[(int64_t)c * a.n + i];
-        if (s < best || (s == best && id < bi)) {
-            best = s;
-            bi = id;
+    const bool valid = i < a.n;
+    unsigned long long key = 0;
+    if (valid) {
+        double best = INFINITY;
+        int bi = 0x7fffffff;
+        for (int c = 0; c < nchunks; ++c) {  // chunks ascend in index: strict < keeps the lowest
+            const double s = part_d2[(int64_t)c * a.n + i];
+            const int id = part_idx[(int64_t)c * a.n + i];
+            if (s < best || (s == best && id < bi)) {
+                best = s;
+                bi = id;
+            }
+        }
+        key = write_out(a, i, best, bi);
+        if (a.cx) {
+            a.cx[i] = a.tx[bi];
+            a.cy[i] = a.ty[bi];
         }
     }
-    write_out(a, i, best, bi);
+    if (a.range) range_accumulate(a.range, valid, ~key, key);
 }
 
 __global__ __launch_bounds__(256) void k_apply_inplace(double *x, double *y, int64_t n,
@@ -345,6 +376,50 @@ __global__ __launch_bounds__(256) void k_grid_sort_cells(TPt *pts, const int32_t
         }
         pts[b + 1] = v;
     }
+}
+
+// ---------------------------------------------------------------- work order
+__global__ __launch_bounds__(256) void k_src_cellkey(const double *sx, const double *sy,
+                                                     int64_t n, GridView g,
+                                                     unsigned long long *key) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int cx = cell_coord(sx[i], g.x0, g.inv_h, g.gx);
+    const int cy = cell_coord(sy[i], g.y0, g.inv_h, g.gy);
+    const unsigned nstx = (unsigned)(g.gx + 7) >> 3;
+    const unsigned st = ((unsigned)cy >> 3) * nstx + ((unsigned)cx >> 3);
+    const unsigned long long ck = ((unsigned long long)st << 6) | ((cy & 7) << 3) | (cx & 7);
+    key[i] = (ck << 32) | (unsigned long long)i;
+}
+
+__global__ __launch_bounds__(256) void k_gather_work(const uint32_t *perm, const double *sx,
+                                                     const double *sy, const double *sz,
+                                                     int64_t n, double *wx, double *wy,
+                                                     double *wz, uint32_t *worig) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t i = perm[p];
+    wx[p] = sx[i];
+    wy[p] = sy[i];
+    if (sz) wz[p] = sz[i];
+    worig[p] = i;
+}
+
+__global__ __launch_bounds__(256) void k_scatter_xy(const uint32_t *worig, const double *wx,
+                                                    const double *wy, int64_t n, double *sx,
+                                                    double *sy) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t i = worig[p];
+    sx[i] = wx[p];
+    sy[i] = wy[p];
+}
+
+__global__ __launch_bounds__(256) void k_scatter_i32(const uint32_t *worig, const int32_t *w,
+                                                     int64_t n, int32_t *out) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    out[worig[p]] = w[p];
 }
 
 __global__ __launch_bounds__(256) void k_deinterleave(const double *rows, int64_t n, int64_t ld,
@@ -474,6 +549,36 @@ hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hip
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_apply_inplace, dim3(nblk(n)), dim3(256), 0, s, x, y, n, T,
                        (const int *)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_src_cellkey(const double *sx, const double *sy, int64_t n, const GridView &g,
+                              unsigned long long *key, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_src_cellkey, dim3(nblk(n)), dim3(256), 0, s, sx, sy, n, g, key);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_work(const uint32_t *perm, const double *sx, const double *sy,
+                              const double *sz, int64_t n, double *wx, double *wy, double *wz,
+                              uint32_t *worig, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_work, dim3(nblk(n)), dim3(256), 0, s, perm, sx, sy, sz, n, wx, wy,
+                       wz, worig);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_xy(const uint32_t *worig, const double *wx, const double *wy, int64_t n,
+                             double *sx, double *sy, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter_xy, dim3(nblk(n)), dim3(256), 0, s, worig, wx, wy, n, sx, sy);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_i32(const uint32_t *worig, const int32_t *w, int64_t n, int32_t *out,
+                              hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter_i32, dim3(nblk(n)), dim3(256), 0, s, worig, w, n, out);
     return hipGetLastError();
 }
 

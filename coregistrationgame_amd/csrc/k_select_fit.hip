@@ -225,17 +225,19 @@ __global__ __launch_bounds__(256) void k_frac_final(const BestRec *tbest, int nb
 }
 
 // ------------------------------------------------------------------------- fit
+// threshold pair (key, orig) of the k-th entry of the stable order
 __device__ __forceinline__ bool fit_threshold(const FitIn &a, unsigned long long &tk,
-                                              int64_t &ti) {
+                                              int64_t &to) {
     if (!a.key) return true;  // every row selected
     const long long k = a.st->k;
     if (k <= 0) {
         tk = 0;
-        ti = -1;
+        to = -1;
         return false;
     }
-    ti = (int64_t)a.order[k - 1];
-    tk = a.key[ti];
+    const int64_t tp = (int64_t)a.order[k - 1];
+    tk = a.key[tp];
+    to = a.orig ? (int64_t)a.orig[tp] : tp;
     return false;
 }
 
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, const in
             bool sel = all;
             if (!all) {
                 const unsigned long long ki = a.key[i];
-                sel = ki < tk || (ki == tk && i <= ti);
+                sel = ki < tk || (ki == tk && (a.orig ? (int64_t)a.orig[i] : i) <= ti);
             }
             if (sel) {
                 const double xs = a.sx[i] - a.px, ys = a.sy[i] - a.py;

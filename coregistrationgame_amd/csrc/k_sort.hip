@@ -1,35 +1,68 @@
 // k_sort.hip -- the fractional-trim residual sort (ficp.py:63,78: argsort(distances))
 // and the int32 exclusive scan used by the grid build.
 //
-// Sort contract: stable order of (key, val) pairs by the 64-bit order-preserving key of
-// the distance, val = source index, input in index order -> ties end up ordered by
-// index.  Method:
-//   1. stable LSD radix sort of the TOP 32 key bits (4 passes x 8-bit digits; per pass
-//      a tile histogram, a per-digit scan over tiles and a stable scatter that ranks the
-//      tile in LDS with 64-lane ballot matching and writes digit runs coalesced);
-//   2. fix-up: each run of equal top-32 bits is re-ordered by the full 64-bit key with
-//      an insertion sort by the run's first lane (runs are short: the top 32 bits of a
-//      double carry 20 mantissa bits; equal full keys are already in index order).
-// Top-32 + fix-up moves 20 B per item per pass instead of 32 B and halves the passes of
-// a full 64-bit LSD sort.
+// Contract: `order` = work positions sorted by (key64, orig) lexicographically, where
+// key64 is the order-preserving bit pattern of the distance and orig the caller's index
+// of that position -- i.e. numpy's argsort(dist, kind="stable") in caller indices.
+//
+// Method, one launch per 8-bit digit, no global prefix-sum kernels:
+//  0. k_os_hist: derives a 32-bit key (key64 - kmin) >> s from the key range (kmin/kmax
+//     accumulated by the NN kernel, or by k_key_range), scatters (key32, position) into
+//     ORIG order -- so LSD stability alone orders exact ties by orig -- and builds the
+//     four digit histograms at once (they do not depend on the order).
+//  1-4. k_os_pass<P>: single-pass stable scatter per digit ("onesweep"): tiles take ids
+//     in dispatch order from an atomic ticket, rank their items with 64-lane ballot
+//     matching and per-wave LDS counters (no block barrier inside the ranking loop),
+//     publish their digit counts and find their global offsets by decoupled look-back
+//     over predecessor tiles (agent-scope relaxed atomics on 4-byte {flag|count} words:
+//     the data is the flag, MI355X_MICROARCH.md Valid forms / R2), then write digit runs
+//     coalesced from an LDS staging copy.  The last pass also emits r in selection order.
+//  5. k_os_fixup: runs of equal key32 (distinct distances closer than 2^s ulps: rare)
+//     are re-ordered by key64 with a stable insertion sort; resets the key range.
 #include "ficp_internal.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 namespace ficp {
 
 namespace {
 
-constexpr int SB = 256;             // threads per sort block
-constexpr int SI = 16;              // items per thread
-constexpr int STILE = SB * SI;      // items per tile
+constexpr int OB = 256;              // threads per pass block (4 waves)
+constexpr int OIPT = 8;              // items per thread
+constexpr int OTILE = OB * OIPT;     // 2048 items per tile
+constexpr uint32_t F_AGG = 1u << 30;
+constexpr uint32_t F_PRE = 2u << 30;
+constexpr uint32_t F_MASK = 3u << 30;
+constexpr uint32_t C_MASK = F_AGG - 1;
 constexpr int SCAN_I = 16;
 constexpr int SCAN_TILE = 256 * SCAN_I;
 
-__device__ __forceinline__ unsigned long long ordkey(double v) {
-    unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+struct SortWS {
+    uint32_t *kA, *kB, *vB;      // key32 ping-pong, val pong (ping = the caller's order)
+    uint32_t *hist;              // [4][256]
+    uint32_t *status;            // [4][ntiles][256]
+    uint32_t *tickets;           // [4] tile tickets + [1] spin-timeout flag
+    uint32_t *counts;            // [256][ntiles] (reduce-then-scan mode, plain stores only)
+    int ntiles;
+};
+
+// range = {max(~key), max(key)}, accumulated by atomics: read it at the memory side
+__device__ __forceinline__ void load_range(const unsigned long long *range,
+                                           unsigned long long &kmin, unsigned long long &kmax) {
+    unsigned long long *r = const_cast<unsigned long long *>(range);
+    kmin = ~__hip_atomic_fetch_or(&r[0], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    kmax = __hip_atomic_fetch_or(&r[1], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// exclusive scan of one uint32 per thread over a 256-thread block (4 waves)
+__device__ __forceinline__ int key_shift(unsigned long long kmin, unsigned long long kmax) {
+    const unsigned long long span = kmax > kmin ? kmax - kmin : 0ULL;
+    const int bits = span ? 64 - __clzll((long long)span) : 0;
+    return bits > 32 ? bits - 32 : 0;
+}
+
 template <typename T>
 __device__ __forceinline__ T block_excl_scan256(T v, T *s_w /* [4] */, T &total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -48,157 +81,319 @@ __device__ __forceinline__ T block_excl_scan256(T v, T *s_w /* [4] */, T &total)
     return pre + x - v;
 }
 
-template <bool FROM64>
-__device__ __forceinline__ uint32_t load_key(const void *kin, int64_t i) {
-    if (FROM64) return (uint32_t)(((const unsigned long long *)kin)[i] >> 32);
-    return ((const uint32_t *)kin)[i];
-}
-
-template <bool FROM64>
-__global__ __launch_bounds__(SB) void k_radix_hist(const void *kin, int64_t n, int shift,
-                                                   uint32_t *counts, int nb, const int *skip) {
-    if (skip && *skip) return;
-    __shared__ uint32_t s_h[256];
-    s_h[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * STILE;
-    const int cnt = (int)min((int64_t)STILE, n - t0);
-    for (int li = threadIdx.x; li < cnt; li += SB) {
-        const uint32_t k = load_key<FROM64>(kin, t0 + li);
-        atomicAdd(&s_h[(k >> shift) & 255], 1u);
+// key range for callers without a fused producer (API paths): range[0] = max(~key),
+// range[1] = max(key); both start at 0.
+__global__ __launch_bounds__(256) void k_key_range(const unsigned long long *key, int64_t n,
+                                                   unsigned long long *range) {
+    __shared__ unsigned long long s_a[4], s_b[4];
+    unsigned long long a = 0, b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const unsigned long long k = key[i];
+        a = max(a, ~k);
+        b = max(b, k);
+    }
+    wave_range_reduce(a, b);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_a[wave] = a;
+        s_b[wave] = b;
     }
     __syncthreads();
-    counts[(int64_t)threadIdx.x * nb + blockIdx.x] = s_h[threadIdx.x];
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) {
+            a = max(a, s_a[w]);
+            b = max(b, s_b[w]);
+        }
+        atomicMax(&range[0], s_a[0] > a ? s_a[0] : a);
+        atomicMax(&range[1], s_b[0] > b ? s_b[0] : b);
+    }
 }
 
-// one block per digit: exclusive scan of counts[d][0..nb) in place, rowtot[d] = total
-__global__ __launch_bounds__(SB) void k_radix_rowscan(uint32_t *counts, int nb, uint32_t *rowtot,
-                                                      const int *skip) {
+__device__ __forceinline__ void wave_hist_add(uint32_t *h, uint32_t d, bool valid) {
+    // aggregate equal digits of the wave (ballot match) -> one LDS atomic per distinct digit
+    const int lane = threadIdx.x & 63;
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const unsigned long long bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+    }
+    if (valid && __popcll(peers & ((1ULL << lane) - 1ULL)) == 0)
+        atomicAdd(&h[d], (uint32_t)__popcll(peers));
+}
+
+__global__ __launch_bounds__(256) void k_os_hist(const unsigned long long *key64,
+                                                 const uint32_t *orig, int64_t n,
+                                                 const unsigned long long *range, SortWS ws,
+                                                 uint32_t *vout, int64_t status_words,
+                                                 const int *skip) {
+    if (skip && *skip) return;
+    __shared__ uint32_t s_h[4][256];
+    for (int e = threadIdx.x; e < 4 * 256; e += 256) (&s_h[0][0])[e] = 0;
+    // zero the look-back status words and the tickets for the passes that follow; they
+    // are only ever touched by device-scope atomics (plain stores to words that other
+    // kernels update atomically are not reliably ordered with those atomics)
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < status_words;
+         e += (int64_t)gridDim.x * 256)
+        __hip_atomic_exchange(&ws.status[e], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x < 4)  // [4] is the sticky error flag
+        __hip_atomic_exchange(&ws.tickets[threadIdx.x], 0u, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    __shared__ unsigned long long s_rng[2];
+    if (threadIdx.x == 0) load_range(range, s_rng[0], s_rng[1]);
+    __syncthreads();
+    const unsigned long long kmin = s_rng[0];
+    const int s = key_shift(kmin, s_rng[1]);
+    const int64_t nround = (n + 255) / 256;
+    for (int64_t q = blockIdx.x; q < nround; q += gridDim.x) {  // block-uniform trip count
+        const int64_t p = q * 256 + threadIdx.x;
+        const bool valid = p < n;
+        uint32_t k = 0;
+        if (valid) {
+            k = (uint32_t)((key64[p] - kmin) >> s);
+            const int64_t o = orig ? (int64_t)orig[p] : p;
+            ws.kA[o] = k;
+            vout[o] = (uint32_t)p;
+        }
+        wave_hist_add(s_h[0], k & 255u, valid);
+        wave_hist_add(s_h[1], (k >> 8) & 255u, valid);
+        wave_hist_add(s_h[2], (k >> 16) & 255u, valid);
+        wave_hist_add(s_h[3], k >> 24, valid);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 4 * 256; e += 256) {
+        const uint32_t c = (&s_h[0][0])[e];
+        if (c) atomicAdd(&ws.hist[e], c);
+    }
+}
+
+// LB = true: onesweep (tile ids from tickets, offsets by decoupled look-back).
+// LB = false: reduce-then-scan (tile = blockIdx.x, offsets from excl_tab[digit][tile]
+// built by k_rs_count + k_rs_rowscan; no communication between workgroups of a launch).
+template <int PASS, bool LB>
+__global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint32_t *vin,
+                                                uint32_t *kout, uint32_t *vout, int64_t n,
+                                                SortWS ws, const uint32_t *excl_tab,
+                                                const double *r, double *rs, const int *skip) {
+    if (skip && *skip) return;
+    constexpr int SH = 8 * PASS;
+    __shared__ uint32_t s_k[OTILE];
+    __shared__ uint32_t s_v[OTILE];
+    __shared__ uint32_t s_cnt[4][256];
+    __shared__ uint32_t s_loc[256];
+    __shared__ uint32_t s_gb[256];
+    __shared__ uint32_t s_w[4];
+    __shared__ int s_tile;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = LB ? (int)atomicAdd(&ws.tickets[PASS], 1u) : (int)blockIdx.x;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s_cnt[w][tid] = 0;
+    // digit base = exclusive scan of this pass's global histogram (built by atomics:
+    // read it at the memory side too)
+    uint32_t htot;
+    const uint32_t hv = __hip_atomic_fetch_or(&ws.hist[PASS * 256 + tid], 0u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t dbase = block_excl_scan256<uint32_t>(hv, s_w, htot);
+    const int t = s_tile;  // the scan's barriers published s_tile and s_cnt
+    if (t >= ws.ntiles) {  // cannot happen with reset tickets; never write out of bounds
+        if (tid == 0) atomicOr(&ws.tickets[4], 4u);
+        return;
+    }
+    const int64_t t0 = (int64_t)t * OTILE;
+    const int cnt = (int)min((int64_t)OTILE, n - t0);
+
+    // ---- load + rank (stable) without block barriers
+    uint32_t k[OIPT], v[OIPT], rk[OIPT];
+    const unsigned long long lt = (1ULL << lane) - 1ULL;
+#pragma unroll
+    for (int j = 0; j < OIPT; ++j) {
+        const int li = wave * (OIPT * 64) + j * 64 + lane;
+        const bool valid = li < cnt;
+        k[j] = valid ? kin[t0 + li] : 0u;
+        v[j] = valid ? vin[t0 + li] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < OIPT; ++j) {
+        const int li = wave * (OIPT * 64) + j * 64 + lane;
+        const bool valid = li < cnt;
+        const uint32_t d = (k[j] >> SH) & 255u;
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t old = s_cnt[wave][d];
+        const int lr = __popcll(peers & lt);
+        rk[j] = old + (uint32_t)lr;
+        if (valid && lr == 0) s_cnt[wave][d] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // ---- per digit (thread = digit): wave offsets, tile count, look-back
+    const uint32_t c0 = s_cnt[0][tid], c1 = s_cnt[1][tid], c2 = s_cnt[2][tid], c3 = s_cnt[3][tid];
+    const uint32_t mine = c0 + c1 + c2 + c3;
+    uint32_t excl = 0;
+    if (!LB) {
+        excl = excl_tab[(int64_t)tid * ws.ntiles + t];
+    } else {
+    uint32_t *st = ws.status + ((int64_t)PASS * ws.ntiles + t) * 256 + tid;
+    // Status words are published and polled with device-scope atomic RMWs: atomics are
+    // performed at the memory side, so a poll can never be served by a stale copy of the
+    // line in this XCD's L2 (plain/sc1 loads can: the per-XCD L2s are not coherent).
+    if (t == 0) {
+        __hip_atomic_exchange(st, F_PRE | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_exchange(st, F_AGG | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t *prev = st - 256;
+        unsigned spins = 0;
+        for (int j = t - 1; j >= 0; --j, prev -= 256) {
+            uint32_t w;
+            for (;;) {
+                w = __hip_atomic_fetch_or(prev, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (w & F_MASK) break;
+                if (++spins > (1u << 20)) {  // bounded: never hang the device
+                    __hip_atomic_exchange(&ws.tickets[4], 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    w = F_PRE;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            excl += w & C_MASK;
+            if (w & F_PRE) break;
+        }
+        __hip_atomic_exchange(st, F_PRE | (excl + mine), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    }
+    }  // LB
+    s_gb[tid] = dbase + excl;
+    s_cnt[0][tid] = 0;
+    s_cnt[1][tid] = c0;
+    s_cnt[2][tid] = c0 + c1;
+    s_cnt[3][tid] = c0 + c1 + c2;
+    uint32_t ltot;
+    s_loc[tid] = block_excl_scan256<uint32_t>(mine, s_w, ltot);  // barriers publish s_*
+    // ---- stage the tile in LDS in output order, then write digit runs coalesced
+#pragma unroll
+    for (int j = 0; j < OIPT; ++j) {
+        const int li = wave * (OIPT * 64) + j * 64 + lane;
+        if (li < cnt) {
+            const uint32_t d = (k[j] >> SH) & 255u;
+            const uint32_t pos = s_loc[d] + s_cnt[wave][d] + rk[j];
+            s_k[pos] = k[j];
+            s_v[pos] = v[j];
+        }
+    }
+    __syncthreads();
+    for (int p = tid; p < cnt; p += OB) {
+        const uint32_t kk = s_k[p];
+        const uint32_t d = (kk >> SH) & 255u;
+        const uint32_t g = s_gb[d] + ((uint32_t)p - s_loc[d]);
+        const uint32_t vv = s_v[p];
+        if (g >= (uint64_t)n || vv >= (uint64_t)n) {  // inconsistent offsets: flag, never fault
+            atomicOr(&ws.tickets[4], 8u);
+            continue;
+        }
+        kout[g] = kk;
+        vout[g] = vv;
+        if (rs) rs[g] = r[vv];
+    }
+}
+
+// reduce-then-scan: per-tile digit counts of pass PASS -> counts[digit][tile]
+template <int PASS>
+__global__ __launch_bounds__(OB) void k_rs_count(const uint32_t *kin, int64_t n, uint32_t *counts,
+                                                 int ntiles, const int *skip) {
+    if (skip && *skip) return;
+    constexpr int SH = 8 * PASS;
+    __shared__ uint32_t s_h[256];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    s_h[tid] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * OTILE;
+    const int cnt = (int)min((int64_t)OTILE, n - t0);
+#pragma unroll
+    for (int j = 0; j < OIPT; ++j) {
+        const int li = wave * (OIPT * 64) + j * 64 + lane;
+        const bool valid = li < cnt;
+        const uint32_t k = valid ? kin[t0 + li] : 0u;
+        wave_hist_add(s_h, (k >> SH) & 255u, valid);
+    }
+    __syncthreads();
+    counts[(int64_t)tid * ntiles + blockIdx.x] = s_h[tid];
+}
+
+// one block per digit: exclusive scan over the tiles, in place
+__global__ __launch_bounds__(256) void k_rs_rowscan(uint32_t *counts, int ntiles, const int *skip) {
     if (skip && *skip) return;
     __shared__ uint32_t s_w[4];
-    uint32_t *row = counts + (int64_t)blockIdx.x * nb;
-    const int per = (nb + SB - 1) / SB;
+    uint32_t *row = counts + (int64_t)blockIdx.x * ntiles;
+    const int per = (ntiles + 255) / 256;
     const int b0 = threadIdx.x * per;
     uint32_t sum = 0;
-    for (int b = b0; b < min(nb, b0 + per); ++b) sum += row[b];
+    for (int b = b0; b < min(ntiles, b0 + per); ++b) sum += row[b];
     uint32_t total;
     uint32_t pre = block_excl_scan256<uint32_t>(sum, s_w, total);
-    for (int b = b0; b < min(nb, b0 + per); ++b) {
+    for (int b = b0; b < min(ntiles, b0 + per); ++b) {
         const uint32_t c = row[b];
         row[b] = pre;
         pre += c;
     }
-    if (threadIdx.x == 0) rowtot[blockIdx.x] = total;
 }
 
-template <bool FROM64>
-__global__ __launch_bounds__(SB) void k_radix_scatter(const void *kin, const uint32_t *vin,
-                                                      int64_t n, int shift,
-                                                      const uint32_t *counts,
-                                                      const uint32_t *rowtot, int nb,
-                                                      uint32_t *kout, uint32_t *vout,
-                                                      const double *rin, double *rout,
-                                                      const int *skip) {
-    if (skip && *skip) return;
-    __shared__ uint32_t s_k[STILE];
-    __shared__ uint32_t s_v[STILE];
-    __shared__ uint32_t s_base[256];
-    __shared__ uint32_t s_loc[256];
-    __shared__ uint32_t s_run[256];
-    __shared__ uint32_t s_wc[4][256];
-    __shared__ uint32_t s_w[4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t t0 = (int64_t)blockIdx.x * STILE;
-    const int cnt = (int)min((int64_t)STILE, n - t0);
-
-    const uint32_t tot = rowtot[tid];
-    const uint32_t mine = counts[(int64_t)tid * nb + blockIdx.x];
-    const uint32_t nxt = (blockIdx.x + 1 < (unsigned)nb) ? counts[(int64_t)tid * nb + blockIdx.x + 1] : tot;
-    uint32_t dummy;
-    const uint32_t ex_tot = block_excl_scan256<uint32_t>(tot, s_w, dummy);
-    const uint32_t ex_loc = block_excl_scan256<uint32_t>(nxt - mine, s_w, dummy);
-    s_base[tid] = ex_tot + mine;
-    s_loc[tid] = ex_loc;
-    s_run[tid] = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) s_wc[w][tid] = 0;
-    __syncthreads();
-
-    const unsigned long long lt = (1ULL << lane) - 1ULL;
-    for (int r = 0; r < SI; ++r) {
-        const int li = r * SB + tid;
-        const bool valid = li < cnt;
-        uint32_t k = 0, v = 0;
-        int d = 0;
-        if (valid) {
-            k = load_key<FROM64>(kin, t0 + li);
-            v = vin ? vin[t0 + li] : (uint32_t)(t0 + li);
-            d = (k >> shift) & 255;
-        }
-        unsigned long long peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1;
-            const unsigned long long bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const int lrank = __popcll(peers & lt);
-        if (valid && lrank == 0) s_wc[wave][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pre = s_run[d];
-            for (int w = 0; w < wave; ++w) pre += s_wc[w][d];
-            const uint32_t pos = s_loc[d] + pre + (uint32_t)lrank;
-            s_k[pos] = k;
-            s_v[pos] = v;
-        }
-        __syncthreads();
-        s_run[tid] += s_wc[0][tid] + s_wc[1][tid] + s_wc[2][tid] + s_wc[3][tid];
-#pragma unroll
-        for (int w = 0; w < 4; ++w) s_wc[w][tid] = 0;
-        __syncthreads();
-    }
-    for (int li = tid; li < cnt; li += SB) {
-        const uint32_t k = s_k[li];
-        const int d = (k >> shift) & 255;
-        const uint32_t g = s_base[d] + ((uint32_t)li - s_loc[d]);
-        kout[g] = k;
-        vout[g] = s_v[li];
-        if (rout) rout[g] = rin[s_v[li]];  // last pass: residuals in selection order
-    }
-}
-
-// runs of equal top-32 bits: order by the full key (stable insertion sort by the run head)
-__global__ __launch_bounds__(256) void k_sort_fixup(const uint32_t *k32, uint32_t *val,
-                                                    const unsigned long long *key64,
-                                                    const double *rin, double *rout, int64_t n,
-                                                    const int *skip) {
+// Runs of equal key32 hold distinct distances closer than 2^s ulps: order them by the
+// full key (stable: equal key64 keep their orig order).  Also resets the key range.
+__global__ __launch_bounds__(256) void k_os_fixup(const uint32_t *k32, uint32_t *val,
+                                                  const unsigned long long *key64,
+                                                  const double *r, double *rs, int64_t n,
+                                                  unsigned long long *range_reset,
+                                                  const int *skip) {
     if (skip && *skip) return;
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j == 0 && range_reset) {  // atomic-only word: reset with atomics too
+        __hip_atomic_exchange(&range_reset[0], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_exchange(&range_reset[1], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (j + 1 >= n) return;
     const uint32_t kj = k32[j];
     if (k32[j + 1] != kj) return;
     if (j > 0 && k32[j - 1] == kj) return;  // not the head of the run
     int64_t e = j + 1;
     while (e < n && k32[e] == kj) ++e;
+    bool moved = false;
     for (int64_t a = j + 1; a < e; ++a) {
         const uint32_t v = val[a];
         const unsigned long long kv = key64[v];
         int64_t b = a - 1;
         while (b >= j) {
             const uint32_t vb = val[b];
-            const unsigned long long kb = key64[vb];
-            if (kb > kv || (kb == kv && vb > v)) {
+            if (key64[vb] > kv) {
                 val[b + 1] = vb;
                 --b;
+                moved = true;
             } else {
                 break;
             }
         }
         val[b + 1] = v;
     }
-    if (rout)
-        for (int64_t a = j; a < e; ++a) rout[a] = rin[val[a]];
+    if (rs && moved)
+        for (int64_t a = j; a < e; ++a) rs[a] = r[val[a]];
+}
+
+// Resets of words that kernels update with atomics (histograms, counters, key ranges,
+// flags): done with atomics, never with memset or plain stores.
+__global__ __launch_bounds__(256) void k_atomic_zero32(uint32_t *p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        __hip_atomic_exchange(&p[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_atomic_zero64(unsigned long long *p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        __hip_atomic_exchange(&p[i], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void k_keys_from_doubles(const double *d, int64_t n,
@@ -207,17 +402,26 @@ __global__ __launch_bounds__(256) void k_keys_from_doubles(const double *d, int6
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     key[i] = ordkey(d[i]);
-    val[i] = (uint32_t)i;
+    if (val) val[i] = (uint32_t)i;
 }
 
 // ------------------------------------------------------------- int32 exclusive scan
+template <bool ATOMIC_IN>
+__device__ __forceinline__ int32_t scan_load(const int32_t *in, int64_t i) {
+    if (ATOMIC_IN)
+        return __hip_atomic_fetch_or(const_cast<int32_t *>(in) + i, 0, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    return in[i];
+}
+
+template <bool ATOMIC_IN>
 __global__ __launch_bounds__(256) void k_scan_partial(const int32_t *in, int64_t n, int32_t *bsum) {
     __shared__ int32_t s_w[4];
     const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
     int32_t s = 0;
 #pragma unroll
     for (int q = 0; q < SCAN_I; ++q)
-        if (t0 + q < n) s += in[t0 + q];
+        if (t0 + q < n) s += scan_load<ATOMIC_IN>(in, t0 + q);
     int32_t total;
     block_excl_scan256<int32_t>(s, s_w, total);
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
@@ -239,6 +443,7 @@ __global__ __launch_bounds__(256) void k_scan_bsums(int32_t *bsum, int nb) {
     if (threadIdx.x == 0) bsum[nb] = total;
 }
 
+template <bool ATOMIC_IN>
 __global__ __launch_bounds__(256) void k_scan_final(const int32_t *in, int32_t *out, int64_t n,
                                                     const int32_t *bsum, int nb) {
     __shared__ int32_t s_w[4];
@@ -247,7 +452,7 @@ __global__ __launch_bounds__(256) void k_scan_final(const int32_t *in, int32_t *
     int32_t s = 0;
 #pragma unroll
     for (int q = 0; q < SCAN_I; ++q) {
-        v[q] = (t0 + q < n) ? in[t0 + q] : 0;
+        v[q] = (t0 + q < n) ? scan_load<ATOMIC_IN>(in, t0 + q) : 0;
         s += v[q];
     }
     int32_t total;
@@ -261,76 +466,132 @@ __global__ __launch_bounds__(256) void k_scan_final(const int32_t *in, int32_t *
 }
 
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+SortWS carve(void *tmp, int64_t n) {
+    SortWS w{};
+    w.ntiles = (int)((n + OTILE - 1) / OTILE);
+    char *p = (char *)tmp;
+    w.kA = (uint32_t *)p;
+    p += align_up(n * 4, 256);
+    w.kB = (uint32_t *)p;
+    p += align_up(n * 4, 256);
+    w.vB = (uint32_t *)p;
+    p += align_up(n * 4, 256);
+    w.hist = (uint32_t *)p;
+    p += 4 * 256 * 4;
+    w.tickets = (uint32_t *)p;
+    p += 256;
+    w.status = (uint32_t *)p;
+    p += align_up(4LL * w.ntiles * 256 * 4, 256);
+    w.counts = (uint32_t *)p;
+    return w;
+}
 
 }  // namespace
 
 int64_t scan_tmp_elems(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
 hipError_t launch_scan_i32(const int32_t *in, int32_t *out, int64_t n, int32_t *tmp,
-                           hipStream_t s) {
+                           bool atomic_in, hipStream_t s) {
     const int nb = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
     if (nb == 0) {
         hipMemsetAsync(out, 0, sizeof(int32_t), s);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_scan_partial, dim3(nb), dim3(256), 0, s, in, n, tmp);
+    if (atomic_in)
+        hipLaunchKernelGGL(k_scan_partial<true>, dim3(nb), dim3(256), 0, s, in, n, tmp);
+    else
+        hipLaunchKernelGGL(k_scan_partial<false>, dim3(nb), dim3(256), 0, s, in, n, tmp);
     hipLaunchKernelGGL(k_scan_bsums, dim3(1), dim3(256), 0, s, tmp, nb);
-    hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(256), 0, s, in, out, n, tmp, nb);
+    if (atomic_in)
+        hipLaunchKernelGGL(k_scan_final<true>, dim3(nb), dim3(256), 0, s, in, out, n, tmp, nb);
+    else
+        hipLaunchKernelGGL(k_scan_final<false>, dim3(nb), dim3(256), 0, s, in, out, n, tmp, nb);
     return hipGetLastError();
 }
 
-static inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
-
-int64_t sort_tmp_bytes(int64_t n) {
-    const int64_t nb = (n + STILE - 1) / STILE;
-    return 3 * align_up(n * 4, 256) + align_up(256 * nb * 4, 256) + 256 * 4 + 256;
+hipError_t launch_atomic_zero32(uint32_t *p, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int nb = (int)std::min<int64_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(k_atomic_zero32, dim3(nb), dim3(256), 0, s, p, n);
+    return hipGetLastError();
 }
 
-hipError_t launch_sort_pairs(const unsigned long long *key, const uint32_t *val_in, int64_t n,
-                             uint32_t *val_out, const double *r_in, double *r_sorted, void *tmp,
-                             const int *skip, hipStream_t s) {
+hipError_t launch_atomic_zero64(unsigned long long *p, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int nb = (int)std::min<int64_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(k_atomic_zero64, dim3(nb), dim3(256), 0, s, p, n);
+    return hipGetLastError();
+}
+
+uint32_t *sort_timeout_flag(void *tmp, int64_t n) { return carve(tmp, n).tickets + 4; }
+
+int64_t sort_tmp_bytes(int64_t n) {
+    const int64_t nt = (n + OTILE - 1) / OTILE;
+    return 3 * align_up(n * 4, 256) + 4 * 256 * 4 + 256 + align_up(4 * nt * 256 * 4, 256) +
+           nt * 256 * 4 + 256;
+}
+
+hipError_t launch_key_range(const unsigned long long *key, int64_t n, unsigned long long *range,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_atomic_zero64, dim3(1), dim3(256), 0, s, range, (int64_t)2);
+    if (n == 0) return hipGetLastError();
+    const int nb = (int)std::min<int64_t>(512, (n + 255) / 256);
+    hipLaunchKernelGGL(k_key_range, dim3(nb), dim3(256), 0, s, key, n, range);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, int64_t n,
+                       unsigned long long *range, uint32_t *order, const double *r, double *rs,
+                       void *tmp, const int *skip, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const int nb = (int)((n + STILE - 1) / STILE);
-    char *p = (char *)tmp;
-    uint32_t *kA = (uint32_t *)p;
-    p += align_up(n * 4, 256);
-    uint32_t *kB = (uint32_t *)p;
-    p += align_up(n * 4, 256);
-    uint32_t *vB = (uint32_t *)p;
-    p += align_up(n * 4, 256);
-    uint32_t *counts = (uint32_t *)p;
-    p += align_up((int64_t)256 * nb * 4, 256);
-    uint32_t *rowtot = (uint32_t *)p;
-    // pass 0: from the u64 keys (bits 32..39) into B; then B->A(val_out), A->B, B->A
-    const void *kin = key;
-    const uint32_t *vin = val_in;
-    uint32_t *kouts[4] = {kB, kA, kB, kA};
-    uint32_t *vouts[4] = {vB, val_out, vB, val_out};
-    for (int pass = 0; pass < 4; ++pass) {
-        const int shift = 8 * pass;
-        if (pass == 0) {
-            hipLaunchKernelGGL(k_radix_hist<true>, dim3(nb), dim3(SB), 0, s, kin, n, shift, counts,
-                               nb, skip);
-        } else {
-            hipLaunchKernelGGL(k_radix_hist<false>, dim3(nb), dim3(SB), 0, s, kin, n, shift,
-                               counts, nb, skip);
-        }
-        hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(SB), 0, s, counts, nb, rowtot, skip);
-        if (pass == 0) {
-            hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(SB), 0, s, kin, vin, n, shift,
-                               counts, rowtot, nb, kouts[pass], vouts[pass],
-                               (const double *)nullptr, (double *)nullptr, skip);
-        } else {
-            hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nb), dim3(SB), 0, s, kin, vin, n,
-                               shift, counts, rowtot, nb, kouts[pass], vouts[pass],
-                               pass == 3 ? r_in : (const double *)nullptr,
-                               pass == 3 ? r_sorted : (double *)nullptr, skip);
-        }
-        kin = kouts[pass];
-        vin = vouts[pass];
-    }
-    hipLaunchKernelGGL(k_sort_fixup, dim3(nblk(n)), dim3(256), 0, s, kA, val_out, key, r_in,
-                       r_sorted, n, skip);
+    static const int dbg = getenv("FICP_SORT_SYNC") ? atoi(getenv("FICP_SORT_SYNC")) : 0;
+    // FICP_SORT=onesweep selects the single-launch-per-digit look-back passes (DESIGN.md
+    // §4.2); the default reduce-then-scan passes need no inter-workgroup communication
+    static const bool onesweep = getenv("FICP_SORT") && !strcmp(getenv("FICP_SORT"), "onesweep");
+    auto step = [&]() {
+        if (dbg) (void)hipStreamSynchronize(s);
+    };
+    SortWS w = carve(tmp, n);
+    hipLaunchKernelGGL(k_atomic_zero32, dim3(4), dim3(256), 0, s, w.hist, (int64_t)(4 * 256));
+    step();
+    const int64_t status_words = onesweep ? 4LL * w.ntiles * 256 : 0;
+    const int hb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 2047) / 2048));
+    hipLaunchKernelGGL(k_os_hist, dim3(hb), dim3(256), 0, s, key64, orig, n,
+                       (const unsigned long long *)range, w, order, status_words, skip);
+    step();
+    // ping = (kA, order), pong = (kB, vB): four passes end back in (kA, order)
+    const dim3 g(w.ntiles), b(OB);
+    const uint32_t *kins[4] = {w.kA, w.kB, w.kA, w.kB};
+    const uint32_t *vins[4] = {order, w.vB, order, w.vB};
+    uint32_t *kouts[4] = {w.kB, w.kA, w.kB, w.kA};
+    uint32_t *vouts[4] = {w.vB, order, w.vB, order};
+#define FICP_PASS(P)                                                                          \
+    if (onesweep) {                                                                           \
+        hipLaunchKernelGGL((k_os_pass<P, true>), g, b, 0, s, kins[P], vins[P], kouts[P],      \
+                           vouts[P], n, w, (const uint32_t *)nullptr,                         \
+                           P == 3 ? r : (const double *)nullptr,                              \
+                           P == 3 ? rs : (double *)nullptr, skip);                            \
+    } else {                                                                                  \
+        hipLaunchKernelGGL(k_rs_count<P>, g, b, 0, s, kins[P], n, w.counts, w.ntiles, skip);  \
+        step();                                                                               \
+        hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles, skip); \
+        step();                                                                               \
+        hipLaunchKernelGGL((k_os_pass<P, false>), g, b, 0, s, kins[P], vins[P], kouts[P],     \
+                           vouts[P], n, w, (const uint32_t *)w.counts,                        \
+                           P == 3 ? r : (const double *)nullptr,                              \
+                           P == 3 ? rs : (double *)nullptr, skip);                            \
+    }                                                                                         \
+    step();
+    FICP_PASS(0)
+    FICP_PASS(1)
+    FICP_PASS(2)
+    FICP_PASS(3)
+#undef FICP_PASS
+    hipLaunchKernelGGL(k_os_fixup, dim3(nblk(n)), dim3(256), 0, s, w.kA, order, key64, r, rs, n,
+                       range, skip);
+    step();
     return hipGetLastError();
 }
 

@@ -41,7 +41,10 @@ WORKLOADS = {
            "C3: 1M trees vs 1M CHM stems, f=0.6, md=3, run() to convergence (threshold 1e-6)"),
     "c2": (100_000, 100_000, 0.8, 100_000, 3, float("-inf"), 25,
            "C2: 100k trees vs 100k CHM stems, f=0.8, md=3, exactly 2x25 loop bodies"),
+    "batch": (10_000, 10_000, 0.8, 10_000_000, 3, 1e-6, 1000,
+              "C4: 1024 plots of 10k trees vs 10k CHM stems, f=0.8, md=3, per-plot run() to convergence"),
 }
+BATCH_PLOTS = 1024
 
 
 def dist_env():
@@ -96,6 +99,122 @@ def cpu_baseline(plot, threads):
                       f"{threads} OpenMP threads"}
 
 
+def cpu_baseline_batch(plots, threads, budget_s=15.0):
+    """The C oracle on the first plots of this rank's share, one run() each, until the
+    time budget is spent (bounded sample); iterations/s = its loop bodies / time."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import ficp_oracle
+    ficp_oracle.build()
+    fits = done = 0
+    t0 = time.perf_counter()
+    for pl in plots:
+        _, tr = ficp_oracle.run(pl.source, pl.target, nthreads=threads, trace=True)
+        fits += tr["n_fits"]
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": fits / dt, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": f"{done} C4 plots (10k x 10k, md=3), full run() each: {fits} loop bodies in "
+                      f"{dt:.2f} s; kd-tree built once per plot, O(N) FRMSD scan, {threads} OpenMP threads"}
+
+
+def bench_batch(args, rank, world, local, dist):
+    """C4: the batch is dealt over ranks (shard.deal_plots); each rank runs its plots in
+    one ficp_run_batch_device per step; no collective on the data path."""
+    from coregistrationgame_amd import shard
+    n, m, f, seed0, md, thr, max_it, desc = WORKLOADS["batch"]
+    nplots = args.plots or BATCH_PLOTS
+    deal = shard.deal_plots(np.full(nplots, float(n) * m), world)
+    mine = deal[rank]
+    plots = [synth.make_plot(n, m, f, seed0 + int(p), md=md) for p in mine]
+    ctx = _lib.Context(local)
+    so = np.zeros(len(plots) + 1, np.int64)
+    to = np.zeros(len(plots) + 1, np.int64)
+    so[1:] = np.cumsum([len(pl.source) for pl in plots])
+    to[1:] = np.cumsum([len(pl.target) for pl in plots])
+    S = np.concatenate([pl.source for pl in plots])
+    T = np.concatenate([pl.target for pl in plots])
+    src0 = [DevArray(ctx, S[:, j]) for j in range(md)]
+    src = [DevArray(ctx, S[:, j]) for j in range(md)]
+    tgt = [DevArray(ctx, T[:, j]) for j in range(md)]
+    lam = [3.0, 0.95 if md == 3 else 1.3]
+
+    def step():
+        src[0].copy_from(src0[0])
+        src[1].copy_from(src0[1])
+        return ctx.run_batch_device(so, src[0].ptr, src[1].ptr, src[2].ptr if md == 3 else 0, to,
+                                    tgt[0].ptr, tgt[1].ptr, tgt[2].ptr if md == 3 else 0, md, lam, thr, max_it)
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.profile_report()
+    ctx.profile_enable(_lib.PROF_NN | _lib.PROF_SORT | _lib.PROF_FRAC | _lib.PROF_FIT)
+    barrier()
+    t0 = time.perf_counter()
+    fits = calls = 0
+    last = None
+    for _ in range(args.steps):
+        last = step()
+        fits += int(last["n_fits"].sum())
+        calls += int(last["n_nn_calls"].sum())
+    barrier()
+    dt = time.perf_counter() - t0
+    ctx.profile_enable(0)
+    prof = json.loads(ctx.profile_report())
+    tot = np.array([dt, fits, calls], dtype=np.float64)
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        c = torch.tensor([float(fits), float(calls)], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        tot = np.array([t.item(), c[0].item(), c[1].item()])
+        # one all-gather of the per-plot records (SURVEY.md §8(e)), outside the timed region
+        shard.gather_plot_stats(deal, last, rank, device=f"cuda:{local}")
+    dt_max, fits_all, calls_all = tot
+    if rank == 0:
+        nn = prof.get("nn_grid_batch") or {"count": 0, "ms": 0.0}
+        avg_ms = nn["ms"] / max(nn["count"], 1)
+        n_loc = int(so[-1])
+        bytes_launch = nn_bytes_per_launch(n_loc, int(to[-1]), md)
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        out = {
+            "metric": METRIC, "value": fits_all / dt_max, "unit": "iterations/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * dt_max / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic (SURVEY.md §8(d) generator, seeds {seed0}+plot, geo-referenced)",
+            "config": {"workload": desc, "plots": nplots, "plots_per_rank": len(mine), "n_trees": n,
+                       "n_chm": m, "inlier_fraction": f, "match_dims": md,
+                       "parallelism": f"plots dealt over {world} GPU(s), no data-path collective"},
+            "iterations_per_step": fits_all / args.steps,
+            "nn_calls_per_step": calls_all / args.steps,
+            "correspondences_per_s": calls_all * n / dt_max,
+            "roofline": {"bound": "hbm", "kernel": "nn_grid_batch (fused apply + exact 1-NN, all plots)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_us": avg_ms * 1e3,
+                         "launches": nn["count"], "algorithmic_bytes_per_launch": bytes_launch,
+                         "note": "bytes count every tree of the rank as live"},
+            "kernel_ms": prof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline_batch(plots, threads)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    for a in src0 + src + tgt:
+        a.free()
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,6 +224,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nn-mode", default="grid", choices=["auto", "brute", "grid"])
+    ap.add_argument("--plots", type=int, default=0, help="batch workload: number of plots (default 1024)")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -116,6 +236,12 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    if args.workload == "batch":
+        bench_batch(args, rank, world, local, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     n, m, f, seed0, md, thr, max_it, desc = WORKLOADS[args.workload]
     plot = synth.make_plot(n, m, f, seed0 + rank, md=md)

@@ -51,6 +51,14 @@ class Stats(C.Structure):
     ]
 
 
+# struct ficp_plot_stats (include/ficp.h) as a numpy record: one row per plot of a batch
+PLOT_STATS_DTYPE = np.dtype([
+    ("T_total", np.float64, (9,)), ("frmsd_last", np.float64), ("k_last", np.int64),
+    ("n_nn_calls", np.int32), ("n_fits", np.int32), ("iters", np.int32, (2,)),
+], align=True)
+assert PLOT_STATS_DTYPE.itemsize == 104
+
+
 def header_symbols() -> list[str]:
     """Every entry point declared in include/ficp.h."""
     txt = HEADER.read_text()
@@ -103,6 +111,10 @@ def lib():
                      C.c_int),
         "ficp_run_device": ([_vp, _vp, _vp, _vp, _i64, _i32, _dp, C.c_double, _i32, _i32,
                              C.POINTER(Stats)], C.c_int),
+        "ficp_run_batch": ([_vp, _i32, _ip64, _dp, _i64, _ip64, _dp, _i64, _i32, _i32, _dp, C.c_double,
+                            _i32, _i32, _vp], C.c_int),
+        "ficp_run_batch_device": ([_vp, _i32, _ip64, _vp, _vp, _vp, _ip64, _vp, _vp, _vp, _i32, _i32, _dp,
+                                   C.c_double, _i32, _i32, _vp], C.c_int),
         "ficp_dev_alloc": ([_vp, _i64, C.POINTER(_vp)], C.c_int),
         "ficp_dev_free": ([_vp, _vp], C.c_int),
         "ficp_memcpy_h2d": ([_vp, _vp, _vp, _i64], C.c_int),
@@ -267,6 +279,36 @@ class Context:
                                      float(threshold), int(max_iterations), int(bool(allow_reflection)),
                                      C.byref(st)))
         return _stats_dict(st, keep, n)
+
+    def run_batch(self, src_off, src_inout: np.ndarray, tgt_off, tgt: np.ndarray, md: int, lambdas,
+                  threshold: float, max_iterations: int, allow_reflection: bool = False) -> np.ndarray:
+        """ficp_run_batch: plots concatenated in src_inout/tgt, delimited by the offsets."""
+        assert src_inout.dtype == np.float64 and src_inout.flags.c_contiguous and src_inout.ndim == 2
+        tgt = np.ascontiguousarray(tgt, dtype=np.float64)
+        so = np.ascontiguousarray(src_off, dtype=np.int64)
+        to = np.ascontiguousarray(tgt_off, dtype=np.int64)
+        if so.ndim != 1 or so.shape != to.shape or len(so) < 2:
+            raise ValueError("offset arrays must be 1-D, equal length >= 2")
+        lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+        out = np.zeros(len(so) - 1, PLOT_STATS_DTYPE)
+        _check(lib().ficp_run_batch(self.h, len(so) - 1, _p(so, _ip64), _p(src_inout), len(src_inout) and src_inout.shape[1],
+                                    _p(to, _ip64), _p(tgt), len(tgt) and tgt.shape[1], int(md), len(lam), _p(lam),
+                                    float(threshold), int(max_iterations), int(bool(allow_reflection)),
+                                    _vp(out.ctypes.data)))
+        return out
+
+    def run_batch_device(self, src_off, x_ptr: int, y_ptr: int, z_ptr: int, tgt_off, tx_ptr: int, ty_ptr: int,
+                         tz_ptr: int, md: int, lambdas, threshold: float, max_iterations: int,
+                         allow_reflection: bool = False) -> np.ndarray:
+        so = np.ascontiguousarray(src_off, dtype=np.int64)
+        to = np.ascontiguousarray(tgt_off, dtype=np.int64)
+        lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+        out = np.zeros(len(so) - 1, PLOT_STATS_DTYPE)
+        _check(lib().ficp_run_batch_device(self.h, len(so) - 1, _p(so, _ip64), _vp(x_ptr), _vp(y_ptr), _vp(z_ptr or 0),
+                                           _p(to, _ip64), _vp(tx_ptr), _vp(ty_ptr), _vp(tz_ptr or 0), int(md),
+                                           len(lam), _p(lam), float(threshold), int(max_iterations),
+                                           int(bool(allow_reflection)), _vp(out.ctypes.data)))
+        return out
 
     def synchronize(self):
         _check(lib().ficp_synchronize(self.h))

@@ -4,7 +4,7 @@
 // the device; per iteration the host reads back one small IterState (k, FRMSD, T) to
 // take the convergence decision `current - new <= threshold` (ficp.py:142).
 #include "../../include/ficp.h"
-#include "ficp_internal.h"
+#include "capi_internal.h"
 
 #include <math.h>
 #include <stdarg.h>
@@ -19,160 +19,13 @@
 
 using namespace ficp;
 
-namespace {
+using namespace ficp_capi;
 
+namespace ficp_capi {
 thread_local std::string g_err;
-
-int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char *fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    return code;
-}
-
-#define HIPCHK(expr)                                                                       \
-    do {                                                                                   \
-        hipError_t e_ = (expr);                                                            \
-        if (e_ != hipSuccess)                                                              \
-            return fail(FICP_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                        __FILE__, __LINE__);                                               \
-    } while (0)
-
-#define CHK(expr)                     \
-    do {                              \
-        int r_ = (expr);              \
-        if (r_ != FICP_OK) return r_; \
-    } while (0)
-
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    int ensure(size_t bytes) {
-        if (bytes <= cap && p) return FICP_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(bytes, 256);
-        hipError_t e = hipMalloc(&p, want);
-        if (e != hipSuccess) {
-            p = nullptr;
-            return fail(FICP_ENOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
-        }
-        cap = want;
-        return FICP_OK;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    template <typename T>
-    T *as() const {
-        return (T *)p;
-    }
-};
-
-enum ProfClass { P_NN = 1, P_SORT = 2, P_FRAC = 4, P_FIT = 8, P_GRID = 16, P_MISC = 32 };
-
-struct ProfRec {
-    const char *name;
-    hipEvent_t a, b;
-};
-
-}  // namespace
-
-struct ficp_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    int nn_mode = 0;
-
-    // target (CHM layer)
-    bool has_target = false;
-    int64_t m = 0;
-    int md = 2;
-    DevBuf tx, ty, tz;
-    bool grid_ready = false, bbox_ready = false;
-    double bb[4] = {0, 0, 0, 0};
-    DevBuf cell_of, counts, cell_start, fill, pts, scan_tmp, mm_part, mm_out;
-    GridView gv{};
-    int64_t ncells = 0;
-    double pivot_x = 0.0, pivot_y = 0.0;
-
-    // per-call buffers (work order)
-    DevBuf sx, sy, sz, idx, dist, r, key, val, order, sort_tmp, frac_tmp, fit_tmp, bd2, bidx;
-    DevBuf ccx, ccy, rs, range;      // matched XY, r in selection order, key range
-    DevBuf wx, wy, wz, worig, tidx;  // spatial work order of the source
-    DevBuf stage, stage2, cx, cy, cz, state_dev;
-    IterState *h_state = nullptr;  // pinned
-
-    // profiling
-    int prof_mask = 0;
-    std::vector<ProfRec> recs;
-    std::vector<hipEvent_t> ev_pool;
-    std::map<std::string, std::pair<int64_t, double>> prof_acc;
-
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-};
+}  // namespace ficp_capi
 
 namespace {
-
-hipEvent_t ev_get(ficp_ctx *c) {
-    if (!c->ev_pool.empty()) {
-        hipEvent_t e = c->ev_pool.back();
-        c->ev_pool.pop_back();
-        return e;
-    }
-    hipEvent_t e = nullptr;
-    (void)hipEventCreate(&e);
-    return e;
-}
-
-struct ProfScope {
-    ficp_ctx *c;
-    const char *name;
-    hipEvent_t a = nullptr;
-    ProfScope(ficp_ctx *c_, int cls, const char *n) : c(c_), name(n) {
-        if (c->prof_mask & cls) {
-            a = ev_get(c);
-            (void)hipEventRecord(a, c->stream);
-        }
-    }
-    ~ProfScope() {
-        if (a) {
-            hipEvent_t b = ev_get(c);
-            (void)hipEventRecord(b, c->stream);
-            c->recs.push_back({name, a, b});
-        }
-    }
-};
-
-int set_device(ficp_ctx *c) {
-    HIPCHK(hipSetDevice(c->device));
-    return FICP_OK;
-}
-
-int sync(ficp_ctx *c) {
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return FICP_OK;
-}
-
-// host (n x ld) rows -> device SoA columns (first ncols)
-int upload_rows(ficp_ctx *c, const double *rows, int64_t n, int64_t ld, int ncols, DevBuf &c0,
-                DevBuf &c1, DevBuf *c2) {
-    CHK(c0.ensure(n * 8));
-    CHK(c1.ensure(n * 8));
-    if (c2) CHK(c2->ensure(n * 8));
-    if (n == 0) return FICP_OK;
-    CHK(c->stage.ensure(n * ld * 8));
-    HIPCHK(hipMemcpyAsync(c->stage.p, rows, n * ld * 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(launch_deinterleave(c->stage.as<double>(), n, ld, ncols, c0.as<double>(),
-                               c1.as<double>(), c2 ? c2->as<double>() : nullptr, c->stream));
-    return FICP_OK;
-}
 
 // bounding box of the CHM layer (grid geometry and the fit's pivot), once per target
 int ensure_bbox(ficp_ctx *c) {
@@ -199,21 +52,9 @@ int ensure_grid(ficp_ctx *c) {
     ProfScope ps(c, P_GRID, "grid_build");
     CHK(ensure_bbox(c));
     const double x0 = c->bb[0], x1 = c->bb[1], y0 = c->bb[2], y1 = c->bb[3];
-    // geometry: about kPerCell stems per cell
-    const double kPerCell = 2.0;
-    const double sxr = x1 - x0, syr = y1 - y0;
-    double h;
-    if (m <= 1 || (sxr <= 0.0 && syr <= 0.0)) h = 1.0;
-    else if (sxr > 0.0 && syr > 0.0) h = sqrt(sxr * syr * kPerCell / (double)m);
-    else h = std::max(sxr, syr) * kPerCell / (double)m;
-    if (!(h > 0.0)) h = 1.0;
+    double h, margin;
     int64_t gx, gy;
-    for (;;) {
-        gx = (int64_t)floor(sxr / h) + 1;
-        gy = (int64_t)floor(syr / h) + 1;
-        if (gx * gy <= 4 * m + 64 && gx < (1 << 24) && gy < (1 << 24)) break;
-        h *= 1.5;
-    }
+    plan_grid(x0, x1, y0, y1, m, h, gx, gy, margin);
     c->ncells = gx * gy;
     GridView g{};
     g.x0 = x0;
@@ -222,7 +63,7 @@ int ensure_grid(ficp_ctx *c) {
     g.inv_h = 1.0 / h;
     g.gx = (int)gx;
     g.gy = (int)gy;
-    g.margin = 64.0 * 2.220446049250313e-16 * (fabs(x0) + fabs(y0) + sxr + syr + h);
+    g.margin = margin;
     // counting sort of the stems by cell
     CHK(c->cell_of.ensure(m * 4));
     CHK(c->counts.ensure((c->ncells + 1) * 4));
@@ -548,6 +389,8 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev};
     for (DevBuf *b : bufs) b->release();
+    batch_release(c->batch);
+    c->batch = nullptr;
     for (auto &r : c->recs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);

@@ -1,0 +1,315 @@
+// capi_batch.hip -- ficp_run_batch / ficp_run_batch_device: many independent plots per
+// device pass (BASELINE config C4, 1024 plots x 10k trees vs 10k CHM stems).
+//
+// The reference joins plots one at a time (App.join_plot, app.py:630-661, one
+// FractionalICP(...).run() per plot).  Here every plot's CHM grid lives in one set of
+// arrays (per-plot geometry, global cell ids), and one batch iteration advances every
+// live plot by one step of ficp.py:122-147:
+//
+//   batch_fit (LOOP plots: fit on the plot's selection, T kept in the plot's state)
+//   -> nn_grid_batch (applies T, exact 1-NN against the plot's own grid, keys + r)
+//   -> sort_seg      (distance order, then stable partition by plot)
+//   -> batch_fraction(one workgroup per plot: FRMSD argmin over its segment)
+//   -> batch_update  (per-plot convergence test ficp.py:142, stage switch ficp.py:152)
+//
+// The host reads one counter (live plots) per batch iteration.
+#include "capi_internal.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <cmath>
+#include <vector>
+
+struct BatchBufs {
+    DevBuf so, to, plot_of, tplot, grids, st, active, bb, lams;
+    DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp;
+    DevBuf key, idx, r, ccx, ccy, order, rs, sort_tmp, range;
+    DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
+    unsigned int *h_active = nullptr;      // pinned
+    bool range_ready = false;
+};
+
+void batch_release(BatchBufs *b) {
+    if (!b) return;
+    DevBuf *bufs[] = {&b->so,       &b->to,      &b->plot_of,  &b->tplot, &b->grids, &b->st,
+                      &b->active,   &b->bb,      &b->lams,     &b->cell_of, &b->counts,
+                      &b->fill,     &b->cell_start, &b->pts,   &b->scan_tmp, &b->key, &b->idx,
+                      &b->r,        &b->ccx,     &b->ccy,      &b->order, &b->rs,
+                      &b->sort_tmp, &b->range,   &b->sx,       &b->sy,    &b->sz,    &b->tx,
+                      &b->ty,       &b->tz,      &b->stage};
+    for (DevBuf *d : bufs) d->release();
+    if (b->h_active) (void)hipHostFree(b->h_active);
+    delete b;
+}
+
+namespace {
+
+int check_offsets(const int64_t *off, int32_t nplots, const char *what, int64_t &total) {
+    if (!off) return fail(FICP_EINVAL, "null %s offsets", what);
+    if (off[0] != 0) return fail(FICP_EINVAL, "%s offsets must start at 0", what);
+    for (int32_t p = 0; p < nplots; ++p)
+        if (off[p + 1] < off[p]) return fail(FICP_EINVAL, "%s offsets must be non-decreasing", what);
+    total = off[nplots];
+    return FICP_OK;
+}
+
+BatchBufs *batch_of(ficp_ctx *c) {
+    if (!c->batch) c->batch = new BatchBufs();
+    return c->batch;
+}
+
+// per-plot CHM grids in one set of arrays (cells of plot p: cell_base_p .. +gx*gy-1)
+int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *to_h,
+                      const double *tx, const double *ty, const double *tz, int64_t m, int md,
+                      std::vector<PlotGrid> &grids) {
+    CHK(b.bb.ensure((size_t)nplots * 4 * 8));
+    HIPCHK(launch_batch_bbox(tx, ty, b.to.as<int64_t>(), nplots, b.bb.as<double>(), c->stream));
+    std::vector<double> bb((size_t)nplots * 4);
+    HIPCHK(hipMemcpyAsync(bb.data(), b.bb.p, bb.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    grids.assign(nplots, PlotGrid{});
+    int64_t ncells = 0;
+    for (int32_t p = 0; p < nplots; ++p) {
+        PlotGrid &g = grids[p];
+        const int64_t mp = to_h[p + 1] - to_h[p];
+        g.m = (int)mp;
+        g.cell_base = ncells;
+        if (mp == 0) {  // no CHM stems: the plot never runs (ficp.py:66-68, 125-126)
+            g.x0 = g.y0 = g.px = g.py = 0.0;
+            g.h = g.inv_h = 1.0;
+            g.gx = g.gy = 1;
+            ncells += 1;
+            continue;
+        }
+        const double x0 = bb[4 * p], x1 = bb[4 * p + 1], y0 = bb[4 * p + 2], y1 = bb[4 * p + 3];
+        if (!(std::isfinite(x0) && std::isfinite(x1) && std::isfinite(y0) && std::isfinite(y1)))
+            return fail(FICP_EINVAL, "plot %d: target coordinates must be finite", (int)p);
+        double h, margin;
+        int64_t gx, gy;
+        plan_grid(x0, x1, y0, y1, mp, h, gx, gy, margin);
+        g.x0 = x0;
+        g.y0 = y0;
+        g.h = h;
+        g.inv_h = 1.0 / h;
+        g.margin = margin;
+        g.gx = (int)gx;
+        g.gy = (int)gy;
+        g.px = x0 + 0.5 * (x1 - x0);  // fit pivot: the plot's CHM bbox centre
+        g.py = y0 + 0.5 * (y1 - y0);
+        ncells += gx * gy;
+    }
+    if (ncells > 0x7ffffffe) return fail(FICP_EINVAL, "batch grid too large");
+    CHK(b.grids.ensure((size_t)nplots * sizeof(PlotGrid)));
+    HIPCHK(hipMemcpyAsync(b.grids.p, grids.data(), (size_t)nplots * sizeof(PlotGrid),
+                          hipMemcpyHostToDevice, c->stream));
+    CHK(b.tplot.ensure(m * 4));
+    CHK(b.cell_of.ensure(m * 4));
+    CHK(b.counts.ensure((ncells + 1) * 4));
+    CHK(b.fill.ensure((ncells + 1) * 4));
+    CHK(b.cell_start.ensure((ncells + 1) * 4));
+    CHK(b.pts.ensure(m * sizeof(TPt)));
+    CHK(b.scan_tmp.ensure(scan_tmp_elems(ncells) * 4 + 64));
+    HIPCHK(launch_fill_plot_ids(b.to.as<int64_t>(), nplots, b.tplot.as<int32_t>(), c->stream));
+    HIPCHK(launch_atomic_zero32((uint32_t *)b.counts.p, ncells + 1, c->stream));
+    HIPCHK(launch_atomic_zero32((uint32_t *)b.fill.p, ncells + 1, c->stream));
+    HIPCHK(launch_batch_grid_count(tx, ty, m, b.tplot.as<int32_t>(), b.grids.as<PlotGrid>(),
+                                   b.cell_of.as<int32_t>(), b.counts.as<int32_t>(), c->stream));
+    HIPCHK(launch_scan_i32(b.counts.as<int32_t>(), b.cell_start.as<int32_t>(), ncells,
+                           b.scan_tmp.as<int32_t>(), true, c->stream));
+    HIPCHK(launch_grid_scatter(tx, ty, md == 3 ? tz : nullptr, m, b.cell_of.as<int32_t>(),
+                               b.cell_start.as<int32_t>(), b.fill.as<int32_t>(), b.pts.as<TPt>(),
+                               c->stream));
+    HIPCHK(launch_grid_sort_cells(b.pts.as<TPt>(), b.cell_start.as<int32_t>(), ncells, c->stream));
+    return FICP_OK;
+}
+
+int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, double *sy,
+               const double *sz, const int64_t *to_h, const double *tx, const double *ty,
+               const double *tz, int md, int32_t nstages, const double *lambdas,
+               double threshold, int32_t max_iter, int32_t allow_refl,
+               ficp_plot_stats *per_plot) {
+    const int64_t n = so_h[nplots], m = to_h[nplots];
+    BatchBufs &b = *batch_of(c);
+    if (!b.h_active)
+        HIPCHK(hipHostMalloc((void **)&b.h_active, sizeof(unsigned int), hipHostMallocDefault));
+    CHK(b.so.ensure((size_t)(nplots + 1) * 8));
+    CHK(b.to.ensure((size_t)(nplots + 1) * 8));
+    CHK(b.st.ensure((size_t)nplots * sizeof(PlotState)));
+    CHK(b.active.ensure(64));
+    CHK(b.lams.ensure((size_t)std::max(nstages, 1) * 8));
+    HIPCHK(hipMemcpyAsync(b.so.p, so_h, (size_t)(nplots + 1) * 8, hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(b.to.p, to_h, (size_t)(nplots + 1) * 8, hipMemcpyHostToDevice,
+                          c->stream));
+    if (nstages > 0)
+        HIPCHK(hipMemcpyAsync(b.lams.p, lambdas, (size_t)nstages * 8, hipMemcpyHostToDevice,
+                              c->stream));
+    HIPCHK(launch_batch_init(b.so.as<int64_t>(), b.to.as<int64_t>(), nplots, nstages,
+                             b.st.as<PlotState>(), c->stream));
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    if (n > 0 && m > 0 && nstages > 0) {
+        std::vector<PlotGrid> grids;
+        {
+            ProfScope ps(c, P_GRID, "batch_grid_build");
+            CHK(build_batch_grids(c, b, nplots, to_h, tx, ty, tz, m, md, grids));
+        }
+        CHK(b.plot_of.ensure(n * 4));
+        CHK(b.key.ensure(n * 8));
+        CHK(b.idx.ensure(n * 4));
+        CHK(b.r.ensure(n * 8));
+        CHK(b.ccx.ensure(n * 8));
+        CHK(b.ccy.ensure(n * 8));
+        CHK(b.order.ensure(n * 4));
+        CHK(b.rs.ensure(n * 8));
+        CHK(b.sort_tmp.ensure(sort_seg_tmp_bytes(n)));
+        if (!b.range_ready) {
+            CHK(b.range.ensure(64));
+            HIPCHK(launch_atomic_zero64(b.range.as<unsigned long long>(), 2, c->stream));
+            b.range_ready = true;
+        }
+        // keys of plots that never run (no CHM stems) must be defined for the sort
+        HIPCHK(hipMemsetAsync(b.key.p, 0, n * 8, c->stream));
+        HIPCHK(launch_fill_plot_ids(b.so.as<int64_t>(), nplots, b.plot_of.as<int32_t>(),
+                                    c->stream));
+        uint32_t *tflag = sort_timeout_flag(b.sort_tmp.p, n);
+        HIPCHK(launch_atomic_zero32(tflag, 1, c->stream));
+        NNArgs a{};
+        a.sx = sx;
+        a.sy = sy;
+        a.sz = md == 3 ? sz : nullptr;
+        a.n = n;
+        a.idx = b.idx.as<int32_t>();
+        a.r = b.r.as<double>();
+        a.key = b.key.as<unsigned long long>();
+        a.cx = b.ccx.as<double>();
+        a.cy = b.ccy.as<double>();
+        a.tx = tx;
+        a.ty = ty;
+        a.range = b.range.as<unsigned long long>();
+        PlotState *st = b.st.as<PlotState>();
+        // every plot makes at most nstages * (max_iter + 1) NN calls
+        const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1) + 1;
+        for (int64_t bit = 0; bit < cap; ++bit) {
+            {
+                ProfScope ps(c, P_FIT, "batch_fit");
+                HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
+                                        b.key.as<unsigned long long>(), b.order.as<uint32_t>(),
+                                        b.so.as<int64_t>(), b.grids.as<PlotGrid>(), nplots,
+                                        allow_refl, st, c->stream));
+            }
+            {
+                ProfScope ps(c, P_NN, "nn_grid_batch");
+                HIPCHK(launch_nn_grid_batch(a, b.plot_of.as<int32_t>(), b.grids.as<PlotGrid>(),
+                                            b.pts.as<TPt>(), b.cell_start.as<int32_t>(), st, md,
+                                            c->stream));
+            }
+            {
+                ProfScope ps(c, P_SORT, "sort_seg");
+                HIPCHK(launch_sort_seg(b.key.as<unsigned long long>(), b.plot_of.as<int32_t>(), n,
+                                       b.range.as<unsigned long long>(), b.order.as<uint32_t>(),
+                                       b.r.as<double>(), b.rs.as<double>(), b.sort_tmp.p,
+                                       c->stream));
+            }
+            {
+                ProfScope ps(c, P_FRAC, "batch_fraction");
+                HIPCHK(launch_batch_fraction(b.rs.as<double>(), b.so.as<int64_t>(), nplots,
+                                             b.lams.as<double>(), st, c->stream));
+            }
+            HIPCHK(launch_batch_update(nplots, nstages, threshold, max_iter, st,
+                                       (unsigned int *)b.active.p, c->stream));
+            HIPCHK(hipMemcpyAsync(b.h_active, b.active.p, 4, hipMemcpyDeviceToHost, c->stream));
+            CHK(sync(c));
+            if (*b.h_active == 0) break;
+        }
+        uint32_t tf = 0;
+        HIPCHK(hipMemcpyAsync(&tf, tflag, 4, hipMemcpyDeviceToHost, c->stream));
+        CHK(sync(c));
+        if (tf) return fail(FICP_EHIP, "residual sort look-back timed out (results invalid)");
+        if (*b.h_active != 0) return fail(FICP_EHIP, "batch did not converge within its bound");
+    }
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    if (per_plot) {
+        std::vector<PlotState> hs((size_t)nplots);
+        HIPCHK(hipMemcpyAsync(hs.data(), b.st.p, hs.size() * sizeof(PlotState),
+                              hipMemcpyDeviceToHost, c->stream));
+        CHK(sync(c));
+        for (int32_t p = 0; p < nplots; ++p) {
+            const PlotState &s = hs[p];
+            ficp_plot_stats &o = per_plot[p];
+            memcpy(o.T_total, s.Ttot, sizeof o.T_total);
+            o.frmsd_last = s.frmsd;
+            o.k_last = s.k;
+            o.n_nn_calls = s.n_nn;
+            o.n_fits = s.n_fit;
+            o.iters[0] = s.iters0;
+            o.iters[1] = s.iters1;
+        }
+    }
+    return sync(c);
+}
+
+int check_batch_args(int32_t nplots, int32_t md, int32_t nstages, const double *lambdas) {
+    if (nplots <= 0 || nplots > 65535)
+        return fail(FICP_EINVAL, "nplots must be in [1, 65535] (got %d)", (int)nplots);
+    if (md != 2 && md != 3) return fail(FICP_EINVAL, "md must be 2 or 3 (got %d)", (int)md);
+    if (nstages < 0 || (nstages > 0 && !lambdas)) return fail(FICP_EINVAL, "bad stages");
+    return FICP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ficp_run_batch(ficp_ctx *c, int32_t nplots, const int64_t *src_off, double *src,
+                   int64_t lds, const int64_t *tgt_off, const double *tgt, int64_t ldt,
+                   int32_t md, int32_t nstages, const double *lambdas, double threshold,
+                   int32_t max_iterations, int32_t allow_reflection, ficp_plot_stats *per_plot) {
+    if (!c) return fail(FICP_EINVAL, "null context");
+    CHK(set_device(c));
+    CHK(check_batch_args(nplots, md, nstages, lambdas));
+    int64_t n = 0, m = 0;
+    CHK(check_offsets(src_off, nplots, "source", n));
+    CHK(check_offsets(tgt_off, nplots, "target", m));
+    if (n > 0x3fffffff || m > 0x3fffffff) return fail(FICP_EINVAL, "batch too large");
+    if ((n > 0 && (!src || lds < md)) || (m > 0 && (!tgt || ldt < md)))
+        return fail(FICP_EINVAL, "bad source/target arrays");
+    BatchBufs &b = *batch_of(c);
+    CHK(upload_rows(c, src, n, lds, md, b.sx, b.sy, &b.sz));
+    CHK(upload_rows(c, tgt, m, ldt, md, b.tx, b.ty, &b.tz));
+    CHK(batch_core(c, nplots, src_off, b.sx.as<double>(), b.sy.as<double>(), b.sz.as<double>(),
+                   tgt_off, b.tx.as<double>(), b.ty.as<double>(), b.tz.as<double>(), md, nstages,
+                   lambdas, threshold, max_iterations, allow_reflection, per_plot));
+    if (n == 0) return FICP_OK;
+    CHK(b.stage.ensure(n * 16));
+    HIPCHK(launch_interleave_xy(b.sx.as<double>(), b.sy.as<double>(), n, b.stage.as<double>(),
+                                c->stream));
+    std::vector<double> xy((size_t)n * 2);
+    HIPCHK(hipMemcpyAsync(xy.data(), b.stage.p, n * 16, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    for (int64_t i = 0; i < n; ++i) {  // columns 0,1 only
+        src[i * lds] = xy[2 * i];
+        src[i * lds + 1] = xy[2 * i + 1];
+    }
+    return FICP_OK;
+}
+
+int ficp_run_batch_device(ficp_ctx *c, int32_t nplots, const int64_t *src_off, double *x,
+                          double *y, const double *z, const int64_t *tgt_off, const double *tx,
+                          const double *ty, const double *tz, int32_t md, int32_t nstages,
+                          const double *lambdas, double threshold, int32_t max_iterations,
+                          int32_t allow_reflection, ficp_plot_stats *per_plot) {
+    if (!c) return fail(FICP_EINVAL, "null context");
+    CHK(set_device(c));
+    CHK(check_batch_args(nplots, md, nstages, lambdas));
+    int64_t n = 0, m = 0;
+    CHK(check_offsets(src_off, nplots, "source", n));
+    CHK(check_offsets(tgt_off, nplots, "target", m));
+    if (n > 0x3fffffff || m > 0x3fffffff) return fail(FICP_EINVAL, "batch too large");
+    if ((n > 0 && (!x || !y || (md == 3 && !z))) || (m > 0 && (!tx || !ty || (md == 3 && !tz))))
+        return fail(FICP_EINVAL, "bad device arrays");
+    return batch_core(c, nplots, src_off, x, y, z, tgt_off, tx, ty, tz, md, nstages, lambdas,
+                      threshold, max_iterations, allow_reflection, per_plot);
+}
+
+}  // extern "C"

@@ -169,4 +169,61 @@ hipError_t launch_sum_sq_diff(const double *sx, const double *sy, const double *
                               const double *cx, const double *cy, const double *cz, int64_t k,
                               int md, void *tmp, double *out, hipStream_t s);
 
+// ------------------------------------------------------------- batch of plots (C4)
+// Plot p owns source rows [so[p], so[p+1]) and CHM rows [to[p], to[p+1]) of the
+// concatenated layers; every kernel below works on all plots at once.
+struct PlotGrid {
+    double x0, y0, h, inv_h, margin, px, py;  // grid geometry; (px, py) = fit pivot
+    long long cell_base;                     // first cell of this plot in cell_start
+    int gx, gy;
+    int m;                                   // CHM stems of the plot (0: plot is skipped)
+    int pad;
+};
+
+enum PlotPhase { PH_HEAD = 0, PH_LOOP = 1, PH_DONE = 2 };
+
+// Device-resident per-plot ICP state (the _iterate loop of ficp.py:122-147 per plot).
+struct alignas(16) PlotState {
+    double T[9];       // transform to apply before the next NN (when apply != 0)
+    double Ttot[9];    // composite transform of the run
+    double cur;        // current FRMSD (ficp.py:129, 144)
+    double frmsd;      // FRMSD of the last fraction call
+    double frac;
+    long long k;       // k of the last fraction call
+    int phase;         // PlotPhase
+    int stage;         // 0, 1
+    int it;            // loop bodies completed in this stage
+    int apply;
+    int n_nn, n_fit, iters0, iters1;
+};
+
+// per-plot bbox of the CHM layer: bb[4p..4p+3] = xmin, xmax, ymin, ymax
+hipError_t launch_batch_bbox(const double *tx, const double *ty, const int64_t *to, int nplots,
+                             double *bb, hipStream_t s);
+hipError_t launch_fill_plot_ids(const int64_t *off, int nplots, int32_t *plot_of, hipStream_t s);
+hipError_t launch_batch_grid_count(const double *tx, const double *ty, int64_t m,
+                                   const int32_t *tplot, const PlotGrid *grids, int32_t *cell_of,
+                                   int32_t *counts, hipStream_t s);
+// NN of every live plot's trees against its own CHM grid; idx = index in the concatenated
+// CHM layer.  Applies states[p].T first where states[p].apply.
+hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
+                                const TPt *pts, const int32_t *cell_start, const PlotState *st,
+                                int md, hipStream_t s);
+// stable argsort by (segment, key64, position): the distance sort of launch_sort followed
+// by a stable partition by seg[position] (two 8-bit passes, < 65536 segments).
+hipError_t launch_sort_seg(const unsigned long long *key64, const int32_t *seg, int64_t n,
+                           unsigned long long *range, uint32_t *order, const double *r,
+                           double *rs, void *tmp, hipStream_t s);
+int64_t sort_seg_tmp_bytes(int64_t n);
+hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
+                             PlotState *st, hipStream_t s);
+hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
+                            const double *cy, const unsigned long long *key,
+                            const uint32_t *order, const int64_t *so, const PlotGrid *grids,
+                            int nplots, int allow_refl, PlotState *st, hipStream_t s);
+hipError_t launch_batch_fraction(const double *rs, const int64_t *so, int nplots,
+                                 const double *lambdas, PlotState *st, hipStream_t s);
+hipError_t launch_batch_update(int nplots, int nstages, double threshold, int max_iter,
+                               PlotState *st, unsigned int *active, hipStream_t s);
+
 }  // namespace ficp

@@ -167,6 +167,56 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     if (a.range) range_accumulate(a.range, valid, ~key, key);
 }
 
+// Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against
+// plot p's own CHM grid (cells cell_base_p.., stems indexed in the concatenated layer).
+template <int MD>
+__global__ __launch_bounds__(256) void k_nn_grid_batch(NNArgs a, const int32_t *__restrict__ plot_of,
+                                                       const PlotGrid *__restrict__ grids,
+                                                       const TPt *__restrict__ pts,
+                                                       const int32_t *__restrict__ cell_start,
+                                                       const PlotState *__restrict__ st) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool valid = i < a.n;
+    int p = 0;
+    bool live = false;
+    unsigned long long key = 0;
+    if (valid) {
+        p = plot_of[i];
+        live = st[p].phase != PH_DONE;  // converged plots keep their last outputs, but
+        if (!live) key = a.key[i];      // their keys stay inside the sort's key range
+    }
+    if (live) {
+        const PlotGrid pg = grids[p];
+        double qx = a.sx[i], qy = a.sy[i];
+        if (st[p].apply) {
+            apply_T(st[p].T, qx, qy);
+            a.sx[i] = qx;
+            a.sy[i] = qy;
+        }
+        const double qz = (MD == 3) ? a.sz[i] : 0.0;
+        GridView g;
+        g.pts = pts;
+        g.cell_start = cell_start + pg.cell_base;
+        g.x0 = pg.x0;
+        g.y0 = pg.y0;
+        g.h = pg.h;
+        g.inv_h = pg.inv_h;
+        g.margin = pg.margin;
+        g.gx = pg.gx;
+        g.gy = pg.gy;
+        double best = INFINITY;
+        int bi = 0x7fffffff, bp = 0;
+        grid_query<MD>(g, qx, qy, qz, best, bi, bp);
+        if (a.cx) {
+            const double2 c = *reinterpret_cast<const double2 *>(pts + bp);
+            a.cx[i] = c.x;
+            a.cy[i] = c.y;
+        }
+        key = write_out(a, i, best, bi);
+    }
+    if (a.range) range_accumulate(a.range, valid, ~key, key);
+}
+
 constexpr int kTile = 256;
 
 // blockIdx.y = target chunk; one chunk -> final outputs, several -> partials then merge
@@ -572,6 +622,19 @@ hipError_t launch_scatter_xy(const uint32_t *worig, const double *wx, const doub
                              double *sx, double *sy, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_scatter_xy, dim3(nblk(n)), dim3(256), 0, s, worig, wx, wy, n, sx, sy);
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
+                                const TPt *pts, const int32_t *cell_start, const PlotState *st,
+                                int md, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    if (md == 3)
+        hipLaunchKernelGGL(k_nn_grid_batch<3>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
+                           pts, cell_start, st);
+    else
+        hipLaunchKernelGGL(k_nn_grid_batch<2>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
+                           pts, cell_start, st);
     return hipGetLastError();
 }
 

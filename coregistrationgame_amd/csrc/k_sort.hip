@@ -344,6 +344,35 @@ __global__ __launch_bounds__(256) void k_rs_rowscan(uint32_t *counts, int ntiles
     }
 }
 
+// segmented sort: key32[j] = seg[order[j]] for the stable partition passes
+__global__ __launch_bounds__(256) void k_seg_keys(const int32_t *seg, const uint32_t *order,
+                                                  int64_t n, uint32_t *k32) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    k32[j] = (uint32_t)seg[order[j]];
+}
+
+// histograms of digits 0 and 1 of key32 -> hist[0..255], hist[256..511] (atomics)
+__global__ __launch_bounds__(256) void k_hist2(const uint32_t *k32, int64_t n, uint32_t *hist) {
+    __shared__ uint32_t s_h[2][256];
+    s_h[0][threadIdx.x] = 0;
+    s_h[1][threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t nround = (n + 255) / 256;
+    for (int64_t q = blockIdx.x; q < nround; q += gridDim.x) {
+        const int64_t j = q * 256 + threadIdx.x;
+        const bool valid = j < n;
+        const uint32_t k = valid ? k32[j] : 0u;
+        wave_hist_add(s_h[0], k & 255u, valid);
+        wave_hist_add(s_h[1], (k >> 8) & 255u, valid);
+    }
+    __syncthreads();
+    for (int e = 0; e < 2; ++e) {
+        const uint32_t c = s_h[e][threadIdx.x];
+        if (c) atomicAdd(&hist[e * 256 + threadIdx.x], c);
+    }
+}
+
 // Runs of equal key32 hold distinct distances closer than 2^s ulps: order them by the
 // full key (stable: equal key64 keep their orig order).  Also resets the key range.
 __global__ __launch_bounds__(256) void k_os_fixup(const uint32_t *k32, uint32_t *val,
@@ -599,6 +628,40 @@ hipError_t launch_keys_from_doubles(const double *d, int64_t n, unsigned long lo
                                     uint32_t *val, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_keys_from_doubles, dim3(nblk(n)), dim3(256), 0, s, d, n, key, val);
+    return hipGetLastError();
+}
+
+}  // namespace ficp
+
+namespace ficp {
+
+int64_t sort_seg_tmp_bytes(int64_t n) { return sort_tmp_bytes(n); }
+
+hipError_t launch_sort_seg(const unsigned long long *key64, const int32_t *seg, int64_t n,
+                           unsigned long long *range, uint32_t *order, const double *r,
+                           double *rs, void *tmp, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    // 1. distance order, exact ties by position (caller order)
+    hipError_t e = launch_sort(key64, nullptr, n, range, order, nullptr, nullptr, tmp, nullptr, s);
+    if (e != hipSuccess) return e;
+    // 2. stable partition by segment: LSD passes on the 16-bit segment id
+    SortWS w = carve(tmp, n);
+    hipLaunchKernelGGL(k_seg_keys, dim3(nblk(n)), dim3(256), 0, s, seg, order, n, w.kA);
+    hipLaunchKernelGGL(k_atomic_zero32, dim3(2), dim3(256), 0, s, w.hist, (int64_t)512);
+    const int hb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 2047) / 2048));
+    hipLaunchKernelGGL(k_hist2, dim3(hb), dim3(256), 0, s, w.kA, n, w.hist);
+    const dim3 g(w.ntiles), b(OB);
+    hipLaunchKernelGGL(k_rs_count<0>, g, b, 0, s, w.kA, n, w.counts, w.ntiles, (const int *)nullptr);
+    hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles,
+                       (const int *)nullptr);
+    hipLaunchKernelGGL((k_os_pass<0, false>), g, b, 0, s, w.kA, order, w.kB, w.vB, n, w,
+                       (const uint32_t *)w.counts, (const double *)nullptr, (double *)nullptr,
+                       (const int *)nullptr);
+    hipLaunchKernelGGL(k_rs_count<1>, g, b, 0, s, w.kB, n, w.counts, w.ntiles, (const int *)nullptr);
+    hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles,
+                       (const int *)nullptr);
+    hipLaunchKernelGGL((k_os_pass<1, false>), g, b, 0, s, w.kB, w.vB, w.kA, order, n, w,
+                       (const uint32_t *)w.counts, r, rs, (const int *)nullptr);
     return hipGetLastError();
 }
 

@@ -113,6 +113,35 @@ int ficp_run_device(ficp_ctx *ctx, double *x, double *y, const double *z, int64_
                     int32_t nstages, const double *lambdas, double threshold,
                     int32_t max_iterations, int32_t allow_reflection, ficp_stats *stats);
 
+/* --- many plots in one device pass (a stand's Join of every plot) ------- */
+/* Result of one plot of a batch: what ficp_stats reports for a single run. */
+typedef struct ficp_plot_stats {
+    double T_total[9];   /* out: composite transform applied to the plot's trees  */
+    double frmsd_last;   /* out: FRMSD of the plot's last fraction call           */
+    int64_t k_last;      /* out: k of that call                                   */
+    int32_t n_nn_calls;  /* out: NN calls of the plot (all stages)                */
+    int32_t n_fits;      /* out: loop bodies of the plot                          */
+    int32_t iters[2];    /* out: loop bodies in stages 1 and 2                    */
+} ficp_plot_stats;
+
+/* FractionalICP(plot trees, plot CHM).run() for `nplots` independent plots at once
+   (App.join_plot, app.py:630-661, once per plot; ficp.py:122-154 per plot, each plot
+   with its own convergence test).  Plot p moves source rows src_off[p]..src_off[p+1]-1
+   against target rows tgt_off[p]..tgt_off[p+1]-1; src_off[0] = tgt_off[0] = 0 and both
+   non-decreasing.  All plots share md, lambdas, threshold, max_iterations and
+   allow_reflection; 0 < nplots <= 65535.  Source columns 0,1 are updated in place;
+   per_plot (nullable) receives nplots records.  Independent of ficp_set_target. */
+int ficp_run_batch(ficp_ctx *ctx, int32_t nplots, const int64_t *src_off, double *src,
+                   int64_t lds, const int64_t *tgt_off, const double *tgt, int64_t ldt,
+                   int32_t md, int32_t nstages, const double *lambdas, double threshold,
+                   int32_t max_iterations, int32_t allow_reflection, ficp_plot_stats *per_plot);
+/* Same on device-resident SoA layers (offsets stay host arrays); x, y updated in place. */
+int ficp_run_batch_device(ficp_ctx *ctx, int32_t nplots, const int64_t *src_off, double *x,
+                          double *y, const double *z, const int64_t *tgt_off, const double *tx,
+                          const double *ty, const double *tz, int32_t md, int32_t nstages,
+                          const double *lambdas, double threshold, int32_t max_iterations,
+                          int32_t allow_reflection, ficp_plot_stats *per_plot);
+
 /* --- device memory helpers (for callers without their own allocator) ---- */
 int ficp_dev_alloc(ficp_ctx *ctx, int64_t bytes, void **ptr);
 int ficp_dev_free(ficp_ctx *ctx, void *ptr);

@@ -1,0 +1,122 @@
+"""GPU parity of the multi-plot path (ficp_run_batch, C4) against the golden traces and
+the pinned oracle, plot by plot.  Each plot of a batch must end exactly where its own
+FractionalICP(source, target).run() ends (ficp.py:122-154)."""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, K_GAP_PIN, RUN_FIXTURES, load_run, pinned_prefix
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint64)
+
+
+def test_batch_golden_runs():
+    """Every golden run fixture (md 2 and 3, unit and geo coordinates, threshold -inf)
+    in one batch call per (threshold, max_iterations) group."""
+    from coregistrationgame_amd import FractionalICPBatch
+    runs = {name: load_run(name) for name in RUN_FIXTURES}
+    groups = {}
+    for name, r in runs.items():
+        key = (float(r["kwargs_threshold"]), int(r["kwargs_max_iterations"]))
+        groups.setdefault(key, []).append(name)
+    for (thr, mx), names in groups.items():
+        b = FractionalICPBatch([runs[n]["src"] for n in names], [runs[n]["tgt"] for n in names],
+                               threshold=thr, max_iterations=mx)
+        finals = b.run()
+        for j, name in enumerate(names):
+            r = runs[name]
+            np.testing.assert_allclose(finals[j][:, :2], r["final"][:, :2], atol=1e-6, rtol=0, err_msg=name)
+            np.testing.assert_array_equal(bits(finals[j][:, 2:]), bits(r["final"][:, 2:]))
+            scale = 1.0 + np.abs(r["src"][:, :2]).max()
+            if pinned_prefix(r["gap"], r["frmsd"], scale) == len(r["k"]):
+                st = b.stats[j]
+                assert st["n_nn_calls"] == len(r["k"]), name
+                assert st["n_fits"] == len(r["T"]), name
+                assert st["k_last"] == r["k"][-1], name
+
+
+def test_batch_real_stand10():
+    """The 16 real plots of Data/2014 against the whole Data/2019 stem layer, as a batch."""
+    from coregistrationgame_amd import FractionalICPBatch
+    z = np.load(GOLDEN / "run_real_stand10.npz")
+    tgt = z["tgt"]
+    pids = list(z["plot_ids"])
+    b = FractionalICPBatch([z[f"{pid}/src"] for pid in pids], [tgt] * len(pids))
+    finals = b.run()
+    for j, pid in enumerate(pids):
+        np.testing.assert_allclose(finals[j], z[f"{pid}/final"], atol=1e-6, rtol=0, err_msg=str(pid))
+        if np.all(z[f"{pid}/gap"] > K_GAP_PIN):
+            assert b.stats[j]["n_nn_calls"] == len(z[f"{pid}/k"]), pid
+            assert b.stats[j]["k_last"] == z[f"{pid}/k"][-1], pid
+
+
+def test_batch_vs_oracle_mixed(oracle):
+    """64 synthetic plots of mixed sizes (incl. 1-tree plots, empty layers, md=2 plots)
+    vs the oracle run of each plot alone."""
+    from coregistrationgame_amd import FractionalICPBatch, synth
+    rng = np.random.default_rng(7)
+    srcs, tgts = [], []
+    for p in range(64):
+        n = int(rng.choice([1, 2, 50, 400, 3000]))
+        m = int(rng.choice([1, 3, 60, 500, 4000]))
+        pl = synth.make_plot(n, m, 0.8, seed=20_000 + p, md=3)
+        s, t = pl.source, pl.target
+        if p % 7 == 3:
+            s, t = s[:, :2], t[:, :2]  # 2-D plot: lambda 1.3 in stage 2
+        srcs.append(s)
+        tgts.append(t)
+    srcs[5] = srcs[5][:0]            # empty tree layer
+    tgts[9] = tgts[9][:0]            # empty CHM layer
+    b = FractionalICPBatch(srcs, tgts)
+    finals = b.run()
+    for p in range(64):
+        if len(srcs[p]) == 0 or len(tgts[p]) == 0:
+            np.testing.assert_array_equal(finals[p], srcs[p])
+            assert b.stats[p]["n_nn_calls"] == 0
+            continue
+        ofinal, otr = oracle.run(srcs[p], tgts[p], nthreads=8)
+        np.testing.assert_allclose(finals[p][:, :2], ofinal[:, :2], atol=1e-6, rtol=0, err_msg=str(p))
+        np.testing.assert_array_equal(bits(finals[p][:, 2:]), bits(srcs[p][:, 2:]))
+        assert b.stats[p]["n_nn_calls"] == len(otr["k"]), p
+        assert b.stats[p]["k_last"] == otr["k"][-1], p
+
+
+def test_batch_matches_single_runs():
+    """Batch == one FractionalICP per plot on the GPU (same NN calls, same k, same XY)."""
+    from coregistrationgame_amd import FractionalICP, FractionalICPBatch, synth
+    plots = synth.make_batch(24, 10_000, 10_000, 0.8, 10_000_000, md=3)
+    b = FractionalICPBatch([p.source for p in plots], [p.target for p in plots])
+    finals = b.run()
+    for j, p in enumerate(plots):
+        icp = FractionalICP(p.source, p.target, nn_mode="grid")
+        single = icp.run()
+        np.testing.assert_allclose(finals[j][:, :2], single[:, :2], atol=1e-6, rtol=0)
+        assert b.stats[j]["n_nn_calls"] == icp.last_stats["n_nn_calls"]
+        assert b.stats[j]["n_fits"] == icp.last_stats["n_fits"]
+        assert b.stats[j]["k_last"] == icp.last_stats["k_last"]
+
+
+def test_batch_c4_properties():
+    """C4 at full size (1024 plots x 10k/10k): every plot undoes its misregistration, the
+    per-plot transforms reproduce the moved XY, and stage counters are consistent."""
+    from coregistrationgame_amd import FractionalICPBatch, synth
+    plots = synth.make_batch(1024, 10_000, 10_000, 0.8, 10_000_000, md=3)
+    b = FractionalICPBatch([p.source for p in plots], [p.target for p in plots])
+    finals = b.run()
+    st = b.stats
+    # a stage that ends by the convergence test (ficp.py:142) counts its last body as a
+    # fit but not as a completed iteration
+    extra = st["n_fits"] - st["iters"].sum(axis=1)
+    assert np.all((extra >= 0) & (extra <= 2))
+    assert np.all(st["n_nn_calls"] == st["n_fits"] + 2)
+    for j in range(0, 1024, 37):
+        p = plots[j]
+        inl = p.inlier_of >= 0
+        resid = np.linalg.norm(finals[j][inl, :2] - p.target[p.inlier_of[inl], :2], axis=1)
+        assert np.median(resid) < 0.45, (j, np.median(resid))
+        T = st["T_total"][j].reshape(3, 3)
+        xy = p.source[:, :2] @ T[:2, :2].T + T[:2, 2]
+        np.testing.assert_allclose(xy, finals[j][:, :2], atol=1e-6, rtol=0)

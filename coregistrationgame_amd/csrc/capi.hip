@@ -159,6 +159,57 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     return FICP_OK;
 }
 
+// FICP_CHECK=1: synchronise after every sort and fail at the first one that raised the
+// sort's error flag; FICP_CHECK=2 also verifies on the host that the order is a
+// permutation sorted by (key64, orig).  Debug only.
+int check_level() {
+    static const int lvl = getenv("FICP_CHECK") ? atoi(getenv("FICP_CHECK")) : 0;
+    return lvl;
+}
+
+int check_sort(ficp_ctx *c, int64_t n, const uint32_t *orig, const char *what) {
+    if (!check_level() || n == 0) return FICP_OK;
+    static int64_t ncall = 0;
+    ++ncall;
+    uint32_t tf = 0;
+    HIPCHK(hipMemcpyAsync(&tf, sort_timeout_flag(c->sort_tmp.p, n), 4, hipMemcpyDeviceToHost,
+                          c->stream));
+    CHK(sync(c));
+    if (tf) return fail(FICP_EHIP, "FICP_CHECK: sort flag %u after %s (sort call %lld, n=%lld)", tf,
+                        what, (long long)ncall, (long long)n);
+    if (check_level() < 2) return FICP_OK;
+    std::vector<uint32_t> ord(n), org(orig ? n : 0);
+    std::vector<unsigned long long> key(n);
+    HIPCHK(hipMemcpy(ord.data(), c->order.p, n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(key.data(), c->key.p, n * 8, hipMemcpyDeviceToHost));
+    if (orig) HIPCHK(hipMemcpy(org.data(), orig, n * 4, hipMemcpyDeviceToHost));
+    std::vector<char> seen(n, 0);
+    for (int64_t j = 0; j < n; ++j) {
+        if (ord[j] >= (uint64_t)n || seen[ord[j]])
+            return fail(FICP_EHIP, "FICP_CHECK: %s order not a permutation at %lld (v=%u, call %lld)",
+                        what, (long long)j, ord[j], (long long)ncall);
+        seen[ord[j]] = 1;
+    }
+    if (orig) {
+        std::fill(seen.begin(), seen.end(), 0);
+        for (int64_t j = 0; j < n; ++j) {
+            if (org[j] >= (uint64_t)n || seen[org[j]])
+                return fail(FICP_EHIP, "FICP_CHECK: %s orig not a permutation at %lld (call %lld)",
+                            what, (long long)j, (long long)ncall);
+            seen[org[j]] = 1;
+        }
+    }
+    for (int64_t j = 1; j < n; ++j) {
+        const uint32_t a = ord[j - 1], b = ord[j];
+        const unsigned long long ka = key[a], kb = key[b];
+        const uint32_t oa = orig ? org[a] : a, ob = orig ? org[b] : b;
+        if (ka > kb || (ka == kb && oa > ob))
+            return fail(FICP_EHIP, "FICP_CHECK: %s order unsorted at %lld (call %lld)", what,
+                        (long long)j, (long long)ncall);
+    }
+    return FICP_OK;
+}
+
 // sort (key, orig) of the last NN call, then the FRMSD fraction scan
 int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam, const uint32_t *orig) {
     {
@@ -167,6 +218,7 @@ int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam, const uint32_
                            c->order.as<uint32_t>(), c->r.as<double>(), c->rs.as<double>(),
                            c->sort_tmp.p, nullptr, c->stream));
     }
+    CHK(check_sort(c, n, orig, "residual sort"));
     {
         ProfScope ps(c, P_FRAC, "fraction");
         HIPCHK(launch_fraction(c->rs.as<double>(), n, N, lam, c->frac_tmp.p,
@@ -227,6 +279,7 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
     HIPCHK(launch_sort(c->key.as<unsigned long long>(), nullptr, n, range_ptr(c),
                        c->order.as<uint32_t>(), nullptr, nullptr, c->sort_tmp.p, nullptr,
                        c->stream));
+    CHK(check_sort(c, n, nullptr, "work-order sort"));
     HIPCHK(launch_gather_work(c->order.as<uint32_t>(), sx, sy, sz, n, c->wx.as<double>(),
                               c->wy.as<double>(), sz ? c->wz.as<double>() : nullptr,
                               c->worig.as<uint32_t>(), c->stream));
@@ -310,7 +363,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     }
     uint32_t tf = 0;
     HIPCHK(hipMemcpy(&tf, tflag, 4, hipMemcpyDeviceToHost));
-    if (tf) return fail(FICP_EHIP, "residual sort look-back timed out (results invalid)");
+    if (tf) return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", tf);
     return FICP_OK;
 }
 

@@ -275,7 +275,10 @@ __global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint3
     s_cnt[2][tid] = c0 + c1;
     s_cnt[3][tid] = c0 + c1 + c2;
     uint32_t ltot;
-    s_loc[tid] = block_excl_scan256<uint32_t>(mine, s_w, ltot);  // barriers publish s_*
+    // the scan's barriers publish s_gb and s_cnt; s_loc is written after them and needs
+    // a barrier of its own before any thread reads another digit's entry
+    s_loc[tid] = block_excl_scan256<uint32_t>(mine, s_w, ltot);
+    __syncthreads();
     // ---- stage the tile in LDS in output order, then write digit runs coalesced
 #pragma unroll
     for (int j = 0; j < OIPT; ++j) {

@@ -55,13 +55,15 @@ def test_batch_real_stand10():
 
 def test_batch_vs_oracle_mixed(oracle):
     """64 synthetic plots of mixed sizes (incl. 1-tree plots, empty layers, md=2 plots)
-    vs the oracle run of each plot alone."""
+    vs the oracle run of each plot alone.  (A plot whose selection can map onto a single
+    CHM stem has a zero cross-covariance: its rotation is rounding noise in the reference
+    and unpinnable, so the CHM layers here have >= 60 stems.)"""
     from coregistrationgame_amd import FractionalICPBatch, synth
     rng = np.random.default_rng(7)
     srcs, tgts = [], []
     for p in range(64):
         n = int(rng.choice([1, 2, 50, 400, 3000]))
-        m = int(rng.choice([1, 3, 60, 500, 4000]))
+        m = int(rng.choice([60, 500, 4000]))
         pl = synth.make_plot(n, m, 0.8, seed=20_000 + p, md=3)
         s, t = pl.source, pl.target
         if p % 7 == 3:

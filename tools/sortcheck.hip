@@ -1,9 +1,14 @@
 // sortcheck.hip -- GPU self-check of the residual sort (tools only, not shipped).
-// Build: make -C coregistrationgame_amd/csrc sortcheck ; run: ./tools/sortcheck [n] [reps]
+// Build: make -C coregistrationgame_amd/csrc sortcheck
+// Run:   ./tools/sortcheck [n] [reps] [use_orig] [mode] [with_r]
+//   mode 0: exponential distances; 1: work-order cell keys (cell << 32 | i), random
+//   cells; 2: cell keys, monotone cells; 3: all keys equal; 4: 5 distinct distances
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <math.h>
 
 #include <algorithm>
 #include <random>
@@ -32,6 +37,8 @@ int main(int argc, char **argv) {
     const int64_t n = argc > 1 ? atoll(argv[1]) : 1000000;
     const int reps = argc > 2 ? atoi(argv[2]) : 10;
     const int use_orig = argc > 3 ? atoi(argv[3]) : 1;
+    const int mode = argc > 4 ? atoi(argv[4]) : 0;
+    const int with_r = argc > 5 ? atoi(argv[5]) : 1;
     std::mt19937_64 rng(42);
     std::exponential_distribution<double> ex(1.0);
     std::vector<unsigned long long> key(n);
@@ -39,7 +46,11 @@ int main(int argc, char **argv) {
     std::vector<double> r(n);
     for (int64_t i = 0; i < n; ++i) {
         double d = ex(rng);
+        if (mode == 4) d = floor(d * 1.25);
         key[i] = hkey(d);
+        if (mode == 1) key[i] = ((unsigned long long)(rng() % 4000000ULL) << 32) | (uint64_t)i;
+        if (mode == 2) key[i] = ((unsigned long long)(i / 2) << 32) | (uint64_t)i;
+        if (mode == 3) key[i] = hkey(1.5);
         r[i] = d * d;
         orig[i] = (uint32_t)i;
     }
@@ -73,7 +84,8 @@ int main(int argc, char **argv) {
     int bad = 0;
     for (int rep = 0; rep < reps; ++rep) {
         CK(launch_key_range(dk, n, drange, s));
-        CK(launch_sort(dk, use_orig ? dorig : nullptr, n, drange, dorder, dr, drs, tmp, nullptr, s));
+        CK(launch_sort(dk, use_orig ? dorig : nullptr, n, drange, dorder, with_r ? dr : nullptr,
+                              with_r ? drs : nullptr, tmp, nullptr, s));
         CK(hipStreamSynchronize(s));
         uint32_t flag = 0;
         CK(hipMemcpy(&flag, sort_timeout_flag(tmp, n), 4, hipMemcpyDeviceToHost));
@@ -85,7 +97,7 @@ int main(int argc, char **argv) {
                 if (first < 0) first = j;
                 ++mism;
             }
-            if (got[j] < n && grs[j] != r[got[j]]) ++rsm;
+            if (with_r && got[j] < n && grs[j] != r[got[j]]) ++rsm;
         }
         printf("rep %d: flag=%u mismatches=%lld rs_mism=%lld first=%lld\n", rep, flag,
                (long long)mism, (long long)rsm, (long long)first);

@@ -111,10 +111,7 @@ int ensure_work(ficp_ctx *c, int64_t n) {
     CHK(c->ccx.ensure(n * 8));
     CHK(c->ccy.ensure(n * 8));
     CHK(c->rs.ensure(n * 8));
-    if (!c->range.p) {
-        CHK(c->range.ensure(64));
-        HIPCHK(launch_atomic_zero64(c->range.as<unsigned long long>(), 2, c->stream));
-    }
+    CHK(c->range.ensure(range_words(n) * 8));
     return FICP_OK;
 }
 

@@ -27,7 +27,6 @@ struct BatchBufs {
     DevBuf key, idx, r, ccx, ccy, order, rs, sort_tmp, range;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
     unsigned int *h_active = nullptr;      // pinned
-    bool range_ready = false;
 };
 
 void batch_release(BatchBufs *b) {
@@ -163,11 +162,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         CHK(b.order.ensure(n * 4));
         CHK(b.rs.ensure(n * 8));
         CHK(b.sort_tmp.ensure(sort_seg_tmp_bytes(n)));
-        if (!b.range_ready) {
-            CHK(b.range.ensure(64));
-            HIPCHK(launch_atomic_zero64(b.range.as<unsigned long long>(), 2, c->stream));
-            b.range_ready = true;
-        }
+        CHK(b.range.ensure(range_words(n) * 8));
         // keys of plots that never run (no CHM stems) must be defined for the sort
         HIPCHK(hipMemsetAsync(b.key.p, 0, n * 8, c->stream));
         HIPCHK(launch_fill_plot_ids(b.so.as<int64_t>(), nplots, b.plot_of.as<int32_t>(),

@@ -32,6 +32,35 @@ __device__ __forceinline__ void wave_range_reduce(unsigned long long &a, unsigne
     }
 }
 
+// Key range of a sort input, produced without atomics: every producing workgroup stores
+// its {max(~key), max(key)} to range[2 + 2 b .. 3 + 2 b] (plain stores, one lane), then
+// one small reduction kernel writes range[0..1].  range_words(n) u64 words hold the parts
+// of any producer that runs at most one workgroup per 256 keys.
+inline int64_t range_words(int64_t n) { return 2 + 2 * ((n + 255) / 256 + 1); }
+
+// block-wide {max(~key), max(key)} -> range[2 + 2 blockIdx.x ..] (all threads, 256/block)
+__device__ __forceinline__ void block_range_store(unsigned long long *range, bool valid,
+                                                  unsigned long long kmin_c,
+                                                  unsigned long long kmax) {
+    __shared__ unsigned long long s_ra[4], s_rb[4];
+    unsigned long long a = valid ? kmin_c : 0ULL, b = valid ? kmax : 0ULL;
+    wave_range_reduce(a, b);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_ra[wave] = a;
+        s_rb[wave] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            a = s_ra[w] > a ? s_ra[w] : a;
+            b = s_rb[w] > b ? s_rb[w] : b;
+        }
+        range[2 + 2 * (int64_t)blockIdx.x] = a;
+        range[3 + 2 * (int64_t)blockIdx.x] = b;
+    }
+}
+
 struct alignas(32) TPt {
     double x, y, z;
     long long idx;
@@ -63,7 +92,7 @@ struct NNArgs {
     double *cy;
     const double *tx;           // original-order CHM layer (brute path gathers cx, cy)
     const double *ty;
-    unsigned long long *range;  // out: key range {max(~key), max(key)} (atomics; nullable)
+    unsigned long long *range;  // out: key range parts (range_words(n) words; nullable)
 };
 
 // Device-resident state of one ICP stage (written by kernels, read back per iteration).
@@ -126,14 +155,16 @@ hipError_t launch_scan_i32(const int32_t *in, int32_t *out, int64_t n, int32_t *
 hipError_t launch_atomic_zero32(uint32_t *p, int64_t n, hipStream_t s);
 hipError_t launch_atomic_zero64(unsigned long long *p, int64_t n, hipStream_t s);
 // Stable argsort: order[j] = position (0..n-1) of the j-th smallest (key64, orig) pair
-// (orig == null: orig = position).  range = {max(~key), max(key)} of the keys (from the
-// NN kernel or launch_key_range); the sort resets it to {0, 0}.  r/rs (nullable):
+// (orig == null: orig = position).  range[0..1] = {max(~key), max(key)} of the keys (from
+// the NN launchers or launch_key_range, see range_words).  r/rs (nullable):
 // rs[j] = r[order[j]].  Scratch: sort_tmp_bytes(n).
 int64_t sort_tmp_bytes(int64_t n);
 // sticky flag set when a look-back wait timed out (results of that sort are invalid)
 uint32_t *sort_timeout_flag(void *tmp, int64_t n);
 hipError_t launch_key_range(const unsigned long long *key, int64_t n, unsigned long long *range,
                             hipStream_t s);
+// range[0..1] from the nparts parts a producer stored (see block_range_store)
+hipError_t launch_range_reduce(unsigned long long *range, int64_t nparts, hipStream_t s);
 hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, int64_t n,
                        unsigned long long *range, uint32_t *order, const double *r, double *rs,
                        void *tmp, const int *skip, hipStream_t s);

@@ -128,18 +128,6 @@ __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t
     return k;
 }
 
-// wave-level {max(~key), max(key)} folded into the global range (all lanes active)
-__device__ __forceinline__ void range_accumulate(unsigned long long *range, bool valid,
-                                                 unsigned long long kmin_c,
-                                                 unsigned long long kmax) {
-    unsigned long long a = valid ? kmin_c : 0ULL, b = valid ? kmax : 0ULL;
-    wave_range_reduce(a, b);
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax(&range[0], a);
-        atomicMax(&range[1], b);
-    }
-}
-
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     if (a.skip && *a.skip) return;
@@ -164,7 +152,7 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
         }
         key = write_out(a, i, best, bi);
     }
-    if (a.range) range_accumulate(a.range, valid, ~key, key);
+    if (a.range) block_range_store(a.range, valid, ~key, key);
 }
 
 // Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against
@@ -214,7 +202,7 @@ __global__ __launch_bounds__(256) void k_nn_grid_batch(NNArgs a, const int32_t *
         }
         key = write_out(a, i, best, bi);
     }
-    if (a.range) range_accumulate(a.range, valid, ~key, key);
+    if (a.range) block_range_store(a.range, valid, ~key, key);
 }
 
 constexpr int kTile = 256;
@@ -285,7 +273,7 @@ __global__ __launch_bounds__(256) void k_nn_brute(NNArgs a, const double *__rest
             part_idx[(int64_t)blockIdx.y * a.n + i] = bi[q];
         }
     }
-    if (gridDim.y == 1 && a.range) range_accumulate(a.range, any, kmin_c, kmax);
+    if (gridDim.y == 1 && a.range) block_range_store(a.range, any, kmin_c, kmax);
 }
 
 __global__ __launch_bounds__(256) void k_nn_merge(NNArgs a, int nchunks, const double *part_d2,
@@ -311,7 +299,7 @@ __global__ __launch_bounds__(256) void k_nn_merge(NNArgs a, int nchunks, const d
             a.cy[i] = a.ty[bi];
         }
     }
-    if (a.range) range_accumulate(a.range, valid, ~key, key);
+    if (a.range) block_range_store(a.range, valid, ~key, key);
 }
 
 __global__ __launch_bounds__(256) void k_apply_inplace(double *x, double *y, int64_t n,
@@ -538,6 +526,7 @@ hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_
         if (a.T) hipLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, a, g);
         else hipLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, a, g);
     }
+    if (a.range) return launch_range_reduce(a.range, grid.x, s);
     return hipGetLastError();
 }
 
@@ -566,6 +555,7 @@ hipError_t launch_nn_brute(const NNArgs &a0, const double *tx, const double *ty,
     if (nch > 1)
         hipLaunchKernelGGL(k_nn_merge, dim3(nblk(a.n)), dim3(256), 0, s, a, (int)nch, part_d2,
                            part_idx);
+    if (a.range) return launch_range_reduce(a.range, nch > 1 ? (int64_t)nblk(a.n) : qblocks, s);
     return hipGetLastError();
 }
 
@@ -635,6 +625,7 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
     else
         hipLaunchKernelGGL(k_nn_grid_batch<2>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
                            pts, cell_start, st);
+    if (a.range) return launch_range_reduce(a.range, nblk(a.n), s);
     return hipGetLastError();
 }
 

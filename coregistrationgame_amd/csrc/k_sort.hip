@@ -7,8 +7,8 @@
 //
 // Method, one launch per 8-bit digit, no global prefix-sum kernels:
 //  0. k_os_hist: derives a 32-bit key (key64 - kmin) >> s from the key range (kmin/kmax
-//     accumulated by the NN kernel, or by k_key_range), scatters (key32, position) into
-//     ORIG order -- so LSD stability alone orders exact ties by orig -- and builds the
+//     reduced from per-workgroup parts of the NN kernel or of k_key_range), scatters
+//     (key32, position) into ORIG order -- so LSD stability alone orders exact ties by orig -- and builds the
 //     four digit histograms at once (they do not depend on the order).
 //  1-4. k_os_pass<P>: single-pass stable scatter per digit ("onesweep"): tiles take ids
 //     in dispatch order from an atomic ticket, rank their items with 64-lane ballot
@@ -18,7 +18,7 @@
 //     the data is the flag, MI355X_MICROARCH.md Valid forms / R2), then write digit runs
 //     coalesced from an LDS staging copy.  The last pass also emits r in selection order.
 //  5. k_os_fixup: runs of equal key32 (distinct distances closer than 2^s ulps: rare)
-//     are re-ordered by key64 with a stable insertion sort; resets the key range.
+//     are re-ordered by key64 with a stable insertion sort.
 #include "ficp_internal.h"
 
 #include <stdlib.h>
@@ -49,12 +49,12 @@ struct SortWS {
     int ntiles;
 };
 
-// range = {max(~key), max(key)}, accumulated by atomics: read it at the memory side
+// range[0..1] = {max(~key), max(key)}: written by k_range_reduce (plain stores) in an
+// earlier kernel of the stream
 __device__ __forceinline__ void load_range(const unsigned long long *range,
                                            unsigned long long &kmin, unsigned long long &kmax) {
-    unsigned long long *r = const_cast<unsigned long long *>(range);
-    kmin = ~__hip_atomic_fetch_or(&r[0], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    kmax = __hip_atomic_fetch_or(&r[1], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    kmin = ~range[0];
+    kmax = range[1];
 }
 
 __device__ __forceinline__ int key_shift(unsigned long long kmin, unsigned long long kmax) {
@@ -81,16 +81,27 @@ __device__ __forceinline__ T block_excl_scan256(T v, T *s_w /* [4] */, T &total)
     return pre + x - v;
 }
 
-// key range for callers without a fused producer (API paths): range[0] = max(~key),
-// range[1] = max(key); both start at 0.
+// key range for callers without a fused producer (API paths): per-workgroup parts
 __global__ __launch_bounds__(256) void k_key_range(const unsigned long long *key, int64_t n,
                                                    unsigned long long *range) {
-    __shared__ unsigned long long s_a[4], s_b[4];
     unsigned long long a = 0, b = 0;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const unsigned long long k = key[i];
         a = max(a, ~k);
         b = max(b, k);
+    }
+    block_range_store(range, true, a, b);
+}
+
+// one workgroup: range[0..1] = max over the nparts parts (plain loads and stores)
+__global__ __launch_bounds__(1024) void k_range_reduce(unsigned long long *range, int64_t nparts) {
+    __shared__ unsigned long long s_a[16], s_b[16];
+    unsigned long long a = 0, b = 0;
+    const unsigned long long *part = range + 2;
+    for (int64_t p = threadIdx.x; p < nparts; p += 1024) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(part + 2 * p);
+        a = max(a, v.x);
+        b = max(b, v.y);
     }
     wave_range_reduce(a, b);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -100,12 +111,12 @@ __global__ __launch_bounds__(256) void k_key_range(const unsigned long long *key
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; ++w) {
+        for (int w = 1; w < 16; ++w) {
             a = max(a, s_a[w]);
             b = max(b, s_b[w]);
         }
-        atomicMax(&range[0], s_a[0] > a ? s_a[0] : a);
-        atomicMax(&range[1], s_b[0] > b ? s_b[0] : b);
+        range[0] = a;
+        range[1] = b;
     }
 }
 
@@ -377,18 +388,13 @@ __global__ __launch_bounds__(256) void k_hist2(const uint32_t *k32, int64_t n, u
 }
 
 // Runs of equal key32 hold distinct distances closer than 2^s ulps: order them by the
-// full key (stable: equal key64 keep their orig order).  Also resets the key range.
+// full key (stable: equal key64 keep their orig order).
 __global__ __launch_bounds__(256) void k_os_fixup(const uint32_t *k32, uint32_t *val,
                                                   const unsigned long long *key64,
                                                   const double *r, double *rs, int64_t n,
-                                                  unsigned long long *range_reset,
                                                   const int *skip) {
     if (skip && *skip) return;
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j == 0 && range_reset) {  // atomic-only word: reset with atomics too
-        __hip_atomic_exchange(&range_reset[0], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_exchange(&range_reset[1], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (j + 1 >= n) return;
     const uint32_t kj = k32[j];
     if (k32[j + 1] != kj) return;
@@ -565,13 +571,16 @@ int64_t sort_tmp_bytes(int64_t n) {
            nt * 256 * 4 + 256;
 }
 
+hipError_t launch_range_reduce(unsigned long long *range, int64_t nparts, hipStream_t s) {
+    hipLaunchKernelGGL(k_range_reduce, dim3(1), dim3(1024), 0, s, range, nparts);
+    return hipGetLastError();
+}
+
 hipError_t launch_key_range(const unsigned long long *key, int64_t n, unsigned long long *range,
                             hipStream_t s) {
-    hipLaunchKernelGGL(k_atomic_zero64, dim3(1), dim3(256), 0, s, range, (int64_t)2);
-    if (n == 0) return hipGetLastError();
-    const int nb = (int)std::min<int64_t>(512, (n + 255) / 256);
+    const int nb = (int)std::min<int64_t>(512, std::max<int64_t>(1, (n + 255) / 256));
     hipLaunchKernelGGL(k_key_range, dim3(nb), dim3(256), 0, s, key, n, range);
-    return hipGetLastError();
+    return launch_range_reduce(range, nb, s);
 }
 
 hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, int64_t n,
@@ -622,7 +631,7 @@ hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, in
     FICP_PASS(3)
 #undef FICP_PASS
     hipLaunchKernelGGL(k_os_fixup, dim3(nblk(n)), dim3(256), 0, s, w.kA, order, key64, r, rs, n,
-                       range, skip);
+                       skip);
     step();
     return hipGetLastError();
 }

@@ -14,7 +14,7 @@ from pathlib import Path
 import numpy as np
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libficp.so"
+LIB_PATH = Path(os.environ["FICP_LIB"]) if os.environ.get("FICP_LIB") else PKG / "libficp.so"  # FICP_LIB: dev builds
 CSRC = PKG / "csrc"
 HEADER = PKG.parent / "include" / "ficp.h"
 

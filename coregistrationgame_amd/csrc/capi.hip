@@ -86,13 +86,14 @@ int ensure_grid(ficp_ctx *c) {
                                   c->stream));
     g.pts = c->pts.as<TPt>();
     g.cell_start = c->cell_start.as<int32_t>();
+    g.m = m;
     c->gv = g;
     c->grid_ready = true;
     return FICP_OK;
 }
 
 bool use_grid(ficp_ctx *c, int64_t n) {
-    if (c->nn_mode == 1) return false;
+    if (c->nn_mode == 1 || c->m > kMaxGridStems) return false;  // grid limit: brute force
     if (c->nn_mode == 2) return true;
     return (double)n * (double)c->m > 4.0e6;
 }
@@ -118,9 +119,11 @@ int ensure_work(ficp_ctx *c, int64_t n) {
 unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long long>(); }
 
 // NN of the device source (sx, sy, sz) against the target; optional pending transform.
-// With want_keys the sort inputs (key, range, r, matched XY) are produced too.
+// With want_keys the sort inputs (key, range, r, matched XY) are produced too (and dist
+// is not).  warm: 0 = cold search, 1 = record the matched grid slots, 2 = also start
+// every query from its previous match (grid mode, same work order within one run).
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
-            bool want_keys) {
+            bool want_keys, int warm = 0) {
     NNArgs a{};
     a.sx = sx;
     a.sy = sy;
@@ -129,7 +132,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.T = T;
     a.skip = nullptr;
     a.idx = c->idx.as<int32_t>();
-    a.dist = c->dist.as<double>();
+    a.dist = want_keys ? nullptr : c->dist.as<double>();
     a.r = c->r.as<double>();
     a.key = want_keys ? c->key.as<unsigned long long>() : nullptr;
     a.val = nullptr;
@@ -140,6 +143,11 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.range = want_keys ? range_ptr(c) : nullptr;
     if (use_grid(c, n)) {
         CHK(ensure_grid(c));
+        if (warm) {
+            CHK(c->bp.ensure(n * 4));
+            a.out_bp = c->bp.as<int32_t>();
+            a.prev_bp = warm == 2 ? c->bp.as<int32_t>() : nullptr;
+        }
         ProfScope ps(c, P_NN, "nn_grid");
         HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream));
     } else {
@@ -319,7 +327,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
              c->order.as<uint32_t>(), worig, n, c->pivot_x, c->pivot_y, dst};
     for (int s = 0; s < nstages; ++s) {
         const double lam = lambdas[s];
-        CHK(nn_call(c, wx, wy, wz, n, nullptr, true));
+        CHK(nn_call(c, wx, wy, wz, n, nullptr, true, s == 0 ? 1 : 2));
         CHK(sort_and_select(c, n, n, lam, worig));
         CHK(read_state(c));
         CHK(trace_call(c, st, n, lam, worig));
@@ -332,7 +340,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
                 ProfScope ps(c, P_FIT, "fit");
                 HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, nullptr, c->stream));
             }
-            CHK(nn_call(c, wx, wy, wz, n, dst->T, true));
+            CHK(nn_call(c, wx, wy, wz, n, dst->T, true, 2));
             CHK(sort_and_select(c, n, n, lam, worig));
             CHK(read_state(c));
             if (st) {
@@ -437,7 +445,8 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->sort_tmp, &c->frac_tmp, &c->fit_tmp,  &c->bd2,      &c->bidx,
                       &c->ccx,    &c->ccy,        &c->rs,       &c->range,    &c->wx,
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
-                      &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev};
+                      &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
+                      &c->bp};
     for (DevBuf *b : bufs) b->release();
     batch_release(c->batch);
     c->batch = nullptr;

@@ -24,7 +24,7 @@
 struct BatchBufs {
     DevBuf so, to, plot_of, tplot, grids, st, active, bb, lams;
     DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp;
-    DevBuf key, idx, r, ccx, ccy, order, rs, sort_tmp, range;
+    DevBuf key, idx, r, ccx, ccy, order, rs, sort_tmp, range, bp;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
     unsigned int *h_active = nullptr;      // pinned
 };
@@ -36,7 +36,7 @@ void batch_release(BatchBufs *b) {
                       &b->fill,     &b->cell_start, &b->pts,   &b->scan_tmp, &b->key, &b->idx,
                       &b->r,        &b->ccx,     &b->ccy,      &b->order, &b->rs,
                       &b->sort_tmp, &b->range,   &b->sx,       &b->sy,    &b->sz,    &b->tx,
-                      &b->ty,       &b->tz,      &b->stage};
+                      &b->ty,       &b->tz,      &b->stage,    &b->bp};
     for (DevBuf *d : bufs) d->release();
     if (b->h_active) (void)hipHostFree(b->h_active);
     delete b;
@@ -163,6 +163,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         CHK(b.rs.ensure(n * 8));
         CHK(b.sort_tmp.ensure(sort_seg_tmp_bytes(n)));
         CHK(b.range.ensure(range_words(n) * 8));
+        CHK(b.bp.ensure(n * 4));
         // keys of plots that never run (no CHM stems) must be defined for the sort
         HIPCHK(hipMemsetAsync(b.key.p, 0, n * 8, c->stream));
         HIPCHK(launch_fill_plot_ids(b.so.as<int64_t>(), nplots, b.plot_of.as<int32_t>(),
@@ -182,6 +183,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         a.tx = tx;
         a.ty = ty;
         a.range = b.range.as<unsigned long long>();
+        a.out_bp = b.bp.as<int32_t>();
         PlotState *st = b.st.as<PlotState>();
         // every plot makes at most nstages * (max_iter + 1) NN calls
         const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1) + 1;
@@ -193,11 +195,12 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                                         b.so.as<int64_t>(), b.grids.as<PlotGrid>(), nplots,
                                         allow_refl, st, c->stream));
             }
+            a.prev_bp = bit > 0 ? b.bp.as<int32_t>() : nullptr;  // warm start after the first call
             {
                 ProfScope ps(c, P_NN, "nn_grid_batch");
                 HIPCHK(launch_nn_grid_batch(a, b.plot_of.as<int32_t>(), b.grids.as<PlotGrid>(),
-                                            b.pts.as<TPt>(), b.cell_start.as<int32_t>(), st, md,
-                                            c->stream));
+                                            b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
+                                            md, c->stream));
             }
             {
                 ProfScope ps(c, P_SORT, "sort_seg");
@@ -266,7 +269,7 @@ int ficp_run_batch(ficp_ctx *c, int32_t nplots, const int64_t *src_off, double *
     int64_t n = 0, m = 0;
     CHK(check_offsets(src_off, nplots, "source", n));
     CHK(check_offsets(tgt_off, nplots, "target", m));
-    if (n > 0x3fffffff || m > 0x3fffffff) return fail(FICP_EINVAL, "batch too large");
+    if (n > 0x3fffffff || m > kMaxGridStems) return fail(FICP_EINVAL, "batch too large");
     if ((n > 0 && (!src || lds < md)) || (m > 0 && (!tgt || ldt < md)))
         return fail(FICP_EINVAL, "bad source/target arrays");
     BatchBufs &b = *batch_of(c);
@@ -300,7 +303,7 @@ int ficp_run_batch_device(ficp_ctx *c, int32_t nplots, const int64_t *src_off, d
     int64_t n = 0, m = 0;
     CHK(check_offsets(src_off, nplots, "source", n));
     CHK(check_offsets(tgt_off, nplots, "target", m));
-    if (n > 0x3fffffff || m > 0x3fffffff) return fail(FICP_EINVAL, "batch too large");
+    if (n > 0x3fffffff || m > kMaxGridStems) return fail(FICP_EINVAL, "batch too large");
     if ((n > 0 && (!x || !y || (md == 3 && !z))) || (m > 0 && (!tx || !ty || (md == 3 && !tz))))
         return fail(FICP_EINVAL, "bad device arrays");
     return batch_core(c, nplots, src_off, x, y, z, tgt_off, tx, ty, tz, md, nstages, lambdas,

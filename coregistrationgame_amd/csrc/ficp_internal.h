@@ -61,18 +61,32 @@ __device__ __forceinline__ void block_range_store(unsigned long long *range, boo
     }
 }
 
+// XCD-aware block order: the hardware deals workgroups round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, Workgroup dispatch), so block b runs on XCD b % 8.  Returning
+// the logical block (b % 8) * q + min(b % 8, r) + b / 8 (q, r = nb / 8, nb % 8) hands each
+// XCD one contiguous eighth of the work -- with a spatial work order, one compact region
+// of the layer per XCD-private L2 -- and is a bijection on [0, nb).
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t x = b & 7, q = nb >> 3, r = nb & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 struct alignas(32) TPt {
     double x, y, z;
     long long idx;
 };
 
 // Everything an NN kernel needs to search the static CHM grid.
+// grid kernels address the cell-sorted stems (32 B each) through a buffer descriptor
+constexpr int64_t kMaxGridStems = (int64_t)0x7fffffff / 32;
+
 struct GridView {
     const TPt *pts;
     const int32_t *cell_start;  // ncells + 1
     double x0, y0, h, inv_h;
     double margin;              // conservative slack for the ring lower bound (m)
     int gx, gy;
+    int64_t m;                  // stems (pts entries); m * 32 < 2^31 (buffer descriptor)
 };
 
 // Per-launch NN arguments.
@@ -93,6 +107,9 @@ struct NNArgs {
     const double *tx;           // original-order CHM layer (brute path gathers cx, cy)
     const double *ty;
     unsigned long long *range;  // out: key range parts (range_words(n) words; nullable)
+    const int32_t *prev_bp;     // grid kernels: grid slot matched by this query in the previous
+                                // call (warm start; nullable, entries < 0 ignored)
+    int32_t *out_bp;            // grid kernels: out: grid slot matched (nullable; may alias)
 };
 
 // Device-resident state of one ICP stage (written by kernels, read back per iteration).
@@ -238,8 +255,8 @@ hipError_t launch_batch_grid_count(const double *tx, const double *ty, int64_t m
 // NN of every live plot's trees against its own CHM grid; idx = index in the concatenated
 // CHM layer.  Applies states[p].T first where states[p].apply.
 hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
-                                const TPt *pts, const int32_t *cell_start, const PlotState *st,
-                                int md, hipStream_t s);
+                                const TPt *pts, int64_t m, const int32_t *cell_start,
+                                const PlotState *st, int md, hipStream_t s);
 // stable argsort by (segment, key64, position): the distance sort of launch_sort followed
 // by a stable partition by seg[position] (two 8-bit passes, < 65536 segments).
 hipError_t launch_sort_seg(const unsigned long long *key64, const int32_t *seg, int64_t n,

@@ -21,6 +21,7 @@
 #include "ficp_internal.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -49,61 +50,129 @@ __device__ __forceinline__ double sq_dist(double qx, double qy, double qz, doubl
     return s;
 }
 
+// The cell-sorted stems are read through a buffer descriptor: 32-bit per-lane byte
+// offsets, no 64-bit address arithmetic per candidate (cdna_hip_programming.md T8).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef FICP_NN_UNROLL
+#define FICP_NN_UNROLL 2  // candidate loads in flight per lane (2: best of 1, 2, 4, 8 at C3)
+#endif
+
+struct Stems {
+    __amdgpu_buffer_rsrc_t r;
+};
+
+__device__ __forceinline__ Stems stems_of(const TPt *pts, int64_t m) {
+    Stems st;
+    st.r = __builtin_amdgcn_make_buffer_rsrc((void *)pts, 0, (int)(m * (int64_t)sizeof(TPt)),
+                                             0x00020000);
+    return st;
+}
+
+// best candidate so far: d2, stem index (tie-break), grid slot
+struct Best {
+    double d2;
+    int id, slot;
+};
+
 template <int MD>
-__device__ __forceinline__ void scan_pts(const TPt *__restrict__ pts, int p0, int p1, double qx,
-                                         double qy, double qz, double &best, int &bi, int &bp) {
-    for (int p = p0; p < p1; ++p) {
-        const double4 a = *reinterpret_cast<const double4 *>(pts + p);
-        double s = sq_dist<MD>(qx, qy, qz, a.x, a.y, a.z);
-        int id = (int)__double_as_longlong(a.w);
-        bool b = (s < best) | ((s == best) & (id < bi));
-        best = b ? s : best;
-        bi = b ? id : bi;
-        bp = b ? p : bp;
+__device__ __forceinline__ void eval_slot(const Stems &S, int p, double qx, double qy, double qz,
+                                          Best &b) {
+    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32, 0, 0);
+    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32 + 16, 0, 0);
+    const double2 xy = __builtin_bit_cast(double2, lo);
+    const double pz = __builtin_bit_cast(double2, hi).x;
+    const int id = (int)hi.z;
+    const double s = sq_dist<MD>(qx, qy, qz, xy.x, xy.y, pz);
+    // strict < keeps the best; an equal distance goes to the lower stem index
+    const bool take = (s < b.d2) | ((s == b.d2) & (id < b.id));
+    b.d2 = take ? s : b.d2;
+    b.id = take ? id : b.id;
+    b.slot = take ? p : b.slot;
+}
+
+// stems [p0, p1) of the cell-sorted layer, several loads in flight per step (a step past
+// the end re-reads the last stem: evaluating a candidate twice changes nothing)
+template <int MD>
+__device__ __forceinline__ void scan_pts(const Stems &S, int p0, int p1, double qx, double qy,
+                                         double qz, Best &b) {
+    for (int p = p0; p < p1; p += FICP_NN_UNROLL) {
+#pragma unroll
+        for (int u = 0; u < FICP_NN_UNROLL; ++u)
+            eval_slot<MD>(S, min(p + u, p1 - 1), qx, qy, qz, b);
     }
 }
 
+// gap between q and the band [v0 + c0 h, v0 + c1 h) along one axis, less the margin
+__device__ __forceinline__ double band_gap(double q, double v0, double h, int c0, int c1,
+                                           double mq) {
+    const double lo = v0 + (double)c0 * h, hi = v0 + (double)c1 * h;
+    return fmax(fmax(lo - q, q - hi), 0.0) - mq;
+}
+
+__device__ __forceinline__ bool beyond(double gap, double d2) { return gap > 0.0 && gap * gap > d2; }
+
+__device__ __forceinline__ double query_margin(const GridView &g, double qx, double qy) {
+    return g.margin + 1e-15 * (fabs(qx) + fabs(qy));
+}
+
+// Disk-clipped row scan: every stem within sqrt(best) of q (in XY, a lower bound of the
+// md-dimensional distance) lies in a row band whose y-gap is <= sqrt(best) and, inside
+// that row, within +-sqrt(best - gap^2) of qx.  Rows are visited outward from q's own
+// row and each row scans only the cells under that chord, so the work follows the
+// shrinking disk of the best match.  Requires a finite best on entry.
 template <int MD>
-__device__ __forceinline__ void grid_query(const GridView &g, double qx, double qy, double qz,
-                                           double &best, int &bi, int &bp) {
+__device__ __forceinline__ void disk_scan(const GridView &g, const Stems &S, double qx, double qy,
+                                          double qz, int cy, double mq, Best &b) {
+    for (int k = 0;; ++k) {
+        bool any = false;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            if (k == 0 && side == 1) continue;
+            const int yy = side ? cy + k : cy - k;
+            if (yy < 0 || yy >= g.gy) continue;
+            const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
+            if (beyond(gy, b.d2)) continue;
+            any = true;
+            const double gy0 = fmax(gy, 0.0);
+            const double w = sqrt(fmax(b.d2 - gy0 * gy0, 0.0)) + mq;
+            const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
+            const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
+            const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+            scan_pts<MD>(S, row[xl], row[xh + 1], qx, qy, qz, b);
+        }
+        if (!any) break;  // both rows at this offset are beyond the disk: so are all farther
+    }
+}
+
+// Exact 1-NN: a finite first bound from q's own cell (or the warm-start stem, or the
+// first non-empty ring), then the disk-clipped rows.
+template <int MD>
+__device__ __forceinline__ void grid_nn(const GridView &g, const Stems &S, double qx, double qy,
+                                        double qz, Best &b) {
     const int cx = cell_coord(qx, g.x0, g.inv_h, g.gx);
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
-    const double mq = g.margin + 1e-15 * (fabs(qx) + fabs(qy));
-    for (int r = 0;; ++r) {
-        const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
-        const int ylo = max(ya, 0), yhi = min(yb, g.gy - 1);
-        const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);
-        for (int yy = ylo; yy <= yhi; ++yy) {
-            const double by0 = g.y0 + (double)yy * g.h;
-            const double by1 = by0 + g.h;
-            const double gyap = fmax(fmax(by0 - qy, qy - by1), 0.0) - mq;
-            if (gyap > 0.0 && gyap * gyap > best) continue;
-            const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
-            if (yy == ya || yy == yb) {
-                scan_pts<MD>(g.pts, row[xlo], row[xhi + 1], qx, qy, qz, best, bi, bp);
-            } else {
-                if (xa >= 0) {
-                    const double gx0 = qx - (g.x0 + (double)(xa + 1) * g.h) - mq;
-                    if (!(gx0 > 0.0 && gx0 * gx0 > best))
-                        scan_pts<MD>(g.pts, row[xa], row[xa + 1], qx, qy, qz, best, bi, bp);
-                }
-                if (xb < g.gx) {
-                    const double gx1 = (g.x0 + (double)xb * g.h) - qx - mq;
-                    if (!(gx1 > 0.0 && gx1 * gx1 > best))
-                        scan_pts<MD>(g.pts, row[xb], row[xb + 1], qx, qy, qz, best, bi, bp);
+    const double mq = query_margin(g, qx, qy);
+    if (!(b.d2 < INFINITY)) {
+        const int32_t *row = g.cell_start + (int64_t)cy * g.gx;
+        scan_pts<MD>(S, row[cx], row[cx + 1], qx, qy, qz, b);
+        for (int r = 1; !(b.d2 < INFINITY); ++r) {  // empty cell: grow square rings
+            const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
+            if (xa < 0 && ya < 0 && xb >= g.gx && yb >= g.gy) break;  // empty layer
+            const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);
+            for (int yy = max(ya, 0); yy <= min(yb, g.gy - 1); ++yy) {
+                const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
+                if (yy == ya || yy == yb) {
+                    scan_pts<MD>(S, rw[xlo], rw[xhi + 1], qx, qy, qz, b);
+                } else {
+                    if (xa >= 0) scan_pts<MD>(S, rw[xa], rw[xa + 1], qx, qy, qz, b);
+                    if (xb < g.gx) scan_pts<MD>(S, rw[xb], rw[xb + 1], qx, qy, qz, b);
                 }
             }
         }
-        // lower bound on the distance from q to any cell outside the scanned block
-        double lb = INFINITY;
-        if (xa > 0) lb = fmin(lb, qx - (g.x0 + (double)xa * g.h));
-        if (xb < g.gx - 1) lb = fmin(lb, (g.x0 + (double)(xb + 1) * g.h) - qx);
-        if (ya > 0) lb = fmin(lb, qy - (g.y0 + (double)ya * g.h));
-        if (yb < g.gy - 1) lb = fmin(lb, (g.y0 + (double)(yb + 1) * g.h) - qy);
-        if (lb == INFINITY) break;  // the block already covers the whole grid
-        lb -= mq;
-        if (lb > 0.0 && lb * lb > best) break;
+        if (!(b.d2 < INFINITY)) return;
     }
+    disk_scan<MD>(g, S, qx, qy, qz, cy, mq, b);
 }
 
 __device__ __forceinline__ void apply_T(const double *__restrict__ T, double &x, double &y) {
@@ -115,7 +184,7 @@ __device__ __forceinline__ void apply_T(const double *__restrict__ T, double &x,
     y = ny;
 }
 
-// per-point outputs; returns the sort key (for the wave's key-range reduction)
+// per-point outputs; returns the sort key
 __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t i, double best,
                                                         int bi) {
     a.idx[i] = bi;
@@ -128,31 +197,51 @@ __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t
     return k;
 }
 
+// Per-query finish: matched slot, correspondence XY, idx/dist/r/key; folds the key into
+// this thread's range accumulator.
+__device__ __forceinline__ void finish(const NNArgs &a, const Stems &S, int64_t i, const Best &b,
+                                       unsigned long long &kmin_c, unsigned long long &kmax) {
+    if (a.out_bp) a.out_bp[i] = b.slot;
+    if (a.cx) {  // the matched stem's XY from the grid record (L1/L2 hot)
+        const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, b.slot * 32, 0, 0);
+        const double2 c = __builtin_bit_cast(double2, lo);
+        a.cx[i] = c.x;
+        a.cy[i] = c.y;
+    }
+    const unsigned long long k = write_out(a, i, b.d2, b.id);
+    kmin_c = max(kmin_c, ~k);
+    kmax = max(kmax, k);
+}
+
+// Exact 1-NN of one query (lane): warm start from the stem it matched in the previous
+// call, then the disk-clipped row scan of grid_nn.
+template <int MD>
+__device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, const Stems &S,
+                                         int64_t i, const double *T, unsigned long long &kmin_c,
+                                         unsigned long long &kmax) {
+    double qx = a.sx[i], qy = a.sy[i];
+    if (T) {
+        apply_T(T, qx, qy);
+        a.sx[i] = qx;
+        a.sy[i] = qy;
+    }
+    const double qz = (MD == 3) ? a.sz[i] : 0.0;
+    Best b{INFINITY, 0x7fffffff, 0};
+    if (a.prev_bp) {
+        const int pb = a.prev_bp[i];
+        if (pb >= 0) eval_slot<MD>(S, pb, qx, qy, qz, b);
+    }
+    grid_nn<MD>(g, S, qx, qy, qz, b);
+    finish(a, S, i, b, kmin_c, kmax);
+}
+
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     if (a.skip && *a.skip) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = i < a.n;
-    unsigned long long key = 0;
-    if (valid) {
-        double qx = a.sx[i], qy = a.sy[i];
-        if (APPLY) {
-            apply_T(a.T, qx, qy);
-            a.sx[i] = qx;
-            a.sy[i] = qy;
-        }
-        const double qz = (MD == 3) ? a.sz[i] : 0.0;
-        double best = INFINITY;
-        int bi = 0x7fffffff, bp = 0;
-        grid_query<MD>(g, qx, qy, qz, best, bi, bp);
-        if (a.cx) {  // correspondence XY straight from the grid record just scanned (cache hot)
-            const double2 c = *reinterpret_cast<const double2 *>(g.pts + bp);
-            a.cx[i] = c.x;
-            a.cy[i] = c.y;
-        }
-        key = write_out(a, i, best, bi);
-    }
-    if (a.range) block_range_store(a.range, valid, ~key, key);
+    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    unsigned long long kmin_c = 0, kmax = 0;
+    if (i < a.n) nn_query<MD>(a, g, stems_of(g.pts, g.m), i, APPLY ? a.T : nullptr, kmin_c, kmax);
+    if (a.range) block_range_store(a.range, true, kmin_c, kmax);
 }
 
 // Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against
@@ -160,49 +249,33 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
 template <int MD>
 __global__ __launch_bounds__(256) void k_nn_grid_batch(NNArgs a, const int32_t *__restrict__ plot_of,
                                                        const PlotGrid *__restrict__ grids,
-                                                       const TPt *__restrict__ pts,
+                                                       const TPt *__restrict__ pts, int64_t m,
                                                        const int32_t *__restrict__ cell_start,
                                                        const PlotState *__restrict__ st) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool valid = i < a.n;
-    int p = 0;
-    bool live = false;
-    unsigned long long key = 0;
-    if (valid) {
-        p = plot_of[i];
-        live = st[p].phase != PH_DONE;  // converged plots keep their last outputs, but
-        if (!live) key = a.key[i];      // their keys stay inside the sort's key range
-    }
-    if (live) {
-        const PlotGrid pg = grids[p];
-        double qx = a.sx[i], qy = a.sy[i];
-        if (st[p].apply) {
-            apply_T(st[p].T, qx, qy);
-            a.sx[i] = qx;
-            a.sy[i] = qy;
+    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    unsigned long long kmin_c = 0, kmax = 0;
+    if (i < a.n) {
+        const int p = plot_of[i];
+        if (st[p].phase != PH_DONE) {
+            const PlotGrid pg = grids[p];
+            GridView g;
+            g.pts = pts;
+            g.cell_start = cell_start + pg.cell_base;
+            g.x0 = pg.x0;
+            g.y0 = pg.y0;
+            g.h = pg.h;
+            g.inv_h = pg.inv_h;
+            g.margin = pg.margin;
+            g.gx = pg.gx;
+            g.gy = pg.gy;
+            g.m = m;
+            nn_query<MD>(a, g, stems_of(pts, m), i, st[p].apply ? st[p].T : nullptr, kmin_c, kmax);
+        } else {  // converged plot: its last outputs stay, its keys stay inside the range
+            kmin_c = ~a.key[i];
+            kmax = a.key[i];
         }
-        const double qz = (MD == 3) ? a.sz[i] : 0.0;
-        GridView g;
-        g.pts = pts;
-        g.cell_start = cell_start + pg.cell_base;
-        g.x0 = pg.x0;
-        g.y0 = pg.y0;
-        g.h = pg.h;
-        g.inv_h = pg.inv_h;
-        g.margin = pg.margin;
-        g.gx = pg.gx;
-        g.gy = pg.gy;
-        double best = INFINITY;
-        int bi = 0x7fffffff, bp = 0;
-        grid_query<MD>(g, qx, qy, qz, best, bi, bp);
-        if (a.cx) {
-            const double2 c = *reinterpret_cast<const double2 *>(pts + bp);
-            a.cx[i] = c.x;
-            a.cy[i] = c.y;
-        }
-        key = write_out(a, i, best, bi);
     }
-    if (a.range) block_range_store(a.range, valid, ~key, key);
+    if (a.range) block_range_store(a.range, true, kmin_c, kmax);
 }
 
 constexpr int kTile = 256;
@@ -516,8 +589,9 @@ hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t n
     return hipGetLastError();
 }
 
-hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s) {
-    if (a.n == 0) return hipSuccess;
+hipError_t launch_nn_grid(const NNArgs &a0, const GridView &g, int md, hipStream_t s) {
+    if (a0.n == 0) return hipSuccess;
+    const NNArgs &a = a0;
     dim3 grid(nblk(a.n)), blk(256);
     if (md == 3) {
         if (a.T) hipLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, a, g);
@@ -616,15 +690,15 @@ hipError_t launch_scatter_xy(const uint32_t *worig, const double *wx, const doub
 }
 
 hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
-                                const TPt *pts, const int32_t *cell_start, const PlotState *st,
-                                int md, hipStream_t s) {
+                                const TPt *pts, int64_t m, const int32_t *cell_start,
+                                const PlotState *st, int md, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     if (md == 3)
         hipLaunchKernelGGL(k_nn_grid_batch<3>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
-                           pts, cell_start, st);
+                           pts, m, cell_start, st);
     else
         hipLaunchKernelGGL(k_nn_grid_batch<2>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
-                           pts, cell_start, st);
+                           pts, m, cell_start, st);
     if (a.range) return launch_range_reduce(a.range, nblk(a.n), s);
     return hipGetLastError();
 }

@@ -1,0 +1,43 @@
+"""Per-kernel averages of the PMC passes written by tools/pmc.sh (counter_collection.csv).
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KB per dispatch.  On gfx950
+FETCH_SIZE reports half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md,
+HBM section): `fetch_bytes_corrected` doubles it; other access widths are uncalibrated,
+so both values are kept."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"::(k_[a-z0-9_]+)(<[^>]*>)?\(", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+
+
+def main(root):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r.get("Kernel_Name", ""))
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k, ctrs in acc.items():
+        d = {c: sum(v) / len(v) for c, v in ctrs.items()}
+        d["dispatches"] = max(len(v) for v in ctrs.values())
+        if "FETCH_SIZE" in d:
+            d["fetch_bytes_raw"] = d["FETCH_SIZE"] * 1024.0
+            d["fetch_bytes_corrected"] = 2.0 * d["FETCH_SIZE"] * 1024.0
+        if "WRITE_SIZE" in d:
+            d["write_bytes"] = d["WRITE_SIZE"] * 1024.0
+        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"] > 0:
+            d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+        out[k] = d
+    json.dump(dict(sorted(out.items())), sys.stdout, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

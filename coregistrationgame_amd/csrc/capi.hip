@@ -123,14 +123,16 @@ unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long lo
 // is not).  warm: 0 = cold search, 1 = record the matched grid slots, 2 = also start
 // every query from its previous match (grid mode, same work order within one run).
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
-            bool want_keys, int warm = 0) {
+            bool want_keys, int warm = 0, const int *skip = nullptr,
+            const int *apply_flag = nullptr) {
     NNArgs a{};
     a.sx = sx;
     a.sy = sy;
     a.sz = sz;
     a.n = n;
     a.T = T;
-    a.skip = nullptr;
+    a.skip = skip;
+    a.apply_flag = apply_flag;
     a.idx = c->idx.as<int32_t>();
     a.dist = want_keys ? nullptr : c->dist.as<double>();
     a.r = c->r.as<double>();
@@ -148,18 +150,25 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             a.out_bp = c->bp.as<int32_t>();
             a.prev_bp = warm == 2 ? c->bp.as<int32_t>() : nullptr;
         }
-        ProfScope ps(c, P_NN, "nn_grid");
-        HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream));
+        {
+            ProfScope ps(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
+            HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream, false));
+        }
+        if (a.range) HIPCHK(launch_range_reduce(a.range, nn_range_parts(n, c->m, true), c->stream));
     } else {
         const int64_t nch = brute_chunk_count(n, c->m);
         if (nch > 1) {
             CHK(c->bd2.ensure(nch * n * 8));
             CHK(c->bidx.ensure(nch * n * 4));
         }
-        ProfScope ps(c, P_NN, "nn_brute");
-        HIPCHK(launch_nn_brute(a, c->tx.as<double>(), c->ty.as<double>(),
-                               c->md == 3 ? c->tz.as<double>() : nullptr, c->m, c->md,
-                               c->bd2.as<double>(), c->bidx.as<int32_t>(), c->stream));
+        {
+            ProfScope ps(c, P_NN, "nn_brute");
+            HIPCHK(launch_nn_brute(a, c->tx.as<double>(), c->ty.as<double>(),
+                                   c->md == 3 ? c->tz.as<double>() : nullptr, c->m, c->md,
+                                   c->bd2.as<double>(), c->bidx.as<int32_t>(), c->stream, false));
+        }
+        if (a.range)
+            HIPCHK(launch_range_reduce(a.range, nn_range_parts(n, c->m, false), c->stream));
     }
     return FICP_OK;
 }
@@ -216,18 +225,19 @@ int check_sort(ficp_ctx *c, int64_t n, const uint32_t *orig, const char *what) {
 }
 
 // sort (key, orig) of the last NN call, then the FRMSD fraction scan
-int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam, const uint32_t *orig) {
+int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam, const uint32_t *orig,
+                    const int *skip = nullptr, const double *lam_dev = nullptr) {
     {
         ProfScope ps(c, P_SORT, "sort");
         HIPCHK(launch_sort(c->key.as<unsigned long long>(), orig, n, range_ptr(c),
                            c->order.as<uint32_t>(), c->r.as<double>(), c->rs.as<double>(),
-                           c->sort_tmp.p, nullptr, c->stream));
+                           c->sort_tmp.p, skip, c->stream));
     }
     CHK(check_sort(c, n, orig, "residual sort"));
     {
         ProfScope ps(c, P_FRAC, "fraction");
-        HIPCHK(launch_fraction(c->rs.as<double>(), n, N, lam, c->frac_tmp.p,
-                               c->state_dev.as<IterState>(), nullptr, c->stream));
+        HIPCHK(launch_fraction(c->rs.as<double>(), n, N, lam, lam_dev, c->frac_tmp.p,
+                               c->state_dev.as<IterState>(), skip, c->stream));
     }
     return FICP_OK;
 }
@@ -236,38 +246,6 @@ int read_state(ficp_ctx *c) {
     HIPCHK(hipMemcpyAsync(c->h_state, c->state_dev.p, sizeof(IterState), hipMemcpyDeviceToHost,
                           c->stream));
     return sync(c);
-}
-
-void mat3_mul(const double A[9], const double B[9], double C[9]) {
-    double R[9];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j)
-            R[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
-    memcpy(C, R, sizeof R);
-}
-
-int trace_call(ficp_ctx *c, ficp_stats *st, int64_t n, double lam, const uint32_t *worig) {
-    if (!st) return FICP_OK;
-    const int32_t call = st->n_nn_calls;
-    st->n_nn_calls++;
-    st->k_last = c->h_state->k;
-    if (call >= st->max_trace) return FICP_OK;
-    if (st->trace_k) st->trace_k[call] = c->h_state->k;
-    if (st->trace_frmsd) st->trace_frmsd[call] = c->h_state->frmsd;
-    if (st->trace_lambda) st->trace_lambda[call] = lam;
-    if (st->trace_idx && n > 0) {
-        const void *src = c->idx.p;
-        if (worig) {  // back to the caller's row order
-            CHK(c->tidx.ensure(n * 4));
-            HIPCHK(launch_scatter_i32(worig, c->idx.as<int32_t>(), n, c->tidx.as<int32_t>(),
-                                      c->stream));
-            src = c->tidx.p;
-        }
-        HIPCHK(hipMemcpyAsync(st->trace_idx + (int64_t)call * n, src, n * 4,
-                              hipMemcpyDeviceToHost, c->stream));
-        CHK(sync(c));
-    }
-    return FICP_OK;
 }
 
 // Spatial work order: the source permuted into 8x8-cell supertile order of the CHM grid
@@ -325,38 +303,92 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     IterState *dst = c->state_dev.as<IterState>();
     FitIn fa{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
              c->order.as<uint32_t>(), worig, n, c->pivot_x, c->pivot_y, dst};
-    for (int s = 0; s < nstages; ++s) {
-        const double lam = lambdas[s];
-        CHK(nn_call(c, wx, wy, wz, n, nullptr, true, s == 0 ? 1 : 2));
-        CHK(sort_and_select(c, n, n, lam, worig));
-        CHK(read_state(c));
-        CHK(trace_call(c, st, n, lam, worig));
-        if (c->h_state->k == 0) continue;
-        double cur = c->h_state->frmsd;
-        if (st) st->frmsd_last[s < 2 ? s : 1] = cur;
-        int it = 0;
-        while (it < max_iter) {
-            {
-                ProfScope ps(c, P_FIT, "fit");
-                HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, nullptr, c->stream));
-            }
-            CHK(nn_call(c, wx, wy, wz, n, dst->T, true, 2));
-            CHK(sort_and_select(c, n, n, lam, worig));
-            CHK(read_state(c));
-            if (st) {
-                if (st->trace_T && st->n_fits < st->max_trace)
-                    memcpy(st->trace_T + 9 * st->n_fits, c->h_state->T, 9 * sizeof(double));
-                st->n_fits++;
-                mat3_mul(c->h_state->T, st->T_total, st->T_total);
-            }
-            CHK(trace_call(c, st, n, lam, worig));
-            const double nw = c->h_state->frmsd;
-            if (st) st->frmsd_last[s < 2 ? s : 1] = nw;
-            if (cur - nw <= threshold) break;  // ficp.py:142 (transform already applied)
-            cur = nw;
-            ++it;
+    // loop parameters and traces live on the device (k_loop.hip)
+    LoopCtl lc{};
+    lc.nstages = nstages;
+    lc.max_iter = max_iter;
+    lc.threshold = threshold;
+    CHK(c->lams.ensure((size_t)std::max(nstages, 1) * 8));
+    if (nstages > 0)
+        HIPCHK(hipMemcpyAsync(c->lams.p, lambdas, (size_t)nstages * 8, hipMemcpyHostToDevice,
+                              c->stream));
+    lc.lams = c->lams.as<double>();
+    const int mt = (st && st->max_trace > 0) ? st->max_trace : 0;
+    int32_t *tidx = nullptr;
+    if (mt > 0) {
+        lc.max_trace = mt;
+        CHK(c->tr_k.ensure((size_t)mt * 8));
+        CHK(c->tr_f.ensure((size_t)mt * 8));
+        CHK(c->tr_l.ensure((size_t)mt * 8));
+        CHK(c->tr_T.ensure((size_t)mt * 72));
+        lc.tk = c->tr_k.as<long long>();
+        lc.tf = c->tr_f.as<double>();
+        lc.tl = c->tr_l.as<double>();
+        lc.tT = c->tr_T.as<double>();
+        if (st->trace_idx) {
+            if ((double)mt * (double)n * 4.0 > 8e9)
+                return fail(FICP_EINVAL, "trace_idx of %d calls x %lld rows is too large", mt,
+                            (long long)n);
+            CHK(c->tr_idx.ensure((size_t)mt * (size_t)n * 4));
+            tidx = c->tr_idx.as<int32_t>();
         }
-        if (st && s < 2) st->iters[s] = it;
+    }
+    HIPCHK(launch_loop_init(dst, lc, c->stream));
+    // Iterations are enqueued `la` ahead of the one whose done flag the host reads, so
+    // the device never waits for the host; the iterations enqueued past the end are
+    // no-ops (every kernel tests the flags k_loop_update set).
+    static const int la = std::min(
+        kLoopRing - 1, getenv("FICP_LOOKAHEAD") ? std::max(1, atoi(getenv("FICP_LOOKAHEAD"))) : 2);
+    const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1);
+    int64_t j = 0;
+    bool finished = nstages <= 0;
+    for (; j < cap && !finished; ++j) {
+        {
+            ProfScope ps(c, P_FIT, "fit");
+            HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, &dst->no_fit, c->stream));
+        }
+        CHK(nn_call(c, wx, wy, wz, n, dst->T, true, j == 0 ? 1 : 2, &dst->done, &dst->apply));
+        CHK(sort_and_select(c, n, n, 0.0, worig, &dst->done, &dst->lam_cur));
+        if (tidx) HIPCHK(launch_trace_idx(dst, c->idx.as<int32_t>(), worig, n, tidx, mt, c->stream));
+        HIPCHK(launch_loop_update(dst, lc, c->stream));
+        const int slot = (int)(j % kLoopRing);
+        HIPCHK(hipMemcpyAsync(&c->h_flags[slot], &dst->done, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(c->loop_ev[slot], c->stream));
+        if (j >= la) {
+            const int old = (int)((j - la) % kLoopRing);
+            HIPCHK(hipEventSynchronize(c->loop_ev[old]));
+            finished = c->h_flags[old] != 0;
+        }
+    }
+    CHK(read_state(c));
+    if (!c->h_state->done) return fail(FICP_EHIP, "device ICP loop did not finish");
+    if (st) {
+        const IterState &h = *c->h_state;
+        st->n_nn_calls = h.n_nn;
+        st->n_fits = h.n_fit;
+        st->iters[0] = h.iters[0];
+        st->iters[1] = h.iters[1];
+        st->k_last = h.k_last;
+        st->frmsd_last[0] = h.frmsd_last[0];
+        st->frmsd_last[1] = h.frmsd_last[1];
+        memcpy(st->T_total, h.Ttot, sizeof st->T_total);
+        const int nc = std::min(h.n_nn, mt), nf = std::min(h.n_fit, mt);
+        if (nc > 0) {
+            if (st->trace_k)
+                HIPCHK(hipMemcpyAsync(st->trace_k, c->tr_k.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
+            if (st->trace_frmsd)
+                HIPCHK(hipMemcpyAsync(st->trace_frmsd, c->tr_f.p, nc * 8, hipMemcpyDeviceToHost,
+                                      c->stream));
+            if (st->trace_lambda)
+                HIPCHK(hipMemcpyAsync(st->trace_lambda, c->tr_l.p, nc * 8, hipMemcpyDeviceToHost,
+                                      c->stream));
+            if (tidx)
+                HIPCHK(hipMemcpyAsync(st->trace_idx, tidx, (size_t)nc * (size_t)n * 4,
+                                      hipMemcpyDeviceToHost, c->stream));
+        }
+        if (nf > 0 && st->trace_T)
+            HIPCHK(hipMemcpyAsync(st->trace_T, c->tr_T.p, (size_t)nf * 72, hipMemcpyDeviceToHost,
+                                  c->stream));
     }
     if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -426,6 +458,10 @@ int ficp_create(int device, ficp_ctx **out) {
         e = hipHostMalloc((void **)&c->h_state, sizeof(IterState), hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess)
+        e = hipHostMalloc((void **)&c->h_flags, kLoopRing * sizeof(int), hipHostMallocDefault);
+    for (int k = 0; k < kLoopRing && e == hipSuccess; ++k)
+        e = hipEventCreateWithFlags(&c->loop_ev[k], hipEventDisableTiming);
     if (e != hipSuccess) {
         delete c;
         return fail(FICP_EHIP, "context setup: %s", hipGetErrorString(e));
@@ -446,7 +482,8 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->ccx,    &c->ccy,        &c->rs,       &c->range,    &c->wx,
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
-                      &c->bp};
+                      &c->bp,     &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
+                      &c->tr_T,   &c->tr_idx};
     for (DevBuf *b : bufs) b->release();
     batch_release(c->batch);
     c->batch = nullptr;
@@ -458,6 +495,9 @@ void ficp_destroy(ficp_ctx *c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->h_flags) (void)hipHostFree(c->h_flags);
+    for (hipEvent_t &e : c->loop_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

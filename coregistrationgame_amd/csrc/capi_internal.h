@@ -86,6 +86,7 @@ struct ProfRec {
 using namespace ficp_capi;
 
 struct BatchBufs;  // capi_batch.hip
+constexpr int kLoopRing = 16;  // in-flight iterations of the device ICP loop (>= lookahead + 1)
 void batch_release(BatchBufs *b);
 
 struct ficp_ctx {
@@ -111,6 +112,9 @@ struct ficp_ctx {
     DevBuf wx, wy, wz, worig, tidx;  // spatial work order of the source
     DevBuf stage, stage2, cx, cy, cz, state_dev;
     DevBuf bp;  // grid slot of each query's last match (warm start of the next NN call)
+    DevBuf lams, tr_k, tr_f, tr_l, tr_T, tr_idx;  // device loop: lambdas and traces
+    int *h_flags = nullptr;                        // pinned ring of per-iteration done flags
+    hipEvent_t loop_ev[kLoopRing] = {};
     IterState *h_state = nullptr;  // pinned
 
     // profiling

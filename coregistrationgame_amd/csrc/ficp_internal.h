@@ -110,9 +110,12 @@ struct NNArgs {
     const int32_t *prev_bp;     // grid kernels: grid slot matched by this query in the previous
                                 // call (warm start; nullable, entries < 0 ignored)
     int32_t *out_bp;            // grid kernels: out: grid slot matched (nullable; may alias)
+    const int *apply_flag;      // T is applied only while *apply_flag != 0 (nullable: always)
 };
 
 // Device-resident state of one ICP stage (written by kernels, read back per iteration).
+enum PlotPhase { PH_HEAD = 0, PH_LOOP = 1, PH_DONE = 2 };
+
 struct alignas(16) IterState {
     double T[9];           // last fit
     double pad0;
@@ -122,8 +125,34 @@ struct alignas(16) IterState {
     long long n_src;       // N
     double csx, csy, ctx, cty;  // centroids of the last fit (relative to the pivot)
     double H[4];
-    int done;              // set by the fit/scan kernels when nothing is left to do
+    // ---- device-resident ICP loop (k_loop_update: ficp.py:122-154 on the device)
+    double Ttot[9];        // composite transform of the run
+    double cur;            // current FRMSD (ficp.py:129, 144)
+    double lam_cur;        // lambda of the stage in progress (read by the fraction kernels)
+    double frmsd_last[2];  // last FRMSD of stages 1 and 2
+    long long k_last;      // k of the last fraction call
+    int phase;             // PlotPhase: HEAD (stage start), LOOP, DONE
+    int stage, it;         // stage in progress, loop bodies completed in it
+    int n_nn, n_fit;       // NN/fraction calls and fits so far
+    int iters[2];          // loop bodies of stages 1 and 2
+    int done;              // 1 once the run is over: NN, sort and scan are no-ops
+    int no_fit;            // 1 unless a loop body is due: the fit is a no-op
+    int apply;             // the NN call applies T (a fit ran in this iteration)
     int pad1;
+};
+
+// Loop parameters and optional trace buffers of the device-resident loop.
+struct LoopCtl {
+    const double *lams;    // [nstages] on the device
+    int nstages;
+    int max_iter;
+    double threshold;
+    int max_trace;         // capacity of the trace buffers (NN calls), 0 = no trace
+    int pad;
+    long long *tk;         // [max_trace] k per call
+    double *tf;            // [max_trace] FRMSD per call
+    double *tl;            // [max_trace] lambda per call
+    double *tT;            // [max_trace * 9] fits in order
 };
 
 // ----------------------------------------------------------------- launchers
@@ -138,11 +167,15 @@ hipError_t launch_grid_scatter(const double *x, const double *y, const double *z
                                int32_t *fill, TPt *pts, hipStream_t s);
 hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t ncells,
                                   hipStream_t s);
-hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s);
+// The NN launchers finish with launch_range_reduce when a.range is set, unless
+// reduce_range is false (then the caller launches it, over nn_range_parts workgroups).
+hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s,
+                          bool reduce_range = true);
+int64_t nn_range_parts(int64_t n, int64_t m, bool grid);
 int64_t brute_chunk_count(int64_t n, int64_t m);  // target chunks of the brute kernel
 hipError_t launch_nn_brute(const NNArgs &a, const double *tx, const double *ty,
                            const double *tz, int64_t m, int md, double *part_d2,
-                           int32_t *part_idx, hipStream_t s);
+                           int32_t *part_idx, hipStream_t s, bool reduce_range = true);
 hipError_t launch_deinterleave(const double *rows, int64_t n, int64_t ld, int ncols,
                                double *c0, double *c1, double *c2, hipStream_t s);
 hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, double *out_xy,
@@ -195,7 +228,13 @@ hipError_t launch_residuals(const double *sx, const double *sy, const double *sz
                             const double *cx, const double *cy, const double *cz, int64_t n,
                             int md, double *r, hipStream_t s);
 // argmin_k FRMSD(k) over r in selection order (rs) -> st->k, st->frac, st->frmsd
+// device-resident ICP loop (k_loop.hip)
+hipError_t launch_loop_init(IterState *st, const LoopCtl &c, hipStream_t s);
+hipError_t launch_loop_update(IterState *st, const LoopCtl &c, hipStream_t s);
+hipError_t launch_trace_idx(const IterState *st, const int32_t *idx, const uint32_t *worig,
+                            int64_t n, int32_t *out, int max_trace, hipStream_t s);
 hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double lambda_val,
+                           const double *lam_dev,
                            void *tmp, IterState *st, const int *skip, hipStream_t s);
 // Rigid fit of source (sx, sy) onto its correspondences (cx, cy).  With key != null the
 // selected rows are the first st->k entries of the stable order (order, key); with
@@ -228,7 +267,6 @@ struct PlotGrid {
     int pad;
 };
 
-enum PlotPhase { PH_HEAD = 0, PH_LOOP = 1, PH_DONE = 2 };
 
 // Device-resident per-plot ICP state (the _iterate loop of ficp.py:122-147 per plot).
 struct alignas(16) PlotState {

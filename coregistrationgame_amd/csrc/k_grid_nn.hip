@@ -240,7 +240,8 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     if (a.skip && *a.skip) return;
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     unsigned long long kmin_c = 0, kmax = 0;
-    if (i < a.n) nn_query<MD>(a, g, stems_of(g.pts, g.m), i, APPLY ? a.T : nullptr, kmin_c, kmax);
+    const double *T = (APPLY && (!a.apply_flag || *a.apply_flag)) ? a.T : nullptr;
+    if (i < a.n) nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
     if (a.range) block_range_store(a.range, true, kmin_c, kmax);
 }
 
@@ -376,8 +377,9 @@ __global__ __launch_bounds__(256) void k_nn_merge(NNArgs a, int nchunks, const d
 }
 
 __global__ __launch_bounds__(256) void k_apply_inplace(double *x, double *y, int64_t n,
-                                                       const double *T, const int *skip) {
-    if (skip && *skip) return;
+                                                       const double *T, const int *skip,
+                                                       const int *apply_flag) {
+    if ((skip && *skip) || (apply_flag && !*apply_flag)) return;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double qx = x[i], qy = y[i];
@@ -589,9 +591,9 @@ hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t n
     return hipGetLastError();
 }
 
-hipError_t launch_nn_grid(const NNArgs &a0, const GridView &g, int md, hipStream_t s) {
-    if (a0.n == 0) return hipSuccess;
-    const NNArgs &a = a0;
+hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s,
+                          bool reduce_range) {
+    if (a.n == 0) return hipSuccess;
     dim3 grid(nblk(a.n)), blk(256);
     if (md == 3) {
         if (a.T) hipLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, a, g);
@@ -600,18 +602,18 @@ hipError_t launch_nn_grid(const NNArgs &a0, const GridView &g, int md, hipStream
         if (a.T) hipLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, a, g);
         else hipLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, a, g);
     }
-    if (a.range) return launch_range_reduce(a.range, grid.x, s);
+    if (a.range && reduce_range) return launch_range_reduce(a.range, grid.x, s);
     return hipGetLastError();
 }
 
 hipError_t launch_nn_brute(const NNArgs &a0, const double *tx, const double *ty,
                            const double *tz, int64_t m, int md, double *part_d2,
-                           int32_t *part_idx, hipStream_t s) {
+                           int32_t *part_idx, hipStream_t s, bool reduce_range) {
     if (a0.n == 0 || m == 0) return hipSuccess;
     NNArgs a = a0;
     if (a.T) {  // apply first: with several target chunks every chunk reads the moved source
         hipLaunchKernelGGL(k_apply_inplace, dim3(nblk(a.n)), dim3(256), 0, s, a.sx, a.sy, a.n,
-                           a.T, a.skip);
+                           a.T, a.skip, a.apply_flag);
         a.T = nullptr;
     }
     constexpr int QPT = 2;
@@ -629,8 +631,16 @@ hipError_t launch_nn_brute(const NNArgs &a0, const double *tx, const double *ty,
     if (nch > 1)
         hipLaunchKernelGGL(k_nn_merge, dim3(nblk(a.n)), dim3(256), 0, s, a, (int)nch, part_d2,
                            part_idx);
-    if (a.range) return launch_range_reduce(a.range, nch > 1 ? (int64_t)nblk(a.n) : qblocks, s);
+    if (a.range && reduce_range)
+        return launch_range_reduce(a.range, nn_range_parts(a.n, m, false), s);
     return hipGetLastError();
+}
+
+// workgroups that store key-range parts in one NN launch (grid: one per 256 queries;
+// brute: one per 512 queries, or the merge kernel's one per 256 with several chunks)
+int64_t nn_range_parts(int64_t n, int64_t m, bool grid) {
+    if (grid || brute_chunk_count(n, m) > 1) return (int64_t)nblk(n);
+    return (n + 511) / 512;
 }
 
 // target chunks for the brute kernel: enough workgroups to fill 256 CUs
@@ -662,7 +672,7 @@ hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, dou
 hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_apply_inplace, dim3(nblk(n)), dim3(256), 0, s, x, y, n, T,
-                       (const int *)nullptr);
+                       (const int *)nullptr, (const int *)nullptr);
     return hipGetLastError();
 }
 

@@ -126,9 +126,11 @@ struct BestRec {
 };
 
 __global__ __launch_bounds__(FB) void k_frac_eval(const double *rs, int64_t n, int64_t N,
-                                                  double lam, const double *tpre,
-                                                  BestRec *tbest, const int *skip) {
+                                                  double lam, const double *lam_dev,
+                                                  const double *tpre, BestRec *tbest,
+                                                  const int *skip) {
     if (skip && *skip) return;
+    if (lam_dev) lam = *lam_dev;
     __shared__ double s[512];
     __shared__ double s_f[256];
     __shared__ long long s_k[256];
@@ -176,8 +178,10 @@ __global__ __launch_bounds__(FB) void k_frac_eval(const double *rs, int64_t n, i
 
 __global__ __launch_bounds__(256) void k_frac_final(const BestRec *tbest, int nb, const double *tpre,
                                                     int64_t n, int64_t N, double lam,
-                                                    IterState *st, const int *skip) {
+                                                    const double *lam_dev, IterState *st,
+                                                    const int *skip) {
     if (skip && *skip) return;
+    if (lam_dev) lam = *lam_dev;
     __shared__ double s_f[256];
     __shared__ long long s_k[256];
     double bf = INFINITY;
@@ -394,8 +398,9 @@ hipError_t launch_residuals(const double *sx, const double *sy, const double *sz
     return hipGetLastError();
 }
 
-hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double lam, void *tmp,
-                           IterState *st, const int *skip, hipStream_t s) {
+hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double lam,
+                           const double *lam_dev, void *tmp, IterState *st, const int *skip,
+                           hipStream_t s) {
     const int nb = (int)((n + FTILE - 1) / FTILE);
     char *p = (char *)tmp;
     double *tsum = (double *)p;
@@ -404,11 +409,11 @@ hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double la
     if (nb > 0) {
         hipLaunchKernelGGL(k_frac_tilesum, dim3(nb), dim3(FB), 0, s, rs, n, tsum, skip);
         hipLaunchKernelGGL(k_frac_tilescan, dim3(1), dim3(256), 0, s, tsum, nb, skip);
-        hipLaunchKernelGGL(k_frac_eval, dim3(nb), dim3(FB), 0, s, rs, n, n_src, lam, tsum, tbest,
-                           skip);
+        hipLaunchKernelGGL(k_frac_eval, dim3(nb), dim3(FB), 0, s, rs, n, n_src, lam, lam_dev, tsum,
+                           tbest, skip);
     }
-    hipLaunchKernelGGL(k_frac_final, dim3(1), dim3(256), 0, s, tbest, nb, tsum, n, n_src, lam, st,
-                       skip);
+    hipLaunchKernelGGL(k_frac_final, dim3(1), dim3(256), 0, s, tbest, nb, tsum, n, n_src, lam,
+                       lam_dev, st, skip);
     return hipGetLastError();
 }
 

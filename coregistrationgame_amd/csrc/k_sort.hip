@@ -40,8 +40,15 @@ constexpr uint32_t C_MASK = F_AGG - 1;
 constexpr int SCAN_I = 16;
 constexpr int SCAN_TILE = 256 * SCAN_I;
 
+// Derived key width and pass count: (key64 - kmin) >> s keeps the top KEY_BITS bits of
+// the key range; runs of equal derived keys (distinct distances closer than 2^s ulps:
+// 27 % of the elements in short runs, longest 7, at C3) are ordered by k_os_fixup.
+constexpr int KEY_BITS = 24;
+constexpr int NPASS = KEY_BITS / 8;
+
 struct SortWS {
-    uint32_t *kA, *kB, *vB;      // key32 ping-pong, val pong (ping = the caller's order)
+    uint32_t *kA, *kB, *vB;      // key ping-pong, val pong (ping = the caller's order)
+    uint2 *pairs;                // (key, position) in orig order from k_os_hist (aliases kB, vB)
     uint32_t *hist;              // [4][256]
     uint32_t *status;            // [4][ntiles][256]
     uint32_t *tickets;           // [4] tile tickets + [1] spin-timeout flag
@@ -60,7 +67,7 @@ __device__ __forceinline__ void load_range(const unsigned long long *range,
 __device__ __forceinline__ int key_shift(unsigned long long kmin, unsigned long long kmax) {
     const unsigned long long span = kmax > kmin ? kmax - kmin : 0ULL;
     const int bits = span ? 64 - __clzll((long long)span) : 0;
-    return bits > 32 ? bits - 32 : 0;
+    return bits > KEY_BITS ? bits - KEY_BITS : 0;
 }
 
 template <typename T>
@@ -137,11 +144,10 @@ __device__ __forceinline__ void wave_hist_add(uint32_t *h, uint32_t d, bool vali
 __global__ __launch_bounds__(256) void k_os_hist(const unsigned long long *key64,
                                                  const uint32_t *orig, int64_t n,
                                                  const unsigned long long *range, SortWS ws,
-                                                 uint32_t *vout, int64_t status_words,
-                                                 const int *skip) {
+                                                 int64_t status_words, const int *skip) {
     if (skip && *skip) return;
-    __shared__ uint32_t s_h[4][256];
-    for (int e = threadIdx.x; e < 4 * 256; e += 256) (&s_h[0][0])[e] = 0;
+    __shared__ uint32_t s_h[NPASS][256];
+    for (int e = threadIdx.x; e < NPASS * 256; e += 256) (&s_h[0][0])[e] = 0;
     // zero the look-back status words and the tickets for the passes that follow; they
     // are only ever touched by device-scope atomics (plain stores to words that other
     // kernels update atomically are not reliably ordered with those atomics)
@@ -165,16 +171,13 @@ __global__ __launch_bounds__(256) void k_os_hist(const unsigned long long *key64
         if (valid) {
             k = (uint32_t)((key64[p] - kmin) >> s);
             const int64_t o = orig ? (int64_t)orig[p] : p;
-            ws.kA[o] = k;
-            vout[o] = (uint32_t)p;
+            ws.pairs[o] = make_uint2(k, (uint32_t)p);  // one 8-B store per element
         }
-        wave_hist_add(s_h[0], k & 255u, valid);
-        wave_hist_add(s_h[1], (k >> 8) & 255u, valid);
-        wave_hist_add(s_h[2], (k >> 16) & 255u, valid);
-        wave_hist_add(s_h[3], k >> 24, valid);
+#pragma unroll
+        for (int d = 0; d < NPASS; ++d) wave_hist_add(s_h[d], (k >> (8 * d)) & 255u, valid);
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 4 * 256; e += 256) {
+    for (int e = threadIdx.x; e < NPASS * 256; e += 256) {
         const uint32_t c = (&s_h[0][0])[e];
         if (c) atomicAdd(&ws.hist[e], c);
     }
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(256) void k_os_hist(const unsigned long long *key64
 // LB = true: onesweep (tile ids from tickets, offsets by decoupled look-back).
 // LB = false: reduce-then-scan (tile = blockIdx.x, offsets from excl_tab[digit][tile]
 // built by k_rs_count + k_rs_rowscan; no communication between workgroups of a launch).
-template <int PASS, bool LB>
+template <int PASS, bool LB, bool PIN = false>
 __global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint32_t *vin,
                                                 uint32_t *kout, uint32_t *vout, int64_t n,
                                                 SortWS ws, const uint32_t *excl_tab,
@@ -222,8 +225,14 @@ __global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint3
     for (int j = 0; j < OIPT; ++j) {
         const int li = wave * (OIPT * 64) + j * 64 + lane;
         const bool valid = li < cnt;
-        k[j] = valid ? kin[t0 + li] : 0u;
-        v[j] = valid ? vin[t0 + li] : 0u;
+        if (PIN) {  // first pass: the (key, position) pairs k_os_hist stored in orig order
+            const uint2 q = valid ? ws.pairs[t0 + li] : make_uint2(0u, 0u);
+            k[j] = q.x;
+            v[j] = q.y;
+        } else {
+            k[j] = valid ? kin[t0 + li] : 0u;
+            v[j] = valid ? vin[t0 + li] : 0u;
+        }
     }
 #pragma unroll
     for (int j = 0; j < OIPT; ++j) {
@@ -318,9 +327,9 @@ __global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint3
 }
 
 // reduce-then-scan: per-tile digit counts of pass PASS -> counts[digit][tile]
-template <int PASS>
-__global__ __launch_bounds__(OB) void k_rs_count(const uint32_t *kin, int64_t n, uint32_t *counts,
-                                                 int ntiles, const int *skip) {
+template <int PASS, bool PIN = false>
+__global__ __launch_bounds__(OB) void k_rs_count(const uint32_t *kin, const uint2 *pin, int64_t n,
+                                                 uint32_t *counts, int ntiles, const int *skip) {
     if (skip && *skip) return;
     constexpr int SH = 8 * PASS;
     __shared__ uint32_t s_h[256];
@@ -333,7 +342,7 @@ __global__ __launch_bounds__(OB) void k_rs_count(const uint32_t *kin, int64_t n,
     for (int j = 0; j < OIPT; ++j) {
         const int li = wave * (OIPT * 64) + j * 64 + lane;
         const bool valid = li < cnt;
-        const uint32_t k = valid ? kin[t0 + li] : 0u;
+        const uint32_t k = valid ? (PIN ? pin[t0 + li].x : kin[t0 + li]) : 0u;
         wave_hist_add(s_h, (k >> SH) & 255u, valid);
     }
     __syncthreads();
@@ -401,7 +410,7 @@ __global__ __launch_bounds__(256) void k_os_fixup(const uint32_t *k32, uint32_t 
     if (j > 0 && k32[j - 1] == kj) return;  // not the head of the run
     int64_t e = j + 1;
     while (e < n && k32[e] == kj) ++e;
-    bool moved = false;
+    bool moved = false;  // stable insertion sort of the run by key64
     for (int64_t a = j + 1; a < e; ++a) {
         const uint32_t v = val[a];
         const unsigned long long kv = key64[v];
@@ -516,6 +525,7 @@ SortWS carve(void *tmp, int64_t n) {
     p += align_up(n * 4, 256);
     w.vB = (uint32_t *)p;
     p += align_up(n * 4, 256);
+    w.pairs = (uint2 *)w.kB;  // 8n bytes over kB and vB (contiguous; both free until pass 1)
     w.hist = (uint32_t *)p;
     p += 4 * 256 * 4;
     w.tickets = (uint32_t *)p;
@@ -595,40 +605,37 @@ hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, in
         if (dbg) (void)hipStreamSynchronize(s);
     };
     SortWS w = carve(tmp, n);
-    hipLaunchKernelGGL(k_atomic_zero32, dim3(4), dim3(256), 0, s, w.hist, (int64_t)(4 * 256));
+    hipLaunchKernelGGL(k_atomic_zero32, dim3(NPASS), dim3(256), 0, s, w.hist,
+                       (int64_t)(NPASS * 256));
     step();
-    const int64_t status_words = onesweep ? 4LL * w.ntiles * 256 : 0;
+    const int64_t status_words = onesweep ? (int64_t)NPASS * w.ntiles * 256 : 0;
     const int hb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 2047) / 2048));
     hipLaunchKernelGGL(k_os_hist, dim3(hb), dim3(256), 0, s, key64, orig, n,
-                       (const unsigned long long *)range, w, order, status_words, skip);
+                       (const unsigned long long *)range, w, status_words, skip);
     step();
-    // ping = (kA, order), pong = (kB, vB): four passes end back in (kA, order)
+    // pairs -> (kA, order) -> (kB, vB) -> (kA, order); the last pass also gathers rs
+    static_assert(NPASS == 3, "pass chain below is written for three 8-bit digits");
     const dim3 g(w.ntiles), b(OB);
-    const uint32_t *kins[4] = {w.kA, w.kB, w.kA, w.kB};
-    const uint32_t *vins[4] = {order, w.vB, order, w.vB};
-    uint32_t *kouts[4] = {w.kB, w.kA, w.kB, w.kA};
-    uint32_t *vouts[4] = {w.vB, order, w.vB, order};
-#define FICP_PASS(P)                                                                          \
+    const uint32_t *nul = nullptr;
+#define FICP_PASS(P, PIN, KIN, VIN, KOUT, VOUT, R, RS)                                          \
     if (onesweep) {                                                                           \
-        hipLaunchKernelGGL((k_os_pass<P, true>), g, b, 0, s, kins[P], vins[P], kouts[P],      \
-                           vouts[P], n, w, (const uint32_t *)nullptr,                         \
-                           P == 3 ? r : (const double *)nullptr,                              \
-                           P == 3 ? rs : (double *)nullptr, skip);                            \
+        hipLaunchKernelGGL((k_os_pass<P, true, PIN>), g, b, 0, s, KIN, VIN, KOUT, VOUT, n, w,   \
+                           nul, R, RS, skip);                                                 \
     } else {                                                                                  \
-        hipLaunchKernelGGL(k_rs_count<P>, g, b, 0, s, kins[P], n, w.counts, w.ntiles, skip);  \
+        hipLaunchKernelGGL((k_rs_count<P, PIN>), g, b, 0, s, KIN, (const uint2 *)w.pairs, n,   \
+                           w.counts, w.ntiles, skip);                                         \
         step();                                                                               \
         hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles, skip); \
         step();                                                                               \
-        hipLaunchKernelGGL((k_os_pass<P, false>), g, b, 0, s, kins[P], vins[P], kouts[P],     \
-                           vouts[P], n, w, (const uint32_t *)w.counts,                        \
-                           P == 3 ? r : (const double *)nullptr,                              \
-                           P == 3 ? rs : (double *)nullptr, skip);                            \
+        hipLaunchKernelGGL((k_os_pass<P, false, PIN>), g, b, 0, s, KIN, VIN, KOUT, VOUT, n, w,  \
+                           (const uint32_t *)w.counts, R, RS, skip);                          \
     }                                                                                         \
     step();
-    FICP_PASS(0)
-    FICP_PASS(1)
-    FICP_PASS(2)
-    FICP_PASS(3)
+    const double *rnul = nullptr;
+    double *rsnul = nullptr;
+    FICP_PASS(0, true, nul, nul, w.kA, order, rnul, rsnul)
+    FICP_PASS(1, false, w.kA, order, w.kB, w.vB, rnul, rsnul)
+    FICP_PASS(2, false, w.kB, w.vB, w.kA, order, r, rs)
 #undef FICP_PASS
     hipLaunchKernelGGL(k_os_fixup, dim3(nblk(n)), dim3(256), 0, s, w.kA, order, key64, r, rs, n,
                        skip);
@@ -663,13 +670,15 @@ hipError_t launch_sort_seg(const unsigned long long *key64, const int32_t *seg, 
     const int hb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 2047) / 2048));
     hipLaunchKernelGGL(k_hist2, dim3(hb), dim3(256), 0, s, w.kA, n, w.hist);
     const dim3 g(w.ntiles), b(OB);
-    hipLaunchKernelGGL(k_rs_count<0>, g, b, 0, s, w.kA, n, w.counts, w.ntiles, (const int *)nullptr);
+    hipLaunchKernelGGL(k_rs_count<0>, g, b, 0, s, w.kA, (const uint2 *)nullptr, n, w.counts,
+                       w.ntiles, (const int *)nullptr);
     hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles,
                        (const int *)nullptr);
     hipLaunchKernelGGL((k_os_pass<0, false>), g, b, 0, s, w.kA, order, w.kB, w.vB, n, w,
                        (const uint32_t *)w.counts, (const double *)nullptr, (double *)nullptr,
                        (const int *)nullptr);
-    hipLaunchKernelGGL(k_rs_count<1>, g, b, 0, s, w.kB, n, w.counts, w.ntiles, (const int *)nullptr);
+    hipLaunchKernelGGL(k_rs_count<1>, g, b, 0, s, w.kB, (const uint2 *)nullptr, n, w.counts,
+                       w.ntiles, (const int *)nullptr);
     hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles,
                        (const int *)nullptr);
     hipLaunchKernelGGL((k_os_pass<1, false>), g, b, 0, s, w.kB, w.vB, w.kA, order, n, w,

@@ -41,6 +41,8 @@ WORKLOADS = {
            "C3: 1M trees vs 1M CHM stems, f=0.6, md=3, run() to convergence (threshold 1e-6)"),
     "c2": (100_000, 100_000, 0.8, 100_000, 3, float("-inf"), 25,
            "C2: 100k trees vs 100k CHM stems, f=0.8, md=3, exactly 2x25 loop bodies"),
+    "c5": (8_000_000, 8_000_000, 0.8, 8_000_000, 3, float("-inf"), 10,
+           "C5: one 8M-tree plot vs an 8M-stem CHM layer partitioned over the GPUs, f=0.8, md=3, 2x10 loop bodies"),
     "batch": (10_000, 10_000, 0.8, 10_000_000, 3, 1e-6, 1000,
               "C4: 1024 plots of 10k trees vs 10k CHM stems, f=0.8, md=3, per-plot run() to convergence"),
 }
@@ -215,6 +217,58 @@ def bench_batch(args, rank, world, local, dist):
     ctx.close()
 
 
+def bench_c5(args, rank, world, local, dist):
+    """C5: the CHM layer is split in contiguous row shards over the ranks (SURVEY.md §8(e));
+    every NN call merges the shards with two all-reduces over RCCL.  One plot for the whole
+    job: value = its loop bodies per second ("scaling": "strong")."""
+    from coregistrationgame_amd.partitioned import PartitionedFICP
+    n, m, f, seed0, md, thr, max_it, desc = WORKLOADS["c5"]
+    if args.c5_size:
+        n = m = args.c5_size
+    plot = synth.make_plot(n, m, f, seed0, md=md)  # same plot on every rank (replicated source)
+    part = PartitionedFICP(plot.source, plot.target, threshold=thr, max_iterations=max_it,
+                           device=local, local_shards=args.local_shards)
+    for _ in range(args.warmup):
+        part.run_resident(lambda0=3.0)
+
+    def barrier():
+        import torch
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    fits = calls = 0
+    for _ in range(args.steps):
+        st = part.run_resident(lambda0=3.0)
+        fits += st["n_fits"]
+        calls += st["n_nn_calls"]
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": fits / dt, "unit": "iterations/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic (SURVEY.md §8(d) generator, seed {seed0}, geo-referenced)",
+            "config": {"workload": desc, "n_trees": n, "n_chm": m, "inlier_fraction": f, "match_dims": md,
+                       "shards": world * args.local_shards,
+                       "parallelism": f"CHM layer in {world * args.local_shards} row shards over {world} GPU(s); "
+                                      "2 all-reduces (d2 MIN, idx MIN) per NN call"},
+            "iterations_per_step": fits / args.steps, "nn_calls_per_step": calls / args.steps,
+            "correspondences_per_s": calls * n / dt, "roofline": None, "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    part.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,6 +279,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nn-mode", default="grid", choices=["auto", "brute", "grid"])
     ap.add_argument("--plots", type=int, default=0, help="batch workload: number of plots (default 1024)")
+    ap.add_argument("--c5-size", type=int, default=0, help="c5 workload: trees = stems (default 8M)")
+    ap.add_argument("--local-shards", type=int, default=1, help="c5 workload: shards per GPU")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -237,8 +293,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    if args.workload == "batch":
-        bench_batch(args, rank, world, local, dist)
+    if args.workload in ("batch", "c5"):
+        (bench_batch if args.workload == "batch" else bench_c5)(args, rank, world, local, dist)
         if dist is not None:
             dist.destroy_process_group()
         return

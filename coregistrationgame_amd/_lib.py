@@ -115,6 +115,10 @@ def lib():
                             _i32, _i32, _vp], C.c_int),
         "ficp_run_batch_device": ([_vp, _i32, _ip64, _vp, _vp, _vp, _ip64, _vp, _vp, _vp, _i32, _i32, _dp,
                                    C.c_double, _i32, _i32, _vp], C.c_int),
+        "ficp_nn_device": ([_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp], C.c_int),
+        "ficp_select_fit_device": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, C.c_double, _i32,
+                                    C.c_double, C.c_double, _ip64, _dp, _dp], C.c_int),
+        "ficp_apply_device": ([_vp, _vp, _vp, _i64, _dp], C.c_int),
         "ficp_dev_alloc": ([_vp, _i64, C.POINTER(_vp)], C.c_int),
         "ficp_dev_free": ([_vp, _vp], C.c_int),
         "ficp_memcpy_h2d": ([_vp, _vp, _vp, _i64], C.c_int),
@@ -309,6 +313,28 @@ class Context:
                                            len(lam), _p(lam), float(threshold), int(max_iterations),
                                            int(bool(allow_reflection)), _vp(out.ctypes.data)))
         return out
+
+    # ---- partitioned CHM layer (include/ficp.h): device pointers in, device results out
+    def nn_device(self, x_ptr: int, y_ptr: int, z_ptr: int, n: int, idx_offset: int, d2_ptr: int,
+                  idx_ptr: int):
+        _check(lib().ficp_nn_device(self.h, _vp(x_ptr), _vp(y_ptr), _vp(z_ptr or 0), int(n), int(idx_offset),
+                                    _vp(d2_ptr), _vp(idx_ptr)))
+
+    def select_fit_device(self, x_ptr: int, y_ptr: int, n: int, d2_ptr: int, idx_ptr: int, tx_ptr: int,
+                          ty_ptr: int, n_source: int, lambda_val: float, allow_reflection: bool,
+                          pivot) -> tuple[int, float, np.ndarray]:
+        k = C.c_int64(0)
+        f = C.c_double(0.0)
+        T = np.zeros(9)
+        _check(lib().ficp_select_fit_device(self.h, _vp(x_ptr), _vp(y_ptr), int(n), _vp(d2_ptr), _vp(idx_ptr),
+                                            _vp(tx_ptr), _vp(ty_ptr), int(n_source), float(lambda_val),
+                                            int(bool(allow_reflection)), float(pivot[0]), float(pivot[1]),
+                                            C.byref(k), C.byref(f), _p(T)))
+        return int(k.value), float(f.value), T.reshape(3, 3)
+
+    def apply_device(self, x_ptr: int, y_ptr: int, n: int, T):
+        T = np.ascontiguousarray(T, dtype=np.float64).reshape(9)
+        _check(lib().ficp_apply_device(self.h, _vp(x_ptr), _vp(y_ptr), int(n), _p(T)))
 
     def synchronize(self):
         _check(lib().ficp_synchronize(self.h))

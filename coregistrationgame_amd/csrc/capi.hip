@@ -754,6 +754,100 @@ int ficp_run_device(ficp_ctx *c, double *x, double *y, const double *z, int64_t 
                     max_iterations, allow_reflection, stats);
 }
 
+// ---- partitioned target: NN against this context's shard, the
+// caller merges the shards (all-reduce of d2, then of the masked idx), then the
+// selection + fit on the merged correspondences.
+int ficp_nn_device(ficp_ctx *c, const double *x, const double *y, const double *z, int64_t n,
+                   int64_t idx_offset, double *d2, int32_t *idx) {
+    CHK(check_ctx(c));
+    if (!c->has_target) return fail(FICP_ESTATE, "no target set");
+    if (n < 0 || (n > 0 && (!x || !y || (c->md == 3 && !z) || !d2 || !idx)))
+        return fail(FICP_EINVAL, "bad arguments");
+    if (n == 0) return FICP_OK;
+    if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large (max 2^30 - 1)");
+    if (idx_offset < 0 || idx_offset + c->m > 0x7fffffff) return fail(FICP_EINVAL, "bad idx_offset");
+    if (c->m == 0) {  // empty shard: never the minimum of the merge
+        HIPCHK(launch_fill_inf(d2, idx, n, c->stream));
+        return sync(c);
+    }
+    CHK(ensure_work(c, n));
+    NNArgs a{};
+    a.sx = const_cast<double *>(x);
+    a.sy = const_cast<double *>(y);
+    a.sz = c->md == 3 ? z : nullptr;
+    a.n = n;
+    a.idx = idx;
+    a.r = d2;
+    a.tx = c->tx.as<double>();
+    a.ty = c->ty.as<double>();
+    if (use_grid(c, n)) {
+        CHK(ensure_grid(c));
+        ProfScope ps(c, P_NN, "nn_grid");
+        HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream, false));
+    } else {
+        const int64_t nch = brute_chunk_count(n, c->m);
+        if (nch > 1) {
+            CHK(c->bd2.ensure(nch * n * 8));
+            CHK(c->bidx.ensure(nch * n * 4));
+        }
+        ProfScope ps(c, P_NN, "nn_brute");
+        HIPCHK(launch_nn_brute(a, c->tx.as<double>(), c->ty.as<double>(),
+                               c->md == 3 ? c->tz.as<double>() : nullptr, c->m, c->md,
+                               c->bd2.as<double>(), c->bidx.as<int32_t>(), c->stream, false));
+    }
+    HIPCHK(launch_add_offset(idx, n, idx_offset, c->stream));
+    return sync(c);
+}
+
+int ficp_select_fit_device(ficp_ctx *c, const double *x, const double *y, int64_t n,
+                           const double *d2, const int32_t *idx, const double *tx,
+                           const double *ty, int64_t n_source, double lambda_val,
+                           int32_t allow_reflection, double pivot_x, double pivot_y, int64_t *k,
+                           double *frmsd, double T[9]) {
+    CHK(check_ctx(c));
+    if (!k || !frmsd || !T) return fail(FICP_EINVAL, "null output");
+    if (n < 0 || (n > 0 && (!x || !y || !d2 || !idx || !tx || !ty)) || n_source < n)
+        return fail(FICP_EINVAL, "bad arguments");
+    for (int e = 0; e < 9; ++e) T[e] = (e % 4 == 0) ? 1.0 : 0.0;
+    *k = 0;
+    *frmsd = INFINITY;
+    if (n == 0) return FICP_OK;
+    if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large (max 2^30 - 1)");
+    CHK(ensure_work(c, n));
+    uint32_t *tflag = sort_timeout_flag(c->sort_tmp.p, n);
+    HIPCHK(launch_atomic_zero32(tflag, 1, c->stream));
+    HIPCHK(launch_corr_from_merge(d2, idx, tx, ty, n, c->key.as<unsigned long long>(),
+                                  c->r.as<double>(), c->ccx.as<double>(), c->ccy.as<double>(),
+                                  range_ptr(c), c->stream));
+    CHK(sort_and_select(c, n, n_source, lambda_val, nullptr));
+    CHK(read_state(c));
+    *k = c->h_state->k;
+    *frmsd = c->h_state->frmsd;
+    if (*k > 0) {
+        IterState *dst = c->state_dev.as<IterState>();
+        FitIn fa{x, y, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
+                 c->order.as<uint32_t>(), nullptr, n, pivot_x, pivot_y, dst};
+        HIPCHK(launch_fit(fa, allow_reflection, c->fit_tmp.p, dst, nullptr, c->stream));
+        CHK(read_state(c));
+        memcpy(T, c->h_state->T, 9 * sizeof(double));
+    }
+    uint32_t tf = 0;
+    HIPCHK(hipMemcpy(&tf, tflag, 4, hipMemcpyDeviceToHost));
+    if (tf) return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", tf);
+    return FICP_OK;
+}
+
+int ficp_apply_device(ficp_ctx *c, double *x, double *y, int64_t n, const double T[9]) {
+    CHK(check_ctx(c));
+    if (n < 0 || (n > 0 && (!x || !y)) || !T) return fail(FICP_EINVAL, "bad arguments");
+    if (n == 0) return FICP_OK;
+    CHK(c->state_dev.ensure(sizeof(IterState)));
+    double *dT = c->state_dev.as<IterState>()->T;
+    HIPCHK(hipMemcpyAsync(dT, T, 9 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_apply_xy(x, y, n, dT, c->stream));
+    return sync(c);
+}
+
 int ficp_dev_alloc(ficp_ctx *c, int64_t bytes, void **ptr) {
     CHK(check_ctx(c));
     if (!ptr || bytes < 0) return fail(FICP_EINVAL, "bad arguments");

@@ -228,6 +228,13 @@ hipError_t launch_residuals(const double *sx, const double *sy, const double *sz
                             const double *cx, const double *cy, const double *cz, int64_t n,
                             int md, double *r, hipStream_t s);
 // argmin_k FRMSD(k) over r in selection order (rs) -> st->k, st->frac, st->frmsd
+// partitioned target (C5): shard idx offset; merged (d2, idx) -> key, r, cx, cy, range
+hipError_t launch_add_offset(int32_t *idx, int64_t n, int64_t off, hipStream_t s);
+hipError_t launch_fill_inf(double *d2, int32_t *idx, int64_t n, hipStream_t s);
+hipError_t launch_corr_from_merge(const double *d2, const int32_t *idx, const double *tx,
+                                  const double *ty, int64_t n, unsigned long long *key, double *r,
+                                  double *cx, double *cy, unsigned long long *range,
+                                  hipStream_t s);
 // device-resident ICP loop (k_loop.hip)
 hipError_t launch_loop_init(IterState *st, const LoopCtl &c, hipStream_t s);
 hipError_t launch_loop_update(IterState *st, const LoopCtl &c, hipStream_t s);

@@ -335,9 +335,10 @@ __global__ __launch_bounds__(256) void k_nn_brute(NNArgs a, const double *__rest
         if (i >= a.n) continue;
         if (gridDim.y == 1) {
             const unsigned long long k = write_out(a, i, best[q], bi[q]);
-            if (a.cx) {
-                a.cx[i] = a.tx[bi[q]];
-                a.cy[i] = a.ty[bi[q]];
+            if (a.cx) {  // no stem matched (NaN query): no gather out of the layer
+                const int bj = bi[q] < (int)m ? bi[q] : 0;
+                a.cx[i] = a.tx[bj];
+                a.cy[i] = a.ty[bj];
             }
             kmin_c = max(kmin_c, ~k);
             kmax = max(kmax, k);
@@ -368,9 +369,10 @@ __global__ __launch_bounds__(256) void k_nn_merge(NNArgs a, int nchunks, const d
             }
         }
         key = write_out(a, i, best, bi);
-        if (a.cx) {
-            a.cx[i] = a.tx[bi];
-            a.cy[i] = a.ty[bi];
+        if (a.cx) {  // bi stays INT32_MAX only for a NaN query: never gather past the layer
+            const int bj = bi != 0x7fffffff ? bi : 0;
+            a.cx[i] = a.tx[bj];
+            a.cy[i] = a.ty[bj];
         }
     }
     if (a.range) block_range_store(a.range, valid, ~key, key);
@@ -554,6 +556,43 @@ __global__ __launch_bounds__(256) void k_interleave_xy(const double *x, const do
     out[2 * i + 1] = y[i];
 }
 
+// empty shard: +inf distance, an index no real stem has (never chosen by the merge)
+__global__ __launch_bounds__(256) void k_fill_inf(double *d2, int32_t *idx, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        d2[i] = INFINITY;
+        idx[i] = 0x7fffffff;
+    }
+}
+
+// partitioned target (C5): shard-local idx -> global idx
+__global__ __launch_bounds__(256) void k_add_offset(int32_t *idx, int64_t n, int64_t off) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) idx[i] = (int32_t)(idx[i] + off);
+}
+
+// merged (d2, global idx) of every query -> the sort/fit inputs of one NN call: key of
+// dist = sqrt(d2) (exactly as write_out), r = d2, the matched stem's XY; key-range parts
+__global__ __launch_bounds__(256) void k_corr_from_merge(const double *d2, const int32_t *idx,
+                                                         const double *tx, const double *ty,
+                                                         int64_t n, unsigned long long *key,
+                                                         double *r, double *cx, double *cy,
+                                                         unsigned long long *range) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long k = 0;
+    const bool valid = i < n;
+    if (valid) {
+        const double v = d2[i];
+        k = ordkey(sqrt(v));
+        key[i] = k;
+        r[i] = v;
+        const int32_t j = idx[i] != 0x7fffffff ? idx[i] : 0;  // unmatched (NaN) query
+        cx[i] = tx[j];
+        cy[i] = ty[j];
+    }
+    block_range_store(range, valid, ~k, k);
+}
+
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
@@ -711,6 +750,28 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
                            pts, m, cell_start, st);
     if (a.range) return launch_range_reduce(a.range, nblk(a.n), s);
     return hipGetLastError();
+}
+
+hipError_t launch_fill_inf(double *d2, int32_t *idx, int64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_inf, dim3(nblk(n)), dim3(256), 0, s, d2, idx, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_offset(int32_t *idx, int64_t n, int64_t off, hipStream_t s) {
+    if (n == 0 || off == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_add_offset, dim3(nblk(n)), dim3(256), 0, s, idx, n, off);
+    return hipGetLastError();
+}
+
+hipError_t launch_corr_from_merge(const double *d2, const int32_t *idx, const double *tx,
+                                  const double *ty, int64_t n, unsigned long long *key, double *r,
+                                  double *cx, double *cy, unsigned long long *range,
+                                  hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_corr_from_merge, dim3(nblk(n)), dim3(256), 0, s, d2, idx, tx, ty, n, key,
+                       r, cx, cy, range);
+    return launch_range_reduce(range, nblk(n), s);
 }
 
 hipError_t launch_scatter_i32(const uint32_t *worig, const int32_t *w, int64_t n, int32_t *out,

@@ -142,6 +142,30 @@ int ficp_run_batch_device(ficp_ctx *ctx, int32_t nplots, const int64_t *src_off,
                           const double *lambdas, double threshold, int32_t max_iterations,
                           int32_t allow_reflection, ficp_plot_stats *per_plot);
 
+/* --- partitioned CHM layer (one large plot over several GPUs) ------------ */
+/* The target is split into contiguous row ranges (shards), one per rank; the source is
+   replicated.  Per NN call each rank runs ficp_nn_device against its shard, the caller
+   merges the shards (all-reduce MIN of d2, then all-reduce MIN of idx where the rank's
+   d2 equals the merged d2: the lowest global index wins a tie, as in ficp_nn), and every
+   rank runs ficp_select_fit_device on the merged result (deterministic: identical T on
+   every rank), then ficp_apply_device.  All pointers are device pointers. */
+/* find_correspondences (ficp.py:65-71) against the shard set with ficp_set_target*:
+   d2[i] = squared distance, idx[i] = idx_offset + shard index of the nearest stem.
+   An empty shard yields d2 = +inf, idx = INT32_MAX. */
+int ficp_nn_device(ficp_ctx *ctx, const double *x, const double *y, const double *z, int64_t n,
+                   int64_t idx_offset, double *d2, int32_t *idx);
+/* find_optimal_fraction + compute_optimal_transform_2d (ficp.py:73-110) on merged
+   correspondences: tx, ty = the whole CHM layer (rows addressed by idx).  Returns k and
+   its FRMSD; T = the fit on the first k pairs (identity when k == 0).  The fit's sums are
+   taken relative to (pivot_x, pivot_y): pass the same pivot on every rank. */
+int ficp_select_fit_device(ficp_ctx *ctx, const double *x, const double *y, int64_t n,
+                           const double *d2, const int32_t *idx, const double *tx,
+                           const double *ty, int64_t n_source, double lambda_val,
+                           int32_t allow_reflection, double pivot_x, double pivot_y, int64_t *k,
+                           double *frmsd, double T[9]);
+/* apply_transform_2d_xy_only (ficp.py:112-119) in place on device-resident XY. */
+int ficp_apply_device(ficp_ctx *ctx, double *x, double *y, int64_t n, const double T[9]);
+
 /* --- device memory helpers (for callers without their own allocator) ---- */
 int ficp_dev_alloc(ficp_ctx *ctx, int64_t bytes, void **ptr);
 int ficp_dev_free(ficp_ctx *ctx, void *ptr);

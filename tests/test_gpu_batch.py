@@ -122,3 +122,35 @@ def test_batch_c4_properties():
         T = st["T_total"][j].reshape(3, 3)
         xy = p.source[:, :2] @ T[:2, :2].T + T[:2, 2]
         np.testing.assert_allclose(xy, finals[j][:, :2], atol=1e-6, rtol=0)
+
+
+# ------------------------------------------------------------ partitioned CHM layer (C5)
+@pytest.mark.parametrize("shards", [1, 3, 8])
+def test_partitioned_matches_single(shards, oracle):
+    """A CHM layer split into shards (merged by the min / lowest-index rule) gives the run
+    of the unsplit layer: same NN calls and k per call, XY within 1e-6, vs the oracle."""
+    from coregistrationgame_amd import FractionalICP, synth
+    from coregistrationgame_amd.partitioned import PartitionedFICP
+    p = synth.make_plot(20_000, 20_000, 0.8, seed=77, md=3)
+    part = PartitionedFICP(p.source, p.target, local_shards=shards)
+    out = part.run()
+    icp = FractionalICP(p.source, p.target)
+    single = icp.run(trace=True)
+    ofinal, otr = oracle.run(p.source, p.target, nthreads=8)
+    np.testing.assert_allclose(out[:, :2], single[:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(out[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(bits(out[:, 2]), bits(p.source[:, 2]))
+    np.testing.assert_array_equal(np.array(part.last_stats["k"]), otr["k"])
+    assert part.lambda_val == 0.95
+
+
+def test_partitioned_2d_and_tiny_shards():
+    """2-D layers and more shards than stems (empty shards) still give the single run."""
+    from coregistrationgame_amd import FractionalICP
+    from coregistrationgame_amd.partitioned import PartitionedFICP
+    rng = np.random.default_rng(3)
+    tgt = rng.uniform(0, 30, (6, 2))
+    src = tgt[rng.integers(0, 6, 40)] + rng.normal(0, 0.2, (40, 2))
+    out = PartitionedFICP(src, tgt, local_shards=9).run()
+    single = FractionalICP(src, tgt).run()
+    np.testing.assert_allclose(out, single, atol=1e-6, rtol=0)

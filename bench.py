@@ -83,6 +83,20 @@ def nn_bytes_per_launch(n, m, md):
     return n * (8 * md + 16 + 12) + m * 8 * md
 
 
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC profile
+    (profiles/*_pmc_*_nn.json, written from tools/pmc.sh output), or None."""
+    best = None
+    for f in sorted((REPO / "profiles").glob("*_pmc_*_nn.json")):
+        try:
+            d = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        if str(d.get("kernel", "")).startswith(kernel_prefix):
+            best = (d["hbm_bytes_per_launch"], f.name)
+    return best
+
+
 def cpu_baseline(plot, threads):
     """The pinned C oracle (oracle/ficp_oracle.c, kind "port") on the same C3 plot: static
     kd-tree + O(N) fraction scan, 2 stages x 2 loop bodies (threshold -inf), timed on
@@ -356,6 +370,7 @@ def main():
         avg_ms = nn["ms"] / max(launches, 1)
         bytes_launch = nn_bytes_per_launch(n, m, md)
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic = pmc_traffic("k_nn_grid<3" if md == 3 else "k_nn_grid<2") if args.workload == "c3" else None
         out = {
             "metric": METRIC,
             "value": fits_all / dt_max,
@@ -377,7 +392,9 @@ def main():
             "correspondences_per_s": calls_all * n / dt_max,
             "roofline": {"bound": "hbm", "kernel": "nn_grid (fused apply + exact 1-NN)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic[0] if traffic else None,
+                         "traffic_source": traffic[1] if traffic else None,
                          "avg_launch_us": avg_ms * 1e3, "launches": launches,
                          "timed_launches_incl_noop": nn["count"],
                          "algorithmic_bytes_per_launch": bytes_launch},

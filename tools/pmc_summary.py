@@ -1,4 +1,4 @@
-"""Per-kernel averages of the PMC passes written by tools/pmc.sh (counter_collection.csv).
+"""Per-kernel medians of the PMC passes written by tools/pmc.sh (counter_collection.csv).
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KB per dispatch.  On gfx950
 FETCH_SIZE reports half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md,
@@ -26,7 +26,9 @@ def main(root):
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for k, ctrs in acc.items():
-        d = {c: sum(v) / len(v) for c, v in ctrs.items()}
+        # median over dispatches: the device loop's few no-op launches past the end of a
+        # run (early exit, ~0 bytes) would pull a mean down
+        d = {c: float(sorted(v)[len(v) // 2]) for c, v in ctrs.items()}
         d["dispatches"] = max(len(v) for v in ctrs.values())
         if "FETCH_SIZE" in d:
             d["fetch_bytes_raw"] = d["FETCH_SIZE"] * 1024.0

@@ -115,6 +115,7 @@ def lib():
                             _i32, _i32, _vp], C.c_int),
         "ficp_run_batch_device": ([_vp, _i32, _ip64, _vp, _vp, _vp, _ip64, _vp, _vp, _vp, _i32, _i32, _dp,
                                    C.c_double, _i32, _i32, _vp], C.c_int),
+        "ficp_remove_matches": ([_vp, _dp, _i64, _i64, _dp, _ip32, _ip64], C.c_int),
         "ficp_nn_device": ([_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp], C.c_int),
         "ficp_select_fit_device": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, C.c_double, _i32,
                                     C.c_double, C.c_double, _ip64, _dp, _dp], C.c_int),
@@ -313,6 +314,18 @@ class Context:
                                            len(lam), _p(lam), float(threshold), int(max_iterations),
                                            int(bool(allow_reflection)), _vp(out.ctypes.data)))
         return out
+
+    def remove_matches(self, plot, thresh) -> np.ndarray:
+        """ficp_remove_matches against this context's target: removal order (stem rows)."""
+        p = _rows(plot)
+        t = np.ascontiguousarray(thresh, dtype=np.float64)
+        if t.shape != (len(p),):
+            raise ValueError("one threshold per plot tree")
+        out = np.zeros(max(1, min(len(p), self.m)), np.int32)
+        cnt = C.c_int64(0)
+        _check(lib().ficp_remove_matches(self.h, _p(p), len(p), p.shape[1] if len(p) else self.md, _p(t),
+                                         _p(out, _ip32), C.byref(cnt)))
+        return out[:cnt.value].astype(np.int64)
 
     # ---- partitioned CHM layer (include/ficp.h): device pointers in, device results out
     def nn_device(self, x_ptr: int, y_ptr: int, z_ptr: int, n: int, idx_offset: int, d2_ptr: int,

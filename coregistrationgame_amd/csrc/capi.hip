@@ -754,6 +754,72 @@ int ficp_run_device(ficp_ctx *c, double *x, double *y, const double *z, int64_t 
                     max_iterations, allow_reflection, stats);
 }
 
+// ---- CHMPlot.remove_matches (chm_plot.py:223-285), SURVEY.md §8(f1)
+int ficp_remove_matches(ficp_ctx *c, const double *plot, int64_t n, int64_t ld,
+                        const double *thresh, int32_t *removed, int64_t *n_removed) {
+    CHK(check_ctx(c));
+    if (!c->has_target) return fail(FICP_ESTATE, "no target set");
+    if (!n_removed || n < 0 || (n > 0 && (!plot || !thresh || !removed || ld < c->md)))
+        return fail(FICP_EINVAL, "bad arguments");
+    *n_removed = 0;
+    const int64_t m = c->m;
+    if (n == 0 || m == 0) return FICP_OK;
+    if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large (max 2^30 - 1)");
+    if (m > kMaxGridStems) return fail(FICP_EINVAL, "CHM layer too large for the grid");
+    CHK(ensure_grid(c));
+    CHK(upload_rows(c, plot, n, ld, c->md, c->sx, c->sy, &c->sz));
+    CHK(c->bidx.ensure((size_t)n * KNN_K * 4));  // the K candidates of every plot tree
+    CHK(c->bd2.ensure((size_t)n * KNN_K * 8));
+    CHK(c->tidx.ensure((size_t)m));  // the removed-stem mask (one byte per stem)
+    std::vector<int32_t> kid((size_t)n * KNN_K);
+    std::vector<double> kd((size_t)n * KNN_K);
+    std::vector<uint8_t> rem((size_t)m, 0);
+    auto query = [&](int64_t q0, bool masked) -> int {
+        if (masked)
+            HIPCHK(hipMemcpyAsync(c->tidx.p, rem.data(), (size_t)m, hipMemcpyHostToDevice,
+                                  c->stream));
+        HIPCHK(launch_knn_grid(c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(), q0, n,
+                               c->gv, c->md, masked ? (const uint8_t *)c->tidx.p : nullptr,
+                               c->bidx.as<int32_t>(), c->bd2.as<double>(), c->stream));
+        const size_t off = (size_t)q0 * KNN_K, cnt = (size_t)(n - q0) * KNN_K;
+        HIPCHK(hipMemcpyAsync(kid.data() + off, c->bidx.as<int32_t>() + off, cnt * 4,
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(kd.data() + off, c->bd2.as<double>() + off, cnt * 8,
+                              hipMemcpyDeviceToHost, c->stream));
+        return sync(c);
+    };
+    CHK(query(0, false));
+    // The greedy walk of the reference, in plot-tree order: each tree takes its nearest
+    // remaining stem (first of its K candidates not yet removed).  When all K of a tree
+    // are gone, the trees from it on are queried again with the removed stems masked.
+    int64_t remaining = m, cnt = 0;
+    for (int64_t i = 0; i < n && remaining > 0;) {
+        int j = -1;
+        for (int u = 0; u < KNN_K; ++u) {
+            const int32_t id = kid[(size_t)i * KNN_K + u];
+            if (id == 0x7fffffff) break;  // fewer than K stems left for this tree
+            if (!rem[(size_t)id]) {
+                j = u;
+                break;
+            }
+        }
+        if (j < 0) {
+            CHK(query(i, true));
+            if (kid[(size_t)i * KNN_K] == 0x7fffffff) break;  // nothing left at all
+            continue;
+        }
+        const int32_t id = kid[(size_t)i * KNN_K + j];
+        if (kd[(size_t)i * KNN_K + j] < thresh[i]) {  // chm_plot.py:249, 282
+            rem[(size_t)id] = 1;
+            removed[cnt++] = id;
+            --remaining;
+        }
+        ++i;
+    }
+    *n_removed = cnt;
+    return FICP_OK;
+}
+
 // ---- partitioned target: NN against this context's shard, the
 // caller merges the shards (all-reduce of d2, then of the masked idx), then the
 // selection + fit on the merged correspondences.

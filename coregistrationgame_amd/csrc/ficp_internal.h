@@ -231,6 +231,12 @@ hipError_t launch_residuals(const double *sx, const double *sy, const double *sz
 // partitioned target (C5): shard idx offset; merged (d2, idx) -> key, r, cx, cy, range
 hipError_t launch_add_offset(int32_t *idx, int64_t n, int64_t off, hipStream_t s);
 hipError_t launch_fill_inf(double *d2, int32_t *idx, int64_t n, hipStream_t s);
+// remove_matches: the KNN_K best (distance, stem index) of queries [q0, n) in cdist order
+// (d = sqrt(d2), then index), skipping stems with removed[idx] != 0 (nullable)
+constexpr int KNN_K = 8;
+hipError_t launch_knn_grid(const double *sx, const double *sy, const double *sz, int64_t q0,
+                           int64_t n, const GridView &g, int md, const uint8_t *removed,
+                           int32_t *out_id, double *out_d, hipStream_t s);
 hipError_t launch_corr_from_merge(const double *d2, const int32_t *idx, const double *tx,
                                   const double *ty, int64_t n, unsigned long long *key, double *r,
                                   double *cx, double *cy, unsigned long long *range,

@@ -175,6 +175,109 @@ __device__ __forceinline__ void grid_nn(const GridView &g, const Stems &S, doubl
     disk_scan<MD>(g, S, qx, qy, qz, cy, mq, b);
 }
 
+// ---------------------------------------------------------------- k nearest (remove_matches)
+// CHMPlot.remove_matches (chm_plot.py:223-285) matches with scipy's cdist + argmin: the
+// ORDER is by the rounded distance d = sqrt(d2) and then by stem index (np.argmin keeps
+// the first of equal distances).  The K best (d, index) of a query, skipping stems
+// flagged in `removed` (indexed by stem index; nullable).
+constexpr int KNN = KNN_K;
+
+template <int MD>
+__device__ __forceinline__ void knn_eval(const Stems &S, int p, double qx, double qy, double qz,
+                                         const uint8_t *removed, double (&kd)[KNN],
+                                         int (&kid)[KNN]) {
+    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32, 0, 0);
+    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32 + 16, 0, 0);
+    const int id = (int)hi.z;
+    if (removed && removed[id]) return;
+    const double2 xy = __builtin_bit_cast(double2, lo);
+    const double dd = sqrt(sq_dist<MD>(qx, qy, qz, xy.x, xy.y, __builtin_bit_cast(double2, hi).x));
+    if (!(dd < kd[KNN - 1] || (dd == kd[KNN - 1] && id < kid[KNN - 1]))) return;
+    kd[KNN - 1] = dd;
+    kid[KNN - 1] = id;
+#pragma unroll
+    for (int u = KNN - 1; u > 0; --u) {  // bubble the new entry to its place (stable)
+        const bool sw = kd[u] < kd[u - 1] || (kd[u] == kd[u - 1] && kid[u] < kid[u - 1]);
+        const double td = sw ? kd[u - 1] : kd[u];
+        const int ti = sw ? kid[u - 1] : kid[u];
+        kd[u - 1] = sw ? kd[u] : kd[u - 1];
+        kid[u - 1] = sw ? kid[u] : kid[u - 1];
+        kd[u] = td;
+        kid[u] = ti;
+    }
+}
+
+template <int MD>
+__device__ __forceinline__ void knn_range(const Stems &S, int p0, int p1, double qx, double qy,
+                                          double qz, const uint8_t *removed, double (&kd)[KNN],
+                                          int (&kid)[KNN]) {
+    for (int p = p0; p < p1; ++p) knn_eval<MD>(S, p, qx, qy, qz, removed, kd, kid);
+}
+
+template <int MD>
+__global__ __launch_bounds__(256) void k_knn_grid(const double *sx, const double *sy,
+                                                  const double *sz, int64_t q0, int64_t n,
+                                                  GridView g, const uint8_t *removed,
+                                                  int32_t *out_id, double *out_d) {
+    const int64_t i = q0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Stems S = stems_of(g.pts, g.m);
+    const double qx = sx[i], qy = sy[i], qz = (MD == 3) ? sz[i] : 0.0;
+    double kd[KNN];
+    int kid[KNN];
+#pragma unroll
+    for (int u = 0; u < KNN; ++u) {
+        kd[u] = INFINITY;
+        kid[u] = 0x7fffffff;
+    }
+    const int cx = cell_coord(qx, g.x0, g.inv_h, g.gx);
+    const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
+    const double mq = query_margin(g, qx, qy);
+    // square rings until K stems are held (or the grid is exhausted): a finite radius
+    for (int r = 0; kid[KNN - 1] == 0x7fffffff; ++r) {
+        const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
+        if (r > 0 && xa < 0 && ya < 0 && xb >= g.gx && yb >= g.gy) break;
+        const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);
+        for (int yy = max(ya, 0); yy <= min(yb, g.gy - 1); ++yy) {
+            const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
+            if (yy == ya || yy == yb) {
+                knn_range<MD>(S, rw[xlo], rw[xhi + 1], qx, qy, qz, removed, kd, kid);
+            } else {
+                if (xa >= 0) knn_range<MD>(S, rw[xa], rw[xa + 1], qx, qy, qz, removed, kd, kid);
+                if (xb < g.gx) knn_range<MD>(S, rw[xb], rw[xb + 1], qx, qy, qz, removed, kd, kid);
+            }
+        }
+    }
+    if (kid[KNN - 1] != 0x7fffffff) {
+        // disk-clipped rows within the K-th distance (inflated: a d2 a few ulps below
+        // kd^2 can still round to the same d and win on its index)
+        for (int k = 0;; ++k) {
+            bool any = false;
+            for (int side = 0; side < 2; ++side) {
+                if (k == 0 && side == 1) continue;
+                const int yy = side ? cy + k : cy - k;
+                if (yy < 0 || yy >= g.gy) continue;
+                const double b2 = kd[KNN - 1] * kd[KNN - 1] * (1.0 + 1e-12);
+                const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
+                if (beyond(gy, b2)) continue;
+                any = true;
+                const double gy0 = fmax(gy, 0.0);
+                const double w = sqrt(fmax(b2 - gy0 * gy0, 0.0)) + mq;
+                const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
+                const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
+                const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+                knn_range<MD>(S, row[xl], row[xh + 1], qx, qy, qz, removed, kd, kid);
+            }
+            if (!any) break;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < KNN; ++u) {
+        out_id[i * KNN + u] = kid[u];
+        out_d[i * KNN + u] = kd[u];
+    }
+}
+
 __device__ __forceinline__ void apply_T(const double *__restrict__ T, double &x, double &y) {
     // numpy's ([x, y, 1] @ T.T)[:, :2] through OpenBLAS dgemm (ficp.py:117):
     // fma(y, T01, x*T00) + T02 -- pinned bit-exactly by tests/golden/apply.npz
@@ -749,6 +852,20 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
         hipLaunchKernelGGL(k_nn_grid_batch<2>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
                            pts, m, cell_start, st);
     if (a.range) return launch_range_reduce(a.range, nblk(a.n), s);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_grid(const double *sx, const double *sy, const double *sz, int64_t q0,
+                           int64_t n, const GridView &g, int md, const uint8_t *removed,
+                           int32_t *out_id, double *out_d, hipStream_t s) {
+    if (n <= q0) return hipSuccess;
+    const unsigned nb = nblk(n - q0);
+    if (md == 3)
+        hipLaunchKernelGGL(k_knn_grid<3>, dim3(nb), dim3(256), 0, s, sx, sy, sz, q0, n, g, removed,
+                           out_id, out_d);
+    else
+        hipLaunchKernelGGL(k_knn_grid<2>, dim3(nb), dim3(256), 0, s, sx, sy, sz, q0, n, g, removed,
+                           out_id, out_d);
     return hipGetLastError();
 }
 

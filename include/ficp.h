@@ -142,6 +142,17 @@ int ficp_run_batch_device(ficp_ctx *ctx, int32_t nplots, const int64_t *src_off,
                           const double *lambdas, double threshold, int32_t max_iterations,
                           int32_t allow_reflection, ficp_plot_stats *per_plot);
 
+/* --- CHM stems matched by a joined plot --------------------------------- */
+/* CHMPlot.remove_matches (chm_plot.py:223-285) against the CHM layer set with
+   ficp_set_target (md 3: x, y, height; md 2: x, y).  For each plot tree in order, its
+   nearest REMAINING stem (scipy cdist distance, first index on equal distances) is
+   removed iff that distance < thresh[i] (the caller passes min_dist_percent/100 * the
+   tree's height, with the reference's 10 m rule in 2-D).  Stops when no stem remains.
+   removed[0 .. *n_removed) = the removed stems' row indices in removal order (capacity
+   >= min(n, m)).  GPU k-nearest candidates + the reference's greedy walk on the host. */
+int ficp_remove_matches(ficp_ctx *ctx, const double *plot, int64_t n, int64_t ld,
+                        const double *thresh, int32_t *removed, int64_t *n_removed);
+
 /* --- partitioned CHM layer (one large plot over several GPUs) ------------ */
 /* The target is split into contiguous row ranges (shards), one per rank; the source is
    replicated.  Per NN call each rank runs ficp_nn_device against its shard, the caller

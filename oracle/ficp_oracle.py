@@ -239,3 +239,41 @@ class OracleFICP:
                                       self.max_iterations, self.allow_reflection)
         self.lambda_val = lam1
         return self.source
+
+
+# ----------------------------------------------------------------- remove_matches
+def remove_matches(plot, chm, min_dist_percent=15.0):
+    """CHMPlot.remove_matches (chm_plot.py:223-285) restated on arrays: plot and chm are
+    (n, 3) / (m, 3) [x, y, height] (height NaN = missing).  Returns the removal order as
+    indices into chm.  Pure-Python sequential loop: test infrastructure for small cases.
+
+    * 3-D when every height of both layers is present (chm_plot.py:238-250), else 2-D
+      (chm_plot.py:263-283) with the plot tree's height or 10 m as the threshold base;
+    * distance as scipy's cdist: sqrt(((dx*dx) + dy*dy) + dz*dz);
+    * argmin over the remaining stems in their original order (first index on ties);
+    * removal iff distance < min_dist_percent / 100 * height; stop when none remain.
+    """
+    plot = np.asarray(plot, dtype=np.float64)
+    chm = np.asarray(chm, dtype=np.float64)
+    use3d = bool(np.isfinite(plot[:, 2]).all() and np.isfinite(chm[:, 2]).all())
+    remaining = list(range(len(chm)))
+    removed = []
+    for i in range(len(plot)):
+        if not remaining:
+            break
+        t = chm[remaining]
+        dx = t[:, 0] - plot[i, 0]
+        dy = t[:, 1] - plot[i, 1]
+        d2 = dx * dx
+        d2 = d2 + dy * dy
+        if use3d:
+            dz = t[:, 2] - plot[i, 2]
+            d2 = d2 + dz * dz
+        d = np.sqrt(d2)
+        j = int(np.argmin(d))
+        h = plot[i, 2]
+        if not use3d and not np.isfinite(h):
+            h = 10.0
+        if d[j] < (min_dist_percent / 100.0) * h:
+            removed.append(remaining.pop(j))
+    return np.array(removed, dtype=np.int64)

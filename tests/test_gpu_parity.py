@@ -329,3 +329,47 @@ def test_drop_in_module_import():
     import ficp
     from coregistrationgame_amd.ficp import FractionalICP
     assert ficp.FractionalICP is FractionalICP
+
+
+# ------------------------------------------------------------ remove_matches (§8 f1)
+def test_remove_matches_golden():
+    """CHMPlot.remove_matches on the GPU: the reference's removal sequence, every case
+    (3-D, 2-D by missing heights, conflicts, exhaustion, geo coordinates, exact ties, a
+    sequence of plots on one shrinking layer)."""
+    import conftest
+    from coregistrationgame_amd.matches import remove_matches_arrays
+    from test_oracle_golden import _matches_sequence
+    z = np.load(conftest.GOLDEN / "matches.npz")
+    for name in sorted({k.split("/")[0] for k in z.files}):
+        got = _matches_sequence(remove_matches_arrays, z, name)
+        for k, g in enumerate(got):
+            np.testing.assert_array_equal(g, z[f"{name}/removed{k}"], err_msg=f"{name} call {k}")
+
+
+def test_remove_matches_crowded_vs_oracle(oracle):
+    """Many plot trees fighting over few stems: most trees lose all 8 GPU candidates and
+    the walk re-queries with the removed stems masked."""
+    from coregistrationgame_amd.matches import remove_matches_arrays
+    rng = np.random.default_rng(11)
+    chm = np.column_stack([rng.uniform(0, 60, 400), rng.uniform(0, 60, 400), rng.uniform(5, 30, 400)])
+    centre = chm[rng.integers(0, 400, 30)]
+    plot = centre[rng.integers(0, 30, 600)] + np.column_stack(
+        [rng.normal(0, 1.5, 600), rng.normal(0, 1.5, 600), rng.normal(0, 2, 600)])
+    np.testing.assert_array_equal(remove_matches_arrays(plot, chm), oracle.remove_matches(plot, chm))
+    plot[::3, 2] = np.nan  # 2-D with the 10 m rule
+    np.testing.assert_array_equal(remove_matches_arrays(plot, chm), oracle.remove_matches(plot, chm))
+
+
+def test_remove_matches_objects():
+    """The object-level drop-in edits chm.trees / chm.removed_stems like the reference."""
+    from types import SimpleNamespace as NS
+    from coregistrationgame_amd.matches import remove_matches
+    rng = np.random.default_rng(2)
+    stems = [NS(currentx=float(x), currenty=float(y), height=float(h))
+             for x, y, h in zip(rng.uniform(0, 30, 50), rng.uniform(0, 30, 50), rng.uniform(5, 30, 50))]
+    trees = [NS(currentx=s.currentx + 0.1, currenty=s.currenty, height=s.height) for s in stems[:10]]
+    trees.append(NS(currentx=100.0, currenty=100.0, height=None))  # far, no height -> 2-D
+    chm = NS(trees=list(stems), removed_stems=[])
+    removed = remove_matches(chm, NS(trees=trees))
+    assert [id(t) for t in removed] == [id(s) for s in stems[:10]]
+    assert len(chm.trees) == 40 and chm.removed_stems == [removed]

@@ -6,6 +6,7 @@ the oracle is trusted as the HIP path's checker only because these pass.
 import numpy as np
 import pytest
 
+import conftest
 from conftest import K_GAP_PIN, RUN_FIXTURES, load_cases, load_run, pinned_prefix, assert_T_close
 
 
@@ -116,3 +117,27 @@ def test_oracle_kdtree_equals_brute_large(oracle):
     b = oracle.nn(p.source, p.target, 3, "brute", nthreads=8)
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
+
+
+def _matches_sequence(fn, z, name):
+    """Run a fixture's calls on one shrinking CHM layer; removal rows of the original layer."""
+    chm = z[f"{name}/chm"]
+    alive = list(range(len(chm)))
+    out = []
+    for k in range(int(z[f"{name}/calls"])):
+        got = [alive[g] for g in fn(z[f"{name}/plot{k}"], chm[alive])]
+        for g in got:
+            alive.remove(g)
+        out.append(np.array(got, dtype=np.int64))
+    return out
+
+
+def test_remove_matches_oracle_golden(oracle):
+    """chm_plot.py:223-285 restated (oracle.remove_matches) == the reference's removals."""
+    z = np.load(conftest.GOLDEN / "matches.npz")
+    names = sorted({k.split("/")[0] for k in z.files})
+    assert len(names) >= 8
+    for name in names:
+        got = _matches_sequence(oracle.remove_matches, z, name)
+        for k, g in enumerate(got):
+            np.testing.assert_array_equal(g, z[f"{name}/removed{k}"], err_msg=f"{name} call {k}")

@@ -373,3 +373,63 @@ def test_remove_matches_objects():
     removed = remove_matches(chm, NS(trees=trees))
     assert [id(t) for t in removed] == [id(s) for s in stems[:10]]
     assert len(chm.trees) == 40 and chm.removed_stems == [removed]
+
+
+# ------------------------------------------------------------ callers (§8 f2, f3)
+def _ns_plot(xy, cur, flipped=False, heights=None):
+    from types import SimpleNamespace as NS
+    trees = [NS(tree_id=f"t{i}", x=float(a), y=float(b), currentx=float(c), currenty=float(d),
+                height=None if heights is None else float(heights[i]))
+             for i, ((a, b), (c, d)) in enumerate(zip(xy, cur))]
+    return NS(trees=trees, flipped=flipped, center=tuple(np.mean(xy, axis=0)),
+              current_center=tuple(np.mean(cur, axis=0)), plotid=0)
+
+
+def test_get_transform_golden():
+    """Plot.get_transform (trees.py:248-280) on the GPU vs the reference's SVD result:
+    1..120 trees, flipped or not, unit and geo-referenced coordinates."""
+    import conftest
+    from coregistrationgame_amd.stand import get_transform
+    z = np.load(conftest.GOLDEN / "transforms.npz")
+    for case in sorted({k.split("/")[0] for k in z.files}):
+        xy, cur = z[f"{case}/xy"], z[f"{case}/cur"]
+        R, t, fl = get_transform(_ns_plot(xy, cur, bool(z[f"{case}/flipped"])))
+        assert fl == bool(z[f"{case}/flipped"])
+        # With collinear trees (n <= 2) H has rank 1: a rotation and a reflection fit the
+        # trees equally well, and a flipped plot keeps whichever LAPACK's singular vectors
+        # give -- parity unpinned for R there, pinned for its action on the trees.
+        if len(xy) > 2 or not fl:
+            np.testing.assert_allclose(R, z[f"{case}/R"], atol=1e-9, rtol=0, err_msg=case)
+        np.testing.assert_allclose(xy @ R.T + t, xy @ z[f"{case}/R"].T + z[f"{case}/t"], atol=1e-6,
+                                   rtol=0, err_msg=case)
+
+
+def test_join_stand_real_vs_oracle(oracle):
+    """The app's Join loop over stand 10 (16 real plots, one shrinking 259-stem CHM layer):
+    join (2-D: no plot heights), transformation record, remove_matches -- vs the oracle's
+    run + remove_matches composed the same way."""
+    import conftest
+    from types import SimpleNamespace as NS
+    from coregistrationgame_amd.stand import join_stand
+    z = np.load(conftest.GOLDEN / "run_real_stand10.npz")
+    tgt = z["tgt"]
+    stems = [NS(tree_id=i, x=float(a), y=float(b), currentx=float(a), currenty=float(b), height=None)
+             for i, (a, b) in enumerate(tgt)]
+    chm = NS(trees=list(stems), removed_stems=[])
+    plots = [_ns_plot(z[f"{pid}/src"], z[f"{pid}/src"]) for pid in z["plot_ids"]]
+    for pid, p in zip(z["plot_ids"], plots):
+        p.plotid = int(pid)
+    records = join_stand(NS(plots=plots), chm)
+    alive = list(range(len(tgt)))
+    for pid, p in zip(z["plot_ids"], plots):
+        src = z[f"{pid}/src"]
+        final, _ = oracle.run(src, tgt[alive], nthreads=4)
+        got = np.array([[t.currentx, t.currenty] for t in p.trees])
+        np.testing.assert_allclose(got, final[:, :2], atol=1e-6, rtol=0, err_msg=str(pid))
+        plot_xyh = np.column_stack([final[:, :2], np.full(len(final), np.nan)])
+        chm_xyh = np.column_stack([tgt[alive], np.full(len(alive), np.nan)])
+        rem = [alive[i] for i in oracle.remove_matches(plot_xyh, chm_xyh)]
+        for r in rem:
+            alive.remove(r)
+        assert records[int(pid)]["flip"] is False
+    assert sorted(t.tree_id for t in chm.trees) == alive

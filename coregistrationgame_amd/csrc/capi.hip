@@ -98,6 +98,16 @@ bool use_grid(ficp_ctx *c, int64_t n) {
     return (double)n * (double)c->m > 4.0e6;
 }
 
+// fit scratch of n rows; a fresh allocation gets its arrival counter zeroed
+int ensure_fit(ficp_ctx *c, int64_t n) {
+    CHK(c->fit_tmp.ensure(fit_tmp_bytes(n)));
+    if (c->fit_tmp.gen != c->fit_init_gen) {
+        HIPCHK(launch_fit_init(c->fit_tmp.p, c->stream));
+        c->fit_init_gen = c->fit_tmp.gen;
+    }
+    return FICP_OK;
+}
+
 int ensure_work(ficp_ctx *c, int64_t n) {
     CHK(c->idx.ensure(n * 4));
     CHK(c->dist.ensure(n * 8));
@@ -107,13 +117,26 @@ int ensure_work(ficp_ctx *c, int64_t n) {
     CHK(c->order.ensure(n * 4));
     CHK(c->sort_tmp.ensure(sort_tmp_bytes(n)));
     CHK(c->frac_tmp.ensure(frac_tmp_bytes(n)));
-    CHK(c->fit_tmp.ensure(fit_tmp_bytes(n)));
+    CHK(ensure_fit(c, n));
     CHK(c->state_dev.ensure(sizeof(IterState)));
     CHK(c->ccx.ensure(n * 8));
     CHK(c->ccy.ensure(n * 8));
     CHK(c->rs.ensure(n * 8));
     CHK(c->range.ensure(range_words(n) * 8));
+    CHK(c->sel_tmp.ensure(sel_tmp_bytes(n)));
+    CHK(c->sel_stats.ensure(16));
+    if (c->sel_tmp.gen != c->sel_init_gen) {  // fresh allocation: zero its atomic words
+        HIPCHK(launch_select_init(c->sel_tmp.p, n, c->stream));
+        c->sel_init_gen = c->sel_tmp.gen;
+    }
     return FICP_OK;
+}
+
+// FICP_SELECT=0: the run loop uses the full residual sort + prefix scan instead of the
+// bucketed selection (A/B checks; both give the same k and threshold)
+bool use_select() {
+    static const bool on = !getenv("FICP_SELECT") || atoi(getenv("FICP_SELECT")) != 0;
+    return on;
 }
 
 unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long long>(); }
@@ -124,7 +147,7 @@ unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long lo
 // every query from its previous match (grid mode, same work order within one run).
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
             bool want_keys, int warm = 0, const int *skip = nullptr,
-            const int *apply_flag = nullptr) {
+            const int *apply_flag = nullptr, bool reduce_range = true) {
     NNArgs a{};
     a.sx = sx;
     a.sy = sy;
@@ -154,7 +177,8 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             ProfScope ps(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
             HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream, false));
         }
-        if (a.range) HIPCHK(launch_range_reduce(a.range, nn_range_parts(n, c->m, true), c->stream));
+        if (a.range && reduce_range)
+            HIPCHK(launch_range_reduce(a.range, nn_range_parts(n, c->m, true), c->stream));
     } else {
         const int64_t nch = brute_chunk_count(n, c->m);
         if (nch > 1) {
@@ -167,7 +191,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
                                    c->md == 3 ? c->tz.as<double>() : nullptr, c->m, c->md,
                                    c->bd2.as<double>(), c->bidx.as<int32_t>(), c->stream, false));
         }
-        if (a.range)
+        if (a.range && reduce_range)
             HIPCHK(launch_range_reduce(a.range, nn_range_parts(n, c->m, false), c->stream));
     }
     return FICP_OK;
@@ -301,8 +325,9 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         worig = c->worig.as<uint32_t>();
     }
     IterState *dst = c->state_dev.as<IterState>();
+    const bool sel = use_select();
     FitIn fa{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
-             c->order.as<uint32_t>(), worig, n, c->pivot_x, c->pivot_y, dst};
+             sel ? nullptr : c->order.as<uint32_t>(), worig, n, c->pivot_x, c->pivot_y, dst};
     // loop parameters and traces live on the device (k_loop.hip)
     LoopCtl lc{};
     lc.nstages = nstages;
@@ -347,12 +372,28 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             ProfScope ps(c, P_FIT, "fit");
             HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, &dst->no_fit, c->stream));
         }
-        CHK(nn_call(c, wx, wy, wz, n, dst->T, true, j == 0 ? 1 : 2, &dst->done, &dst->apply));
-        CHK(sort_and_select(c, n, n, 0.0, worig, &dst->done, &dst->lam_cur));
-        if (tidx) HIPCHK(launch_trace_idx(dst, c->idx.as<int32_t>(), worig, n, tidx, mt, c->stream));
-        HIPCHK(launch_loop_update(dst, lc, c->stream));
         const int slot = (int)(j % kLoopRing);
-        HIPCHK(hipMemcpyAsync(&c->h_flags[slot], &dst->done, 4, hipMemcpyDeviceToHost, c->stream));
+        // selection path without traces: the selection's last kernel also runs the loop
+        // step and stores the done flag straight into the pinned ring
+        const bool fused = sel && !tidx;
+        CHK(nn_call(c, wx, wy, wz, n, dst->T, true, j == 0 ? 1 : 2, &dst->done, &dst->apply,
+                    !sel));
+        if (sel) {
+            ProfScope ps(c, P_SORT, "select");
+            HIPCHK(launch_select(c->key.as<unsigned long long>(), worig, c->r.as<double>(), n, 0.0,
+                                 &dst->lam_cur, range_ptr(c), nn_range_parts(n, c->m, use_grid(c, n)),
+                                 c->sel_tmp.p, dst, &dst->done, fused ? &lc : nullptr,
+                                 fused ? &c->h_flags[slot] : nullptr, c->stream));
+        } else {
+            CHK(sort_and_select(c, n, n, 0.0, worig, &dst->done, &dst->lam_cur));
+        }
+        if (!fused) {
+            if (tidx)
+                HIPCHK(launch_trace_idx(dst, c->idx.as<int32_t>(), worig, n, tidx, mt, c->stream));
+            HIPCHK(launch_loop_update(dst, lc, c->stream));
+            HIPCHK(hipMemcpyAsync(&c->h_flags[slot], &dst->done, 4, hipMemcpyDeviceToHost,
+                                  c->stream));
+        }
         HIPCHK(hipEventRecord(c->loop_ev[slot], c->stream));
         if (j >= la) {
             const int old = (int)((j - la) % kLoopRing);
@@ -401,6 +442,15 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     uint32_t tf = 0;
     HIPCHK(hipMemcpy(&tf, tflag, 4, hipMemcpyDeviceToHost));
     if (tf) return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", tf);
+    if (sel) {
+        unsigned ss[3] = {0, 0, 0};
+        HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
+        HIPCHK(hipMemcpyAsync(ss, c->sel_stats.p, 12, hipMemcpyDeviceToHost, c->stream));
+        CHK(sync(c));
+        c->sel_levels = ss[1];
+        c->sel_radix = ss[2];
+        if (ss[0]) return fail(FICP_EHIP, "fraction selection raised error flag %u", ss[0]);
+    }
     return FICP_OK;
 }
 
@@ -459,7 +509,7 @@ int ficp_create(int device, ficp_ctx **out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e == hipSuccess)
-        e = hipHostMalloc((void **)&c->h_flags, kLoopRing * sizeof(int), hipHostMallocDefault);
+        e = hipHostMalloc((void **)&c->h_flags, kLoopRing * sizeof(int), hipHostMallocCoherent);
     for (int k = 0; k < kLoopRing && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&c->loop_ev[k], hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -483,7 +533,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
                       &c->bp,     &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
-                      &c->tr_T,   &c->tr_idx};
+                      &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats};
     for (DevBuf *b : bufs) b->release();
     batch_release(c->batch);
     c->batch = nullptr;
@@ -636,11 +686,11 @@ int ficp_frmsd(ficp_ctx *c, const double *src, int64_t lds, const double *corr, 
         return fail(FICP_EINVAL, "bad arguments");
     CHK(upload_rows(c, src, k, lds, md, c->sx, c->sy, &c->sz));
     CHK(upload_rows(c, corr, k, ldc, md, c->cx, c->cy, &c->cz));
-    CHK(c->fit_tmp.ensure(std::max<int64_t>(fit_tmp_bytes(k), 4096)));
+    CHK(ensure_fit(c, std::max<int64_t>(k, 4096)));
     CHK(c->stage2.ensure(64));
     HIPCHK(launch_sum_sq_diff(c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(),
                               c->cx.as<double>(), c->cy.as<double>(), c->cz.as<double>(), k, md,
-                              c->fit_tmp.p, c->stage2.as<double>(), c->stream));
+                              (char *)c->fit_tmp.p + 256, c->stage2.as<double>(), c->stream));
     double S = 0.0;
     HIPCHK(hipMemcpyAsync(&S, c->stage2.p, 8, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));
@@ -681,7 +731,7 @@ int ficp_fit_rigid2d(ficp_ctx *c, const double *src, int64_t lds, const double *
         return fail(FICP_EINVAL, "bad arguments (k must be >= 1)");
     CHK(upload_rows(c, src, k, lds, 2, c->sx, c->sy, nullptr));
     CHK(upload_rows(c, tgt, k, ldt, 2, c->cx, c->cy, nullptr));
-    CHK(c->fit_tmp.ensure(fit_tmp_bytes(k)));
+    CHK(ensure_fit(c, k));
     CHK(c->state_dev.ensure(sizeof(IterState)));
     // pivot: the first source point keeps the sums well conditioned for any offset
     double p[2] = {0.0, 0.0};
@@ -885,14 +935,21 @@ int ficp_select_fit_device(ficp_ctx *c, const double *x, const double *y, int64_
     HIPCHK(launch_corr_from_merge(d2, idx, tx, ty, n, c->key.as<unsigned long long>(),
                                   c->r.as<double>(), c->ccx.as<double>(), c->ccy.as<double>(),
                                   range_ptr(c), c->stream));
-    CHK(sort_and_select(c, n, n_source, lambda_val, nullptr));
+    const bool sel = use_select() && n == n_source;
+    if (sel) {
+        HIPCHK(launch_select(c->key.as<unsigned long long>(), nullptr, c->r.as<double>(), n,
+                             lambda_val, nullptr, range_ptr(c), 0, c->sel_tmp.p,
+                             c->state_dev.as<IterState>(), nullptr, nullptr, nullptr, c->stream));
+    } else {
+        CHK(sort_and_select(c, n, n_source, lambda_val, nullptr));
+    }
     CHK(read_state(c));
     *k = c->h_state->k;
     *frmsd = c->h_state->frmsd;
     if (*k > 0) {
         IterState *dst = c->state_dev.as<IterState>();
         FitIn fa{x, y, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
-                 c->order.as<uint32_t>(), nullptr, n, pivot_x, pivot_y, dst};
+                 sel ? nullptr : c->order.as<uint32_t>(), nullptr, n, pivot_x, pivot_y, dst};
         HIPCHK(launch_fit(fa, allow_reflection, c->fit_tmp.p, dst, nullptr, c->stream));
         CHK(read_state(c));
         memcpy(T, c->h_state->T, 9 * sizeof(double));
@@ -900,6 +957,15 @@ int ficp_select_fit_device(ficp_ctx *c, const double *x, const double *y, int64_
     uint32_t tf = 0;
     HIPCHK(hipMemcpy(&tf, tflag, 4, hipMemcpyDeviceToHost));
     if (tf) return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", tf);
+    if (sel) {
+        unsigned ss[3] = {0, 0, 0};
+        HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
+        HIPCHK(hipMemcpyAsync(ss, c->sel_stats.p, 12, hipMemcpyDeviceToHost, c->stream));
+        CHK(sync(c));
+        c->sel_levels = ss[1];
+        c->sel_radix = ss[2];
+        if (ss[0]) return fail(FICP_EHIP, "fraction selection raised error flag %u", ss[0]);
+    }
     return FICP_OK;
 }
 

@@ -49,6 +49,7 @@ inline int fail(int code, const char *fmt, ...) {
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    unsigned gen = 0;  // bumped on every (re)allocation
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return FICP_OK;
         if (p) (void)hipFree(p);
@@ -61,6 +62,7 @@ struct DevBuf {
             return fail(FICP_ENOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
         }
         cap = want;
+        ++gen;
         return FICP_OK;
     }
     void release() {
@@ -113,6 +115,10 @@ struct ficp_ctx {
     DevBuf stage, stage2, cx, cy, cz, state_dev;
     DevBuf bp;  // grid slot of each query's last match (warm start of the next NN call)
     DevBuf lams, tr_k, tr_f, tr_l, tr_T, tr_idx;  // device loop: lambdas and traces
+    DevBuf sel_tmp, sel_stats;  // bucketed fraction selection (k_select.hip)
+    unsigned sel_init_gen = 0;  // sel_tmp allocation whose atomic words are initialised
+    unsigned fit_init_gen = 0;  // fit_tmp allocation whose arrival counter is zeroed
+    unsigned sel_levels = 0, sel_radix = 0;  // selection statistics (cumulative)
     int *h_flags = nullptr;                        // pinned ring of per-iteration done flags
     hipEvent_t loop_ev[kLoopRing] = {};
     IterState *h_state = nullptr;  // pinned

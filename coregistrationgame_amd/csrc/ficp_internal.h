@@ -139,7 +139,18 @@ struct alignas(16) IterState {
     int no_fit;            // 1 unless a loop body is due: the fit is a no-op
     int apply;             // the NN call applies T (a fit ran in this iteration)
     int pad1;
+    // selection threshold of the last fraction call (k_select.hip): the k-th pair of the
+    // stable (key, orig) order; the fit selects {i : (key_i, orig_i) <= (tkey, torig)}
+    unsigned long long tkey;
+    long long torig;
 };
+
+// FRMSD(k) = (1 / (k/N)**lambda) * sqrt(S_k / k), in the reference's operation order
+// (ficp.py:59-60, 81)
+__device__ __forceinline__ double frmsd_of(long long k, long long N, double S, double lam) {
+    const double frac = (double)k / (double)N;
+    return (1.0 / pow(frac, lam)) * sqrt(S / (double)k);
+}
 
 // Loop parameters and optional trace buffers of the device-resident loop.
 struct LoopCtl {
@@ -154,6 +165,70 @@ struct LoopCtl {
     double *tl;            // [max_trace] lambda per call
     double *tT;            // [max_trace * 9] fits in order
 };
+
+// ---------------------------------------------- device-resident loop (k_loop.hip)
+__device__ __forceinline__ void loop_set_flags(IterState &s) {
+    s.done = s.phase == PH_DONE;
+    s.no_fit = s.phase != PH_LOOP;
+    s.apply = s.phase == PH_LOOP;
+}
+
+__device__ __forceinline__ void loop_end_stage(IterState &s, const LoopCtl &c) {
+    if (s.stage < 2) s.iters[s.stage] = s.it;
+    s.stage += 1;
+    s.it = 0;
+    if (s.stage < c.nstages) {  // ficp.py:152-153: next lambda, next _iterate
+        s.phase = PH_HEAD;
+        s.lam_cur = c.lams[s.stage];
+    } else {
+        s.phase = PH_DONE;
+    }
+}
+
+// one k_loop_update step on the state (thread 0 of one workgroup): the decisions of
+// _iterate/run after an NN call + fraction (ficp.py:122-154)
+__device__ __forceinline__ void loop_step(IterState *st, const LoopCtl &c) {
+    IterState &s = *st;
+    if (s.done) return;
+    const int call = s.n_nn++;
+    s.k_last = s.k;
+    if (call < c.max_trace) {
+        if (c.tk) c.tk[call] = s.k;
+        if (c.tf) c.tf[call] = s.frmsd;
+        if (c.tl) c.tl[call] = s.lam_cur;
+    }
+    if (s.phase == PH_HEAD) {  // ficp.py:123-129
+        if (s.k == 0) {
+            loop_end_stage(s, c);  // ficp.py:125-126: nothing selected, the stage returns
+        } else {
+            s.cur = s.frmsd;
+            if (s.stage < 2) s.frmsd_last[s.stage] = s.cur;
+            s.phase = PH_LOOP;
+            s.it = 0;
+            if (c.max_iter <= 0) loop_end_stage(s, c);
+        }
+    } else {  // a loop body ran: fit -> apply -> NN -> fraction (ficp.py:132-140)
+        if (s.n_fit < c.max_trace && c.tT)
+            for (int e = 0; e < 9; ++e) c.tT[9 * s.n_fit + e] = s.T[e];
+        s.n_fit += 1;
+        double R[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                R[3 * i + j] = s.T[3 * i] * s.Ttot[j] + s.T[3 * i + 1] * s.Ttot[3 + j] +
+                               s.T[3 * i + 2] * s.Ttot[6 + j];
+        for (int e = 0; e < 9; ++e) s.Ttot[e] = R[e];
+        const double nw = s.frmsd;
+        if (s.stage < 2) s.frmsd_last[s.stage] = nw;
+        if (s.cur - nw <= c.threshold) {  // ficp.py:142 (the transform is already applied)
+            loop_end_stage(s, c);
+        } else {
+            s.cur = nw;
+            s.it += 1;
+            if (s.it >= c.max_iter) loop_end_stage(s, c);
+        }
+    }
+    loop_set_flags(s);
+}
 
 // ----------------------------------------------------------------- launchers
 // grid build (k_grid_nn.hip)
@@ -221,6 +296,22 @@ hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, in
 hipError_t launch_keys_from_doubles(const double *d, int64_t n, unsigned long long *key,
                                     uint32_t *val, hipStream_t s);
 
+// FRMSD-optimal fraction by bucketed selection (k_select.hip): st->k, frac, frmsd and the
+// threshold pair (tkey, torig) of the k-th (key, orig) entry, without sorting every row.
+// Requires n == N (the run loop).  range = the NN call's key range.  orig nullable.
+int64_t sel_tmp_bytes(int64_t n);
+hipError_t launch_select_init(void *tmp, int64_t n, hipStream_t s);
+// out3 (device): {sticky error bits, refinement levels run, radix fallbacks}
+hipError_t launch_select_stats(void *tmp, int64_t n, unsigned *out3, hipStream_t s);
+// range_parts > 0: range holds the producer's unreduced parts (block_range_store); the
+// histogram kernel reduces them (no launch_range_reduce needed) and stores range[0..1].
+// loop (nullable): the last kernel also runs the k_loop_update step; host_flag (nullable,
+// coherent pinned host memory): receives st->done after that step.
+hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, const double *r,
+                         int64_t n, double lam, const double *lam_dev, unsigned long long *range,
+                         int64_t range_parts, void *tmp, IterState *st, const int *skip,
+                         const LoopCtl *loop, int *host_flag, hipStream_t s);
+
 // selection + fit + apply (k_select_fit.hip)
 int64_t frac_tmp_bytes(int64_t n);
 // r_i = sum_md (src_i - corr_i)^2 on SoA inputs
@@ -250,7 +341,8 @@ hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double la
                            const double *lam_dev,
                            void *tmp, IterState *st, const int *skip, hipStream_t s);
 // Rigid fit of source (sx, sy) onto its correspondences (cx, cy).  With key != null the
-// selected rows are the first st->k entries of the stable order (order, key); with
+// selected rows are the first st->k entries of the stable order (order, key) -- with
+// order == null the threshold pair is st->(tkey, torig) from launch_select; with
 // key == null every one of the n rows is used.
 struct FitIn {
     const double *sx, *sy, *cx, *cy;
@@ -262,6 +354,8 @@ struct FitIn {
     const IterState *st;
 };
 int64_t fit_tmp_bytes(int64_t n);
+// zero the scratch's arrival counter: once per (re)allocation of the scratch
+hipError_t launch_fit_init(void *tmp, hipStream_t s);
 hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,
                       const int *skip, hipStream_t s);
 hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hipStream_t s);

@@ -15,12 +15,6 @@ namespace ficp {
 
 namespace {
 
-__device__ __forceinline__ void set_flags(IterState &s) {
-    s.done = s.phase == PH_DONE;
-    s.no_fit = s.phase != PH_LOOP;
-    s.apply = s.phase == PH_LOOP;
-}
-
 __global__ void k_loop_init(IterState *st, LoopCtl c) {
     if (threadIdx.x != 0) return;
     IterState &s = *st;
@@ -34,63 +28,14 @@ __global__ void k_loop_init(IterState *st, LoopCtl c) {
     s.iters[0] = s.iters[1] = 0;
     s.phase = c.nstages > 0 ? PH_HEAD : PH_DONE;
     s.lam_cur = c.nstages > 0 ? c.lams[0] : 0.0;
-    set_flags(s);
-}
-
-__device__ __forceinline__ void end_stage(IterState &s, const LoopCtl &c) {
-    if (s.stage < 2) s.iters[s.stage] = s.it;
-    s.stage += 1;
-    s.it = 0;
-    if (s.stage < c.nstages) {  // ficp.py:152-153: next lambda, next _iterate
-        s.phase = PH_HEAD;
-        s.lam_cur = c.lams[s.stage];
-    } else {
-        s.phase = PH_DONE;
-    }
+    loop_set_flags(s);
 }
 
 __global__ void k_loop_update(IterState *st, LoopCtl c) {
     if (threadIdx.x != 0) return;
-    IterState &s = *st;
-    if (s.done) return;
-    const int call = s.n_nn++;
-    s.k_last = s.k;
-    if (call < c.max_trace) {
-        if (c.tk) c.tk[call] = s.k;
-        if (c.tf) c.tf[call] = s.frmsd;
-        if (c.tl) c.tl[call] = s.lam_cur;
-    }
-    if (s.phase == PH_HEAD) {  // ficp.py:123-129
-        if (s.k == 0) {
-            end_stage(s, c);  // ficp.py:125-126: nothing selected, the stage returns
-        } else {
-            s.cur = s.frmsd;
-            if (s.stage < 2) s.frmsd_last[s.stage] = s.cur;
-            s.phase = PH_LOOP;
-            s.it = 0;
-            if (c.max_iter <= 0) end_stage(s, c);
-        }
-    } else {  // a loop body ran: fit -> apply -> NN -> fraction (ficp.py:132-140)
-        if (s.n_fit < c.max_trace && c.tT)
-            for (int e = 0; e < 9; ++e) c.tT[9 * s.n_fit + e] = s.T[e];
-        s.n_fit += 1;
-        double R[9];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j)
-                R[3 * i + j] = s.T[3 * i] * s.Ttot[j] + s.T[3 * i + 1] * s.Ttot[3 + j] +
-                               s.T[3 * i + 2] * s.Ttot[6 + j];
-        for (int e = 0; e < 9; ++e) s.Ttot[e] = R[e];
-        const double nw = s.frmsd;
-        if (s.stage < 2) s.frmsd_last[s.stage] = nw;
-        if (s.cur - nw <= c.threshold) {  // ficp.py:142 (the transform is already applied)
-            end_stage(s, c);
-        } else {
-            s.cur = nw;
-            s.it += 1;
-            if (s.it >= c.max_iter) end_stage(s, c);
-        }
-    }
-    set_flags(s);
+    IterState s = *st;  // one batch of loads instead of a chain of dependent round trips
+    loop_step(&s, c);
+    *st = s;
 }
 
 // idx of this call, in the caller's row order, into the trace (before k_loop_update)

@@ -63,11 +63,6 @@ __device__ __forceinline__ double block_excl_scan_d(double v, double *s /*[2][25
     return ex;
 }
 
-__device__ __forceinline__ double frmsd_of(long long k, long long N, double S, double lam) {
-    const double frac = (double)k / (double)N;  // k / N (ficp.py:81)
-    return (1.0 / pow(frac, lam)) * sqrt(S / (double)k);  // ficp.py:59-60
-}
-
 __device__ __forceinline__ bool better(double f, long long k, double bf, long long bk) {
     return f < bf || (f == bf && k < bk);
 }
@@ -239,15 +234,30 @@ __device__ __forceinline__ bool fit_threshold(const FitIn &a, unsigned long long
         to = -1;
         return false;
     }
+    if (!a.order) {  // threshold pair from the bucketed selection
+        tk = a.st->tkey;
+        to = a.st->torig;
+        return false;
+    }
     const int64_t tp = (int64_t)a.order[k - 1];
     tk = a.key[tp];
     to = a.orig ? (int64_t)a.orig[tp] : tp;
     return false;
 }
 
-__global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, const int *skip) {
+// The finishing step (k_fit_final's work) runs in the block that arrives last at the
+// counter: partials are handed off with sc1 stores/loads and one agent-scope atomic add
+// per block (MI355X_MICROARCH.md hand-off table, first row); the last block resets the
+// counter (atomic exchange) for the next launch.
+__device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow_refl,
+                           IterState *st, double *s);
+
+__global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, unsigned *ctr,
+                                                 int allow_refl, IterState *st,
+                                                 const int *skip) {
     if (skip && *skip) return;
     __shared__ double s[256];
+    __shared__ int s_last;
     unsigned long long tk = 0;
     int64_t ti = 0;
     const bool all = fit_threshold(a, tk, ti);
@@ -276,25 +286,57 @@ __global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, const in
             }
         }
     }
+    // fixed-order reduction: wave butterfly (every lane ends with the same bits), then the
+    // four waves in order
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const double t = block_sum_d(c[e], s);
-        if (threadIdx.x == 0) part[8 * blockIdx.x + e] = t;
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c[e] = c[e] + __shfl_xor(c[e], o, 64);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[8 * (threadIdx.x >> 6) + e] = c[e];
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        const int e = threadIdx.x;
+        const double t = ((s[e] + s[8 + e]) + s[16 + e]) + s[24 + e];
+        __hip_atomic_store(&part[8 * blockIdx.x + e], t, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev =
+            __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == gridDim.x - 1;
+        if (s_last) __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    fit_finish(a, part, (int)gridDim.x, allow_refl, st, s);
 }
 
-__global__ __launch_bounds__(256) void k_fit_final(FitIn a, const double *part, int nb,
-                                                   int allow_refl, IterState *st,
-                                                   const int *skip) {
-    if (skip && *skip) return;
-    __shared__ double s[256];
-    double c[8];
-    for (int e = 0; e < 8; ++e) {
-        double acc = 0.0;
-        for (int b = threadIdx.x; b < nb; b += 256) acc = acc + part[8 * b + e];
-        c[e] = block_sum_d(acc, s);
+__device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow_refl,
+                           IterState *st, double *s) {
+    double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int b = threadIdx.x; b < nb; b += 256) {  // fixed order per thread
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            v[e] = __hip_atomic_load(&part[8 * b + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c[e] = c[e] + v[e];
     }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c[e] = c[e] + __shfl_xor(c[e], o, 64);
+    __syncthreads();  // s[] was used by the caller
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[8 * (threadIdx.x >> 6) + e] = c[e];
+    __syncthreads();
     if (threadIdx.x != 0) return;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) c[e] = ((s[e] + s[8 + e]) + s[16 + e]) + s[24 + e];
     const double k = a.key ? (double)a.st->k : (double)a.n;
     // centroids of the pivot-shifted pairs, then H = sum s't'^T - k cs' ct'^T
     const double csx = c[0] / k, csy = c[1] / k, ctx = c[2] / k, cty = c[3] / k;
@@ -417,17 +459,23 @@ hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double la
     return hipGetLastError();
 }
 
+// fit scratch: [0, 256) the arrival counter (atomics only; zeroed once per allocation by
+// launch_fit_init), then 8 partial sums per block
 int64_t fit_tmp_bytes(int64_t n) {
     const int64_t nb = (n + FTILE - 1) / FTILE + 1;
-    return align_up(nb * 8 * 8, 256);
+    return 256 + align_up(nb * 8 * 8, 256);
+}
+
+hipError_t launch_fit_init(void *tmp, hipStream_t s) {
+    return launch_atomic_zero32((uint32_t *)tmp, 1, s);
 }
 
 hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,
                       const int *skip, hipStream_t s) {
     const int nb = (int)std::max<int64_t>(1, (a.n + FTILE - 1) / FTILE);
-    double *part = (double *)tmp;
-    hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FB), 0, s, a, part, skip);
-    hipLaunchKernelGGL(k_fit_final, dim3(1), dim3(256), 0, s, a, part, nb, allow_reflection, st,
+    unsigned *ctr = (unsigned *)tmp;
+    double *part = (double *)((char *)tmp + 256);
+    hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FB), 0, s, a, part, ctr, allow_reflection, st,
                        skip);
     return hipGetLastError();
 }

@@ -1,0 +1,189 @@
+// selcheck.hip -- GPU self-check and per-kernel timing of the bucketed FRMSD selection
+// (coregistrationgame_amd/csrc/k_select.hip; tools only, not shipped).
+// Build: make -C coregistrationgame_amd/csrc selcheck
+// Run:   ./tools/selcheck [n] [reps] [mode] [lambda]
+//   mode 0: C3-like residuals (60 % inliers: 0.09 (x1^2 + x2^2) + x3^2, 40 % outliers:
+//           Rayleigh(2 m) distances); 1: 30 % exact zeros + exponential; 2: all rows
+//           equal; 3: 5 distinct distances; 4: exponential; 5: geometric (huge range)
+// Checks k, FRMSD and the threshold pair against a CPU sort by (key, orig); prints the
+// time of each of the four kernels (events around each, median over reps).
+#include "../coregistrationgame_amd/csrc/k_select.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <vector>
+
+using namespace ficp;
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e = (x);                                                                \
+        if (e != hipSuccess) {                                                             \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(2);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+static unsigned long long hkey(double v) {
+    unsigned long long u;
+    memcpy(&u, &v, 8);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+
+static double hfrmsd(long long k, long long N, double S, double lam) {
+    const double frac = (double)k / (double)N;
+    return (1.0 / pow(frac, lam)) * sqrt(S / (double)k);
+}
+
+int main(int argc, char **argv) {
+    const int64_t n = argc > 1 ? atoll(argv[1]) : 1000000;
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    const int mode = argc > 3 ? atoi(argv[3]) : 0;
+    const double lam = argc > 4 ? atof(argv[4]) : 3.0;
+    std::mt19937_64 rng(7 + mode);
+    std::normal_distribution<double> nd(0.0, 1.0);
+    std::uniform_real_distribution<double> ud(0.0, 1.0);
+    std::exponential_distribution<double> ex(1.0);
+    std::vector<unsigned long long> key(n);
+    std::vector<uint32_t> orig(n);
+    std::vector<double> r(n);
+    for (int64_t i = 0; i < n; ++i) {
+        double d2 = 0.0;
+        if (mode == 0) {
+            if (ud(rng) < 0.6) {
+                const double a = nd(rng), b = nd(rng), c = nd(rng);
+                d2 = 0.09 * (a * a + b * b) + c * c;
+            } else {
+                const double d = 2.0 * sqrt(-2.0 * log(1.0 - ud(rng)));
+                d2 = d * d;
+            }
+        } else if (mode == 1) {
+            d2 = ud(rng) < 0.3 ? 0.0 : ex(rng);
+        } else if (mode == 2) {
+            d2 = 2.25;
+        } else if (mode == 3) {
+            d2 = floor(ex(rng) * 1.25);
+        } else if (mode == 4) {
+            d2 = ex(rng);
+        } else {
+            d2 = pow(10.0, -8.0 + 12.0 * ud(rng));
+        }
+        const double d = sqrt(d2);
+        key[i] = hkey(d);
+        r[i] = d2;
+        orig[i] = (uint32_t)i;
+    }
+    std::shuffle(orig.begin(), orig.end(), rng);
+    // CPU reference: stable order by (key, orig), prefix sums, first minimum
+    std::vector<uint32_t> ord(n);
+    for (int64_t i = 0; i < n; ++i) ord[i] = (uint32_t)i;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+        return key[a] < key[b] || (key[a] == key[b] && orig[a] < orig[b]);
+    });
+    std::vector<double> S(n + 1, 0.0);
+    for (int64_t j = 0; j < n; ++j) S[j + 1] = S[j] + r[ord[j]];
+    long long bk = 0;
+    double bf = INFINITY;
+    for (int64_t k = 1; k <= n; ++k) {
+        const double f = hfrmsd(k, n, S[k], lam);
+        if (f < bf) {
+            bf = f;
+            bk = k;
+        }
+    }
+    // device
+    unsigned long long *dkey, *drange;
+    uint32_t *dorig;
+    double *dr;
+    void *tmp;
+    IterState *st;
+    CK(hipMalloc(&dkey, n * 8));
+    CK(hipMalloc(&dorig, n * 4));
+    CK(hipMalloc(&dr, n * 8));
+    CK(hipMalloc(&drange, 64));
+    CK(hipMalloc(&tmp, sel_tmp_bytes(n)));
+    CK(hipMalloc(&st, sizeof(IterState)));
+    CK(hipMemset(st, 0, sizeof(IterState)));
+    CK(hipMemcpy(dkey, key.data(), n * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dorig, orig.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dr, r.data(), n * 8, hipMemcpyHostToDevice));
+    unsigned long long kmn = ~0ULL, kmx = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        kmn = std::min(kmn, key[i]);
+        kmx = std::max(kmx, key[i]);
+    }
+    unsigned long long hr[2] = {~kmn, kmx};
+    CK(hipMemcpy(drange, hr, 16, hipMemcpyHostToDevice));
+    CK(launch_select_init(tmp, n, 0));
+    const SelWS w = carve(tmp, n);
+    const int gb = gather_blocks(n);
+    hipEvent_t ev[5];
+    for (auto &evx : ev) CK(hipEventCreate(&evx));
+    std::vector<std::vector<float>> tk(4);
+    int bad = 0;
+    for (int it = 0; it < reps; ++it) {
+        CK(hipEventRecord(ev[0], 0));
+        hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HT), 0, 0, dkey, dr, n, drange,
+                           (int64_t)0, w, (const int *)nullptr);
+        CK(hipEventRecord(ev[1], 0));
+        hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam, (const double *)nullptr,
+                           (const unsigned long long *)drange, (const int *)nullptr);
+        CK(hipEventRecord(ev[2], 0));
+        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
+                           (const int *)nullptr);
+        CK(hipEventRecord(ev[3], 0));
+        LoopCtl lc{};
+        hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, 0, w, gb, n, lam,
+                           (const double *)nullptr, st, (const int *)nullptr, lc, 0, (int *)nullptr);
+        CK(hipEventRecord(ev[4], 0));
+        CK(hipEventSynchronize(ev[4]));
+        for (int q = 0; q < 4; ++q) {
+            float ms;
+            CK(hipEventElapsedTime(&ms, ev[q], ev[q + 1]));
+            tk[q].push_back(ms * 1000.f);
+        }
+        IterState h;
+        CK(hipMemcpy(&h, st, sizeof h, hipMemcpyDeviceToHost));
+        bool ok = h.k == bk;
+        if (!ok && h.k > 0 && h.k <= n) {  // a rounding-level tie of the FRMSD curve
+            const double fg = hfrmsd(h.k, n, S[h.k], lam);
+            ok = fabs(fg - bf) <= 1e-12 * bf;
+        }
+        if (ok && h.k > 0) {
+            const uint32_t tp = ord[h.k - 1];
+            ok = h.tkey == key[tp] && (uint32_t)h.torig == orig[tp] &&
+                 fabs(h.frmsd - hfrmsd(h.k, n, S[h.k], lam)) <= 1e-12 * h.frmsd;
+        }
+        if (!ok) {
+            ++bad;
+            if (bad < 4)
+                printf("MISMATCH rep %d: gpu k=%lld f=%.17g tkey=%llx torig=%lld | cpu k=%lld "
+                       "f=%.17g\n",
+                       it, h.k, h.frmsd, h.tkey, h.torig, bk, bf);
+        }
+    }
+    unsigned stats[3];
+    unsigned *dstats;
+    CK(hipMalloc(&dstats, 16));
+    CK(launch_select_stats(tmp, n, dstats, 0));
+    CK(hipMemcpy(stats, dstats, 12, hipMemcpyDeviceToHost));
+    SelCtl ctl;
+    CK(hipMemcpy(&ctl, w.ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    const char *names[4] = {"hist", "bounds", "gather", "final"};
+    printf("n=%lld mode=%d lam=%g k=%lld cand=%u buckets=[%d,%d] levels=%u radix=%u err=%u "
+           "bad=%d/%d\n",
+           (long long)n, mode, lam, bk, ctl.ccount, ctl.b0, ctl.b1, stats[1], stats[2], stats[0],
+           bad, reps);
+    float tot = 0.f;
+    for (int q = 0; q < 4; ++q) {
+        std::sort(tk[q].begin(), tk[q].end());
+        const float med = tk[q][tk[q].size() / 2];
+        tot += med;
+        printf("  %-7s %8.2f us\n", names[q], med);
+    }
+    printf("  total   %8.2f us\n", tot);
+    return bad ? 1 : 0;
+}

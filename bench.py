@@ -291,6 +291,8 @@ def main():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--nn-timing", default="first", choices=["first", "all", "none"],
+                    help="timed steps whose NN dispatches carry HIP events")
     ap.add_argument("--nn-mode", default="grid", choices=["auto", "brute", "grid"])
     ap.add_argument("--plots", type=int, default=0, help="batch workload: number of plots (default 1024)")
     ap.add_argument("--c5-size", type=int, default=0, help="c5 workload: trees = stems (default 8M)")
@@ -339,14 +341,22 @@ def main():
     for _ in range(args.warmup):
         step()
     ctx.profile_report()  # drop warmup records
-    ctx.profile_enable(_lib.PROF_NN)
+    # NN launch timing: events carried by the NN dispatches themselves, inside the timed
+    # region.  Each timed dispatch still leaves ~5 us of idle queue around it, so by
+    # default only the first timed step carries them (--nn-timing all: every step).
+    ctx.profile_enable(_lib.PROF_NN if args.nn_timing != "none" else 0)
     barrier()
     t0 = time.perf_counter()
     fits = calls = 0
-    for _ in range(args.steps):
+    timed_calls = 0
+    for s_i in range(args.steps):
         st = step()
         fits += st["n_fits"]
         calls += st["n_nn_calls"]
+        if args.nn_timing == "all" or (args.nn_timing == "first" and s_i == 0):
+            timed_calls += st["n_nn_calls"]
+        if s_i == 0 and args.nn_timing == "first":
+            ctx.profile_enable(0)
     barrier()
     dt = time.perf_counter() - t0
     ctx.profile_enable(0)
@@ -366,7 +376,7 @@ def main():
         nn = prof.get("nn_grid") or prof.get("nn_brute") or {"count": 0, "ms": 0.0}
         # per real NN call: the device loop also enqueues a few no-op iterations past the
         # end of each run (their early-exit launches are in nn["ms"]: conservative)
-        launches = int(calls_all / world) if world else nn["count"]
+        launches = timed_calls
         avg_ms = nn["ms"] / max(launches, 1)
         bytes_launch = nn_bytes_per_launch(n, m, md)
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0

@@ -174,8 +174,8 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             a.prev_bp = warm == 2 ? c->bp.as<int32_t>() : nullptr;
         }
         {
-            ProfScope ps(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
-            HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream, false));
+            KernelEvents ke(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
+            HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream, false, ke.a, ke.b));
         }
         if (a.range && reduce_range)
             HIPCHK(launch_range_reduce(a.range, nn_range_parts(n, c->m, true), c->stream));
@@ -293,6 +293,26 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
     return FICP_OK;
 }
 
+// Wait for a done flag that a kernel stores into coherent pinned memory (-1 = not yet
+// written).  The stream is queried now and then so that a device error or a drained
+// stream without the store ends the wait instead of spinning forever.
+int poll_flag(ficp_ctx *c, int *flag, int &v) {
+    for (uint64_t spin = 1;; ++spin) {
+        v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
+        if (v != -1) return FICP_OK;
+        if ((spin & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) {
+                v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
+                if (v != -1) return FICP_OK;
+                return fail(FICP_EHIP, "device loop flag was not written");
+            }
+            if (e != hipErrorNotReady) return fail(FICP_EHIP, "device loop: %s", hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 // the device-resident ICP: stages of ficp.py:122-147
 int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, int32_t nstages,
              const double *lambdas, double threshold, int32_t max_iter, int32_t allow_refl,
@@ -376,6 +396,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         // selection path without traces: the selection's last kernel also runs the loop
         // step and stores the done flag straight into the pinned ring
         const bool fused = sel && !tidx;
+        if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, j == 0 ? 1 : 2, &dst->done, &dst->apply,
                     !sel));
         if (sel) {
@@ -394,11 +415,19 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             HIPCHK(hipMemcpyAsync(&c->h_flags[slot], &dst->done, 4, hipMemcpyDeviceToHost,
                                   c->stream));
         }
-        HIPCHK(hipEventRecord(c->loop_ev[slot], c->stream));
+        // fused: the final kernel stores the flag itself, so the host polls the pinned word
+        // (no event record: each one costs an idle gap in the queue)
+        if (!fused) HIPCHK(hipEventRecord(c->loop_ev[slot], c->stream));
         if (j >= la) {
             const int old = (int)((j - la) % kLoopRing);
-            HIPCHK(hipEventSynchronize(c->loop_ev[old]));
-            finished = c->h_flags[old] != 0;
+            if (fused) {
+                int v = 0;
+                CHK(poll_flag(c, &c->h_flags[old], v));
+                finished = v != 0;
+            } else {
+                HIPCHK(hipEventSynchronize(c->loop_ev[old]));
+                finished = c->h_flags[old] != 0;
+            }
         }
     }
     CHK(read_state(c));

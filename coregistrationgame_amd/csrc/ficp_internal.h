@@ -244,8 +244,10 @@ hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t n
                                   hipStream_t s);
 // The NN launchers finish with launch_range_reduce when a.range is set, unless
 // reduce_range is false (then the caller launches it, over nn_range_parts workgroups).
+// ev_start/ev_stop (nullable): events carried by the NN dispatch itself (kernel timing)
 hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s,
-                          bool reduce_range = true);
+                          bool reduce_range = true, hipEvent_t ev_start = nullptr,
+                          hipEvent_t ev_stop = nullptr);
 int64_t nn_range_parts(int64_t n, int64_t m, bool grid);
 int64_t brute_chunk_count(int64_t n, int64_t m);  // target chunks of the brute kernel
 hipError_t launch_nn_brute(const NNArgs &a, const double *tx, const double *ty,

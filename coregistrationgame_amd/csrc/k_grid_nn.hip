@@ -20,6 +20,8 @@
 // source load, and write idx, dist, d2, the sort key, and the matched stem's XY.
 #include "ficp_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <math.h>
 #include <stdlib.h>
 
@@ -734,15 +736,15 @@ hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t n
 }
 
 hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s,
-                          bool reduce_range) {
+                          bool reduce_range, hipEvent_t e0, hipEvent_t e1) {
     if (a.n == 0) return hipSuccess;
     dim3 grid(nblk(a.n)), blk(256);
     if (md == 3) {
-        if (a.T) hipLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, a, g);
-        else hipLaunchKernelGGL((k_nn_grid<3, false>), grid, blk, 0, s, a, g);
+        if (a.T) hipExtLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, e0, e1, 0, a, g);
+        else hipExtLaunchKernelGGL((k_nn_grid<3, false>), grid, blk, 0, s, e0, e1, 0, a, g);
     } else {
-        if (a.T) hipLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, a, g);
-        else hipLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, a, g);
+        if (a.T) hipExtLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, e0, e1, 0, a, g);
+        else hipExtLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, e0, e1, 0, a, g);
     }
     if (a.range && reduce_range) return launch_range_reduce(a.range, grid.x, s);
     return hipGetLastError();

@@ -16,11 +16,11 @@
 //  1. k_sel_hist    : 8192 buckets of (key - kmin) >> s over the NN call's key range;
 //                     count + fixed-point sum of r per bucket (grid 2^(e_b - 37) with
 //                     r < 2^e_b in the bucket: relative truncation < 2^-35), in LDS,
-//                     then one integer atomic per non-empty bucket and workgroup.
+//                     stored per workgroup; k_sel_reduce adds the workgroups' copies.
 //  2. k_sel_bounds  : one workgroup; prefix counts/sums over the buckets; U = the
 //                     smallest FRMSD upper bound at any bucket end; candidate buckets
 //                     [b0, b1] = those whose lower bound is <= U.  The true first
-//                     minimum lies inside them.  Reads and resets the histogram.
+//                     minimum lies inside them.
 //  3. k_sel_gather  : one pass: S_base = sum of r below b0 (fixed reduction tree, so
 //                     bitwise deterministic), candidates (key, orig, r) appended.
 //  4. k_sel_final   : one workgroup; (a) <= 4096 candidates: LDS bucket sort by
@@ -46,10 +46,29 @@ namespace {
 typedef unsigned long long u64;
 typedef unsigned __int128 u128;
 
+// phase timestamps of the final kernel (tools/selcheck built with -DSEL_PROF only)
+#ifdef SEL_PROF
+__device__ unsigned long long g_selprof[32];
+__device__ unsigned long long g_selclk[32];
+#define SELPROF(i)                                       \
+    do {                                                 \
+        __syncthreads();                                 \
+        if (threadIdx.x == 0) {                          \
+            g_selprof[i] = wall_clock64();               \
+            g_selclk[i] = clock64();                     \
+        }                                                \
+    } while (0)
+#else
+#define SELPROF(i) \
+    do {           \
+    } while (0)
+#endif
+
 constexpr int NB = 8192;     // level-0 buckets
 constexpr int NB_LOG = 13;
-constexpr int HT = 1024;     // threads of the histogram / bounds / final kernels
+constexpr int HT = 512;      // threads of the bounds / final kernels (at 1024 they spilled)
 constexpr int NWAVE = HT / 64;
+constexpr int HHT = 1024;    // threads of the histogram kernel (33 VGPRs)
 constexpr int CAP = 4096;    // candidates sorted in LDS
 constexpr int NSB = 2048;    // bins of the LDS bucket sort
 constexpr int NSB_LOG = 11;
@@ -57,7 +76,7 @@ constexpr int NS = 4096;     // sub-bins of one refinement level
 constexpr int NS_LOG = 12;
 constexpr int MAXLEV = 4;
 constexpr int GT = 256;      // gather: threads per block
-constexpr int GI = 8;        // gather: rows per thread
+constexpr int GI = 16;       // gather: rows per thread (~1 block per CU at 1M rows)
 
 // error bits of SelCtl::err (sticky; the host checks them after a run)
 constexpr unsigned ERR_EMPTY = 1u;  // candidate set empty (cannot happen with finite r)
@@ -74,8 +93,10 @@ struct SelCtl {
 };
 
 struct SelWS {
-    unsigned *hcnt;  // [NB] agent-scope atomics only
-    u64 *hfix;       // [NB] fixed-point sums, agent-scope atomics only
+    unsigned *hcnt;  // [NB] reduced counts (plain stores, k_sel_reduce)
+    u64 *hfix;       // [NB] reduced fixed-point sums (plain stores, k_sel_reduce)
+    unsigned *pcnt;  // [HBMAX][NB] per-block counts of k_sel_hist (plain stores)
+    u64 *pfix;       // [HBMAX][NB] per-block fixed-point sums
     SelCtl *ctl;
     double *parts;   // [gather blocks]
     u64 *ka, *kb;    // candidate ping-pong buffers (n each)
@@ -85,7 +106,12 @@ struct SelWS {
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 inline int gather_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + GT * GI - 1) / (GT * GI)); }
-inline int hist_blocks(int64_t n) { return (int)std::min<int64_t>(128, std::max<int64_t>(1, (n + 16383) / 16384)); }
+// Histogram blocks: each writes its whole LDS histogram (12 B per bucket) with plain
+// stores and k_sel_reduce sums them.  Global atomics execute at the memory side at one
+// wave-instruction per ~50 ns per CU (MI355X_MICROARCH.md, global atomics), so flushing
+// 8192 buckets with atomics cost ~15 us and reading + resetting them from one CU ~25 us.
+constexpr int HBMAX = 64;
+inline int hist_blocks(int64_t n) { return (int)std::min<int64_t>(HBMAX, std::max<int64_t>(1, (n + 8191) / 8192)); }
 
 SelWS carve(void *tmp, int64_t n) {
     char *p = (char *)tmp;
@@ -94,6 +120,10 @@ SelWS carve(void *tmp, int64_t n) {
     p += align_up(NB * 4, 256);
     w.hfix = (u64 *)p;
     p += align_up(NB * 8, 256);
+    w.pcnt = (unsigned *)p;
+    p += align_up((int64_t)HBMAX * NB * 4, 256);
+    w.pfix = (u64 *)p;
+    p += align_up((int64_t)HBMAX * NB * 8, 256);
     w.ctl = (SelCtl *)p;
     p += 256;
     w.parts = (double *)p;
@@ -218,7 +248,8 @@ __device__ __forceinline__ double blk_max_d(double x, Scr &s) {
 }
 
 // {min, max} of two u64 quantities at once: returns min(a), max(b)
-__device__ __forceinline__ void blk_minmax_u64(u64 &a, u64 &b, Scr &s) {
+template <int NW = NWAVE>
+__device__ __forceinline__ void blk_minmax_u64(u64 &a, u64 &b, u64 *su, u64 *sv) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const u64 xa = __shfl_xor(a, o, 64), xb = __shfl_xor(b, o, 64);
@@ -226,18 +257,56 @@ __device__ __forceinline__ void blk_minmax_u64(u64 &a, u64 &b, Scr &s) {
         b = xb > b ? xb : b;
     }
     if ((threadIdx.x & 63) == 0) {
-        s.u[threadIdx.x >> 6] = a;
-        s.v[threadIdx.x >> 6] = b;
+        su[threadIdx.x >> 6] = a;
+        sv[threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    a = su[0];
+    b = sv[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+        a = su[w] < a ? su[w] : a;
+        b = sv[w] > b ? sv[w] : b;
+    }
+    __syncthreads();
+}
+
+// min(a), max(b), min(c), max(d) in one reduction (one pair of barriers)
+__device__ __forceinline__ void blk_minmax2_u64(u64 &a, u64 &b, u64 &c, u64 &d, Scr &s) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const u64 xa = __shfl_xor(a, o, 64), xb = __shfl_xor(b, o, 64);
+        const u64 xc = __shfl_xor(c, o, 64), xd = __shfl_xor(d, o, 64);
+        a = xa < a ? xa : a;
+        b = xb > b ? xb : b;
+        c = xc < c ? xc : c;
+        d = xd > d ? xd : d;
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s.u[wv] = a;
+        s.v[wv] = b;
+        s.l[wv] = (long long)c;
+        s.d[wv] = __longlong_as_double((long long)d);
     }
     __syncthreads();
     a = s.u[0];
     b = s.v[0];
+    c = (u64)s.l[0];
+    d = (u64)__double_as_longlong(s.d[0]);
 #pragma unroll
     for (int w = 1; w < NWAVE; ++w) {
         a = s.u[w] < a ? s.u[w] : a;
         b = s.v[w] > b ? s.v[w] : b;
+        const u64 cw = (u64)s.l[w], dw = (u64)__double_as_longlong(s.d[w]);
+        c = cw < c ? cw : c;
+        d = dw > d ? dw : d;
     }
     __syncthreads();
+}
+
+__device__ __forceinline__ void blk_minmax_u64(u64 &a, u64 &b, Scr &s) {
+    blk_minmax_u64<NWAVE>(a, b, s.u, s.v);
 }
 
 __device__ __forceinline__ long long blk_max_ll(long long x, Scr &s) {
@@ -301,6 +370,46 @@ __device__ __forceinline__ long long blk_excl_scan_ll(long long v, Scr &s, long 
     return off + x - v;
 }
 
+// exclusive scans of a count and two sums at once (the same operations, in the same
+// order, as blk_excl_scan_ll + two blk_excl_scan_d; one set of barriers)
+__device__ __forceinline__ void blk_excl_scan3(long long &c, double &a, double &b, Scr &s) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    long long xc = c;
+    double xa = a, xb = b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long yc = __shfl_up(xc, o, 64);
+        const double ya = __shfl_up(xa, o, 64), yb = __shfl_up(xb, o, 64);
+        if (lane >= o) {
+            xc += yc;
+            xa = ya + xa;
+            xb = yb + xb;
+        }
+    }
+    if (lane == 63) {
+        s.l[wave] = xc;
+        s.d[wave] = xa;
+        s.u[wave] = (u64)__double_as_longlong(xb);
+    }
+    double ea = __shfl_up(xa, 1, 64), eb = __shfl_up(xb, 1, 64);
+    if (lane == 0) ea = eb = 0.0;
+    __syncthreads();
+    long long oc = 0;
+    double oa = 0.0, ob = 0.0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) {
+        if (w < wave) {
+            oc += s.l[w];
+            oa = oa + s.d[w];
+            ob = ob + __longlong_as_double((long long)s.u[w]);
+        }
+    }
+    __syncthreads();
+    c = oc + xc - c;
+    a = wave ? oa + ea : ea;
+    b = wave ? ob + eb : eb;
+}
+
 // block argmin of (f, k) with the first-minimum rule; result broadcast
 __device__ __forceinline__ void blk_argmin(double &f, long long &k, Scr &s) {
 #pragma unroll
@@ -331,24 +440,24 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, Scr &s) {
 // ------------------------------------------------------------------ kernels
 // range: with nparts > 0, every block reduces the producer's range parts itself (see
 // block_range_store) and block 0 stores range[0..1] for the kernels that follow.
-__global__ __launch_bounds__(HT) void k_sel_hist(const u64 *key, const double *r, int64_t n,
+__global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *r, int64_t n,
                                                  u64 *range, int64_t nparts, SelWS w,
                                                  const int *skip) {
     if (skip && *skip) return;
     __shared__ unsigned sc[NB];
     __shared__ u64 sf[NB];
     __shared__ short se[NB];
-    __shared__ Scr scr;
+    __shared__ u64 s_u[HHT / 64], s_v[HHT / 64];
     u64 kmin, kmax;
     if (nparts > 0) {
         u64 a = 0, b = 0;
-        for (int64_t q = threadIdx.x; q < nparts; q += HT) {
+        for (int64_t q = threadIdx.x; q < nparts; q += HHT) {
             const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(range + 2 + 2 * q);
             a = max(a, v.x);
             b = max(b, v.y);
         }
         a = ~a;
-        blk_minmax_u64(a, b, scr);
+        blk_minmax_u64<HHT / 64>(a, b, s_u, s_v);
         kmin = a;
         kmax = b;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -360,7 +469,7 @@ __global__ __launch_bounds__(HT) void k_sel_hist(const u64 *key, const double *r
         kmax = range[1];
     }
     const int s = sel_shift(kmin, kmax);
-    for (int b = threadIdx.x; b < NB; b += HT) {
+    for (int b = threadIdx.x; b < NB; b += HHT) {
         sc[b] = 0u;
         sf[b] = 0ULL;
         se[b] = (short)bucket_exp(kmin, kmax, s, b);
@@ -368,32 +477,84 @@ __global__ __launch_bounds__(HT) void k_sel_hist(const u64 *key, const double *r
     __syncthreads();
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * per, i1 = min(n, i0 + per);
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += HT) {
-        const int b = (int)((key[i] - kmin) >> s);
-        const int e = se[b];
-        const double rv = r[i];
-        const u64 m = (e < 1024 && rv < INFINITY) ? (u64)ldexp(rv, FIXB - e) : 0ULL;
-        atomicAdd(&sc[b], 1u);
-        atomicAdd(&sf[b], m);
+    constexpr int U = 4;  // rows in flight per thread
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * HHT) {
+        u64 kk[U];
+        double rv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = i + (int64_t)u * HHT;
+            kk[u] = q < i1 ? key[q] : 0ULL;
+            rv[u] = q < i1 ? r[q] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (i + (int64_t)u * HHT < i1) {
+                const int b = (int)((kk[u] - kmin) >> s);
+                const int e = se[b];
+                const u64 m = (e < 1024 && rv[u] < INFINITY) ? (u64)ldexp(rv[u], FIXB - e) : 0ULL;
+                atomicAdd(&sc[b], 1u);
+                atomicAdd(&sf[b], m);
+            }
+        }
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < NB; b += HT) {
-        if (sc[b]) {
-            __hip_atomic_fetch_add(&w.hcnt[b], sc[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&w.hfix[b], sf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    unsigned *pc = w.pcnt + (int64_t)blockIdx.x * NB;
+    u64 *pf = w.pfix + (int64_t)blockIdx.x * NB;
+    for (int b = threadIdx.x; b < NB; b += HHT) {
+        pc[b] = sc[b];
+        pf[b] = sf[b];
     }
 }
 
+// sum of the per-block histograms, one bucket per thread (integer sums: exact, order-free)
+__global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int *skip) {
+    if (skip && *skip) return;
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    unsigned c = 0;
+    u64 f = 0;
+    int q = 0;
+    for (; q + 8 <= nhb; q += 8) {
+        unsigned cv[8];
+        u64 fv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            cv[u] = w.pcnt[(int64_t)(q + u) * NB + b];
+            fv[u] = w.pfix[(int64_t)(q + u) * NB + b];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            c += cv[u];
+            f += fv[u];
+        }
+    }
+    for (; q < nhb; ++q) {
+        c += w.pcnt[(int64_t)q * NB + b];
+        f += w.pfix[(int64_t)q * NB + b];
+    }
+    w.hcnt[b] = c;
+    w.hfix[b] = f;
+}
+
+// Bounds of the FRMSD curve over the level-0 buckets (one workgroup).  Per-thread
+// chunks of PER consecutive buckets; the per-bucket work (two or four log2 each) runs
+// only for the chunks that can hold the minimum, one bucket per lane (a chunk walked by
+// its own thread serialised ~16 dependent evaluations: ~10 us at C3).
+constexpr int MAXACT = HT / (NB / HT);  // active chunks evaluated one bucket per lane
 __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double lam,
                                                    const double *lam_dev, const u64 *range,
                                                    const int *skip) {
     if (skip && *skip) return;
     if (lam_dev) lam = *lam_dev;
+    constexpr int PER = NB / HT;
     __shared__ Scr scr;
     __shared__ unsigned lc[NB];
     __shared__ u64 lf[NB];
-    constexpr int PER = NB / HT;
+    __shared__ long long eC[MAXACT * PER];  // rows before bucket j of active chunk a
+    __shared__ double eLo[MAXACT * PER];    // lower sum before it
+    __shared__ double eHi[MAXACT * PER];    // upper sum through it
+    __shared__ int s_act[MAXACT];
+    __shared__ int s_nact;
     const int t = threadIdx.x;
     const u64 kmin = ~range[0], kmax = range[1];
     const int s = sel_shift(kmin, kmax);
@@ -408,78 +569,133 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
             hi = ldexp((double)(fx + c), e - FIXB);
         }
     };
+    SELPROF(8);
+    if (t == 0) s_nact = 0;
+    for (int j = 0; j < PER; ++j) {  // coalesced: bucket j * HT + t
+        const int b = j * HT + t;
+        lc[b] = w.hcnt[b];
+        lf[b] = w.hfix[b];
+    }
+    __syncthreads();
+    SELPROF(9);
     long long ct = 0;
     double tlo = 0.0, thi = 0.0;
     unsigned cc[PER];
-    u64 ff[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {  // all 2 * PER exchanges in flight at once
-        const int b = t * PER + j;
-        cc[j] = __hip_atomic_exchange(&w.hcnt[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ff[j] = __hip_atomic_exchange(&w.hfix[b], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    double blo[PER], bhi[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const int b = t * PER + j;
-        const unsigned c = cc[j];
-        const u64 fx = ff[j];
-        lc[b] = c;
-        lf[b] = fx;
-        double lo, hi;
-        sums(b, c, fx, lo, hi);
-        ct += c;
-        tlo = tlo + lo;
-        thi = thi + hi;
+        cc[j] = lc[b];
+        sums(b, cc[j], lf[b], blo[j], bhi[j]);
+        ct += cc[j];
+        tlo = tlo + blo[j];
+        thi = thi + bhi[j];
     }
-    long long ctot;
-    double stot;
-    const long long Cex = blk_excl_scan_ll(ct, scr, ctot);
-    const double Plo = blk_excl_scan_d(tlo, scr, stot);
-    const double Phi = blk_excl_scan_d(thi, scr, stot);
-    // U: the smallest upper bound of h at any bucket end
+    long long Cex = ct;
+    double Plo = tlo, Phi = thi;
+    blk_excl_scan3(Cex, Plo, Phi, scr);
+    SELPROF(10);
+    // U: the smallest upper bound of h at any bucket end.  Evaluated coarse to fine, with
+    // the same result as evaluating every bucket: (1) U1 = the bound at each thread's
+    // chunk end; (2) a chunk whose lower bound (its rows are all >= the first bucket's
+    // lo_r) exceeds U1 can neither hold the minimising bucket end nor a candidate bucket;
+    // (3) only the remaining chunks (a few, near the minimum) evaluate their buckets.
     const double p = 2.0 * lam + 1.0;
-    double U = INFINITY;
-    {
-        long long C = Cex;
-        double P = Phi;
-        for (int j = 0; j < PER; ++j) {
-            const int b = t * PER + j;
-            const unsigned c = lc[b];
-            if (c) {
-                double lo, hi;
-                sums(b, c, lf[b], lo, hi);
-                C += c;
-                P = P + hi;
-                U = fmin(U, h_of(C, P, p) + kMarg);
+    double Pend = Phi;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) Pend = Pend + bhi[j];
+    double U1 = ct ? h_of(Cex + ct, Pend, p) + kMarg : INFINITY;
+    U1 = blk_min_d(U1, scr);
+    SELPROF(11);
+    // (the extra 1e-9 covers the fixed-point truncation of the per-bucket lower sums, so
+    // that a chunk's bound never exceeds the bound of a bucket inside it)
+    const bool active = ct && (!(block_lb(Cex, ct, Plo, lo_r(kmin + ((u64)(t * PER) << s)), p) -
+                                       1e-9 > U1) ||
+                               !(p >= 1.0));
+    if (active) {
+        const int a = atomicAdd(&s_nact, 1);
+        if (a < MAXACT) {
+            s_act[a] = t;
+            long long C = Cex;
+            double PL = Plo, PH = Phi;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                eC[a * PER + j] = C;
+                eLo[a * PER + j] = PL;
+                C += cc[j];
+                PL = PL + blo[j];
+                PH = PH + bhi[j];
+                eHi[a * PER + j] = PH;
             }
         }
     }
-    U = blk_min_d(U, scr);
-    // candidate buckets: lower bound <= U (NaN bounds count as candidates)
+    __syncthreads();
+    const int nact = s_nact;
+    double U = INFINITY;
     long long bmin = 0x7fffffffLL, bmax = -1, kb = 0;
-    {
-        long long C = Cex;
-        double P = Plo;
-        for (int j = 0; j < PER; ++j) {
-            const int b = t * PER + j;
+    if (nact <= MAXACT) {
+        // one bucket per lane: work item q = (active chunk q / PER, bucket q % PER)
+        for (int q = t; q < nact * PER; q += HT) {
+            const int b = s_act[q / PER] * PER + (q % PER);
+            const unsigned c = lc[b];
+            if (c) U = fmin(U, h_of(eC[q] + c, eHi[q], p) + kMarg);
+        }
+        U = fmin(blk_min_d(U, scr), U1);
+        SELPROF(12);
+        for (int q = t; q < nact * PER; q += HT) {
+            const int b = s_act[q / PER] * PER + (q % PER);
             const unsigned c = lc[b];
             if (c) {
-                double lo, hi;
-                sums(b, c, lf[b], lo, hi);
-                const double lb = block_lb(C, c, P, lo_r(kmin + ((u64)b << s)), p);
+                const double lb = block_lb(eC[q], c, eLo[q], lo_r(kmin + ((u64)b << s)), p);
                 if (!(lb > U) || !(p >= 1.0)) {
-                    if (bmax < 0) kb = C;  // rows before this thread's first candidate
+                    if (b < bmin) kb = eC[q];  // rows before this lane's first candidate
                     bmin = min(bmin, (long long)b);
                     bmax = max(bmax, (long long)b);
                 }
-                C += c;
-                P = P + lo;
+            }
+        }
+    } else {  // many active chunks: every active thread walks its own buckets
+        if (active) {
+            long long C = Cex;
+            double P = Phi;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                if (cc[j]) {
+                    C += cc[j];
+                    P = P + bhi[j];
+                    U = fmin(U, h_of(C, P, p) + kMarg);
+                }
+            }
+        }
+        U = fmin(blk_min_d(U, scr), U1);
+        SELPROF(12);
+        if (active) {
+            long long C = Cex;
+            double P = Plo;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int b = t * PER + j;
+                if (cc[j]) {
+                    const double lb = block_lb(C, cc[j], P, lo_r(kmin + ((u64)b << s)), p);
+                    if (!(lb > U) || !(p >= 1.0)) {
+                        if (bmax < 0) kb = C;  // rows before this thread's first candidate
+                        bmin = min(bmin, (long long)b);
+                        bmax = max(bmax, (long long)b);
+                    }
+                    C += cc[j];
+                    P = P + blo[j];
+                }
             }
         }
     }
+    SELPROF(13);
     const long long my_bmin = bmin;
-    bmin = blk_min_ll(bmin, scr);
-    bmax = blk_max_ll(bmax, scr);
+    {
+        u64 a = (u64)bmin, z = (u64)(bmax + 1);  // min(bmin), max(bmax) in one reduction
+        blk_minmax_u64(a, z, scr);
+        bmin = (long long)a;
+        bmax = (long long)z - 1;
+    }
     if (bmax < 0) {  // no bucket qualifies (non-finite r): every row is a candidate
         bmin = 0;
         bmax = NB - 1;
@@ -495,6 +711,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
         w.ctl->U = U;
         __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    SELPROF(14);
 }
 
 __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_t *orig,
@@ -532,12 +749,24 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
         inm |= (in ? 1u : 0u) << q;
         wtot += (unsigned)__popcll(masks[q]);
     }
-    if (wtot) {  // one append reservation per wave
-        unsigned pos = 0;
-        if (lane == 0)
-            pos = __hip_atomic_fetch_add(&w.ctl->ccount, wtot, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-        pos = __shfl(pos, 0, 64);
+    // one append reservation per workgroup: a single word takes ~88 atomics/us, so one
+    // per wave (~1800 at 1M rows) serialised this kernel at ~15 us
+    __shared__ unsigned s_cnt[GT / 64], s_pos;
+    const int wave = threadIdx.x >> 6;
+    if (lane == 0) s_cnt[wave] = wtot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot = 0;
+#pragma unroll
+        for (int q = 0; q < GT / 64; ++q) tot += s_cnt[q];
+        s_pos = tot ? __hip_atomic_fetch_add(&w.ctl->ccount, tot, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                    : 0u;
+    }
+    __syncthreads();
+    if (wtot) {
+        unsigned pos = s_pos;
+        for (int q = 0; q < wave; ++q) pos += s_cnt[q];
         const u64 lt = (1ULL << lane) - 1ULL;
 #pragma unroll
         for (int q = 0; q < GI; ++q) {
@@ -667,14 +896,16 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
         omx = o > omx ? o : omx;
     }
     for (int b = t; b < NSB; b += HT) bc[b] = 0u;
-    blk_minmax_u64(kmn, kmx, scr);
-    blk_minmax_u64(omn, omx, scr);
+    SELPROF(2);
+    blk_minmax2_u64(kmn, kmx, omn, omx, scr);
     const Comp cmp = make_comp(kmn, kmx, (uint32_t)omn, (uint32_t)omx);
     const u64 vspan = cmp(kmx, (uint32_t)omx);
     const int vb = bits_of(vspan);
     const int sh = vb > NSB_LOG ? vb - NSB_LOG : 0;
+    SELPROF(16);
     for (unsigned i = t; i < c; i += HT) atomicAdd(&bc[(int)(cmp(lk[i], lo[i]) >> sh)], 1u);
     __syncthreads();
+    SELPROF(17);
     {
         constexpr int PB = NSB / HT;  // 2 bins per thread
         unsigned v[PB];
@@ -694,11 +925,13 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
         }
     }
     __syncthreads();
+    SELPROF(18);
     for (unsigned i = t; i < c; i += HT) {
         const int b = (int)(cmp(lk[i], lo[i]) >> sh);
         mem[bo[b] + atomicAdd(&bc[b], 1u)] = (uint16_t)i;
     }
     __syncthreads();
+    SELPROF(19);
     // rank inside the bin (bins hold few rows unless keys cluster)
     for (unsigned i = t; i < c; i += HT) {
         const u64 k = lk[i];
@@ -713,6 +946,7 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
         pos[rank] = (uint16_t)i;
     }
     __syncthreads();
+    SELPROF(3);
     // exact prefix sums in sorted order, FRMSD of every candidate k
     constexpr int PP = CAP / HT;  // 4 positions per thread
     double v[PP];
@@ -725,21 +959,30 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
     }
     double all;
     double run = blk_excl_scan_d(tsum, scr, all);
-    double bf = INFINITY;
-    long long bk = 0x7fffffffffffffffLL;
+    // prefix sums by sorted position into LDS (over lr: its rows are in v[] now), then
+    // FRMSD of every position with the positions dealt over all lanes (a thread's own
+    // PP positions would run PP dependent pow() chains back to back)
+    __syncthreads();
+    double *ls = lr;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
         const unsigned p = (unsigned)(t * PP + q);
-        if (p < c) {
-            run = run + v[q];
-            const long long k = in.K0 + (long long)p + 1;
-            const double f = frmsd_of(k, in.N, in.S0 + run, in.lam);
-            if (f < bf) {
-                bf = f;
-                bk = k;
-            }
+        run = run + v[q];
+        if (p < c) ls[p] = run;
+    }
+    __syncthreads();
+    SELPROF(20);
+    double bf = INFINITY;
+    long long bk = 0x7fffffffffffffffLL;
+    for (unsigned p = t; p < c; p += HT) {
+        const long long k = in.K0 + (long long)p + 1;
+        const double f = frmsd_of(k, in.N, in.S0 + ls[p], in.lam);
+        if (f < bf) {
+            bf = f;
+            bk = k;
         }
     }
+    SELPROF(4);
     blk_argmin(bf, bk, scr);
     if (t == 0) {
         u64 tk = 0;
@@ -777,8 +1020,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
         rs[b] = 0.0;
     }
     if (t == 0) *rn = 0u;
-    blk_minmax_u64(kmn, kmx, scr);
-    blk_minmax_u64(omn, omx, scr);
+    blk_minmax2_u64(kmn, kmx, omn, omx, scr);
     rmax = blk_max_d(rmax, scr);
     if (!(rmax < INFINITY)) return false;
     const Comp cmp = make_comp(kmn, kmx, (uint32_t)omn, (uint32_t)omx);
@@ -929,8 +1171,7 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
         omn = o < omn ? o : omn;
         omx = o > omx ? o : omx;
     }
-    blk_minmax_u64(kmn, kmx, scr);
-    blk_minmax_u64(omn, omx, scr);
+    blk_minmax2_u64(kmn, kmx, omn, omx, scr);
     const int po = (bits_of(omx - omn) + 7) / 8, pk = (bits_of(kmx - kmn) + 7) / 8;
     const int np = po + pk;  // <= 4 + 8
     for (int j = t; j < 12 * 256; j += HT) hist[j] = 0u;
@@ -1052,6 +1293,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     __shared__ Scr scr;
     __shared__ IterState s_st;  // thread 0's working copy of the state (one load, one store)
     const int t = threadIdx.x;
+    SELPROF(0);
     if (t == 0) s_st = *st;
     double a = 0.0;
     for (int p = t; p < nparts; p += HT) a = a + w.parts[p];  // fixed order per thread
@@ -1063,6 +1305,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     in.U = w.ctl->U;
     unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
+    SELPROF(1);
     if (c == 0) {
         if (t == 0) {
             __hip_atomic_fetch_or(&w.ctl->err, ERR_EMPTY, __ATOMIC_RELAXED,
@@ -1087,19 +1330,17 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
             final_radix(src, dst, c, in, sm, scr, &s_st);
         }
     }
+    SELPROF(5);
     if (t == 0) {
         if (fuse_loop) loop_step(&s_st, lc);
         *st = s_st;
         if (host_flag)
             __hip_atomic_store(host_flag, s_st.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    SELPROF(6);
 }
 
 __global__ void k_sel_init(SelWS w) {
-    for (int b = threadIdx.x; b < NB; b += blockDim.x) {
-        __hip_atomic_exchange(&w.hcnt[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_exchange(&w.hfix[b], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (threadIdx.x == 0) {
         __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_exchange(&w.ctl->err, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1120,7 +1361,8 @@ __global__ void k_sel_read_stats(SelWS w, unsigned *out) {
 
 int64_t sel_tmp_bytes(int64_t n) {
     const int64_t nn = std::max<int64_t>(n, 1);
-    return align_up(NB * 4, 256) + align_up(NB * 8, 256) + 256 +
+    return align_up(NB * 4, 256) + align_up(NB * 8, 256) + align_up((int64_t)HBMAX * NB * 4, 256) +
+           align_up((int64_t)HBMAX * NB * 8, 256) + 256 +
            align_up((int64_t)gather_blocks(n) * 8, 256) + 4 * align_up(nn * 8, 256) +
            2 * align_up(nn * 4, 256) + 256;
 }
@@ -1141,8 +1383,9 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
                          const LoopCtl *loop, int *host_flag, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const SelWS w = carve(tmp, n);
-    hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HT), 0, s, key, r, n, range,
+    hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
                        range_parts, w, skip);
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, s, w, hist_blocks(n), skip);
     hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev,
                        (const unsigned long long *)range, skip);
     const int gb = gather_blocks(n);

@@ -30,6 +30,10 @@ namespace {
 constexpr int FB = 256;
 constexpr int FI = 4;
 constexpr int FTILE = FB * FI;
+// k_fit_sums: 16 rows per thread, ~245 workgroups at 1M rows; each workgroup arrives once
+// at the finishing counter, and one word takes only ~88 atomics/us
+constexpr int FIT_I = 16;
+constexpr int FIT_TILE = FB * FIT_I;
 
 __device__ __forceinline__ double block_sum_d(double v, double *s /*[256]*/) {
     // fixed-order tree: deterministic
@@ -261,28 +265,46 @@ __global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, unsigned
     unsigned long long tk = 0;
     int64_t ti = 0;
     const bool all = fit_threshold(a, tk, ti);
-    const int64_t i0 = (int64_t)blockIdx.x * FTILE + threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.x * FIT_TILE + threadIdx.x;
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // FIT_I rows per thread in chunks of 4, every load of a chunk in flight at once.  The
+    // rows' coordinates are loaded whether selected or not: selection is scattered over
+    // the work order, so a skipped row saves no cache line.
 #pragma unroll
-    for (int q = 0; q < FI; ++q) {
-        const int64_t i = i0 + q * FB;
-        if (i < a.n) {
-            bool sel = all;
-            if (!all) {
-                const unsigned long long ki = a.key[i];
-                sel = ki < tk || (ki == tk && (a.orig ? (int64_t)a.orig[i] : i) <= ti);
-            }
-            if (sel) {
-                const double xs = a.sx[i] - a.px, ys = a.sy[i] - a.py;
-                const double xt = a.cx[i] - a.px, yt = a.cy[i] - a.py;
-                c[0] = c[0] + xs;
-                c[1] = c[1] + ys;
-                c[2] = c[2] + xt;
-                c[3] = c[3] + yt;
-                c[4] = c[4] + xs * xt;
-                c[5] = c[5] + xs * yt;
-                c[6] = c[6] + ys * xt;
-                c[7] = c[7] + ys * yt;
+    for (int q0 = 0; q0 < FIT_I; q0 += 4) {
+        unsigned long long kv[4];
+        double xs[4], ys[4], xt[4], yt[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + (int64_t)(q0 + u) * FB;
+            const bool in = i < a.n;
+            kv[u] = (in && !all) ? a.key[i] : 0ULL;
+            xs[u] = in ? a.sx[i] : 0.0;
+            ys[u] = in ? a.sy[i] : 0.0;
+            xt[u] = in ? a.cx[i] : 0.0;
+            yt[u] = in ? a.cy[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + (int64_t)(q0 + u) * FB;
+            if (i < a.n) {
+                bool sel = all;
+                if (!all) {
+                    const unsigned long long ki = kv[u];
+                    sel = ki < tk || (ki == tk && (a.orig ? (int64_t)a.orig[i] : i) <= ti);
+                }
+                if (sel) {
+                    const double dxs = xs[u] - a.px, dys = ys[u] - a.py;
+                    const double dxt = xt[u] - a.px, dyt = yt[u] - a.py;
+                    c[0] = c[0] + dxs;
+                    c[1] = c[1] + dys;
+                    c[2] = c[2] + dxt;
+                    c[3] = c[3] + dyt;
+                    c[4] = c[4] + dxs * dxt;
+                    c[5] = c[5] + dxs * dyt;
+                    c[6] = c[6] + dys * dxt;
+                    c[7] = c[7] + dys * dyt;
+                }
             }
         }
     }
@@ -472,7 +494,7 @@ hipError_t launch_fit_init(void *tmp, hipStream_t s) {
 
 hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,
                       const int *skip, hipStream_t s) {
-    const int nb = (int)std::max<int64_t>(1, (a.n + FTILE - 1) / FTILE);
+    const int nb = (int)std::max<int64_t>(1, (a.n + FIT_TILE - 1) / FIT_TILE);
     unsigned *ctr = (unsigned *)tmp;
     double *part = (double *)((char *)tmp + 256);
     hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FB), 0, s, a, part, ctr, allow_reflection, st,

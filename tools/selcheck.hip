@@ -126,8 +126,10 @@ int main(int argc, char **argv) {
     int bad = 0;
     for (int it = 0; it < reps; ++it) {
         CK(hipEventRecord(ev[0], 0));
-        hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HT), 0, 0, dkey, dr, n, drange,
+        hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, 0, dkey, dr, n, drange,
                            (int64_t)0, w, (const int *)nullptr);
+        hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, 0, w, hist_blocks(n),
+                           (const int *)nullptr);
         CK(hipEventRecord(ev[1], 0));
         hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam, (const double *)nullptr,
                            (const unsigned long long *)drange, (const int *)nullptr);
@@ -172,7 +174,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(stats, dstats, 12, hipMemcpyDeviceToHost));
     SelCtl ctl;
     CK(hipMemcpy(&ctl, w.ctl, sizeof ctl, hipMemcpyDeviceToHost));
-    const char *names[4] = {"hist", "bounds", "gather", "final"};
+    const char *names[4] = {"hist+red", "bounds", "gather", "final"};
     printf("n=%lld mode=%d lam=%g k=%lld cand=%u buckets=[%d,%d] levels=%u radix=%u err=%u "
            "bad=%d/%d\n",
            (long long)n, mode, lam, bk, ctl.ccount, ctl.b0, ctl.b1, stats[1], stats[2], stats[0],
@@ -185,5 +187,23 @@ int main(int argc, char **argv) {
         printf("  %-7s %8.2f us\n", names[q], med);
     }
     printf("  total   %8.2f us\n", tot);
+#ifdef SEL_PROF
+    unsigned long long ts[32];
+    CK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_selprof), sizeof ts));
+    printf("  final phases (us, last rep):");
+    for (int q = 1; q <= 6; ++q) printf(" %d:%.2f", q, (double)(ts[q] - ts[q - 1]) / 100.0);
+    printf("\n  final_lds: minmax %.2f count %.2f scan %.2f scatter %.2f rank %.2f vscan %.2f frmsd %.2f\n",
+           (ts[16] - ts[2]) / 100.0, (ts[17] - ts[16]) / 100.0, (ts[18] - ts[17]) / 100.0,
+           (ts[19] - ts[18]) / 100.0, (ts[3] - ts[19]) / 100.0, (ts[20] - ts[3]) / 100.0,
+           (ts[4] - ts[20]) / 100.0);
+    unsigned long long tc[32];
+    CK(hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_selclk), sizeof tc));
+    printf("  clock: bounds %llu cycles in %.2f us (%.0f MHz); final %llu cycles in %.2f us (%.0f MHz)\n",
+           tc[14] - tc[8], (ts[14] - ts[8]) / 100.0, (double)(tc[14] - tc[8]) / ((ts[14] - ts[8]) / 100.0),
+           tc[6] - tc[0], (ts[6] - ts[0]) / 100.0, (double)(tc[6] - tc[0]) / ((ts[6] - ts[0]) / 100.0));
+    printf("  bounds: loads %.2f sums+scans %.2f U1 %.2f U %.2f lb %.2f tail %.2f\n",
+           (ts[9] - ts[8]) / 100.0, (ts[10] - ts[9]) / 100.0, (ts[11] - ts[10]) / 100.0,
+           (ts[12] - ts[11]) / 100.0, (ts[13] - ts[12]) / 100.0, (ts[14] - ts[13]) / 100.0);
+#endif
     return bad ? 1 : 0;
 }

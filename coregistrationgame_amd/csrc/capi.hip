@@ -64,7 +64,26 @@ int ensure_grid(ficp_ctx *c) {
     g.gx = (int)gx;
     g.gy = (int)gy;
     g.margin = margin;
-    // counting sort of the stems by cell
+    CHK(c->cell_start.ensure((c->ncells + 1) * 4));
+    CHK(c->pts.ensure(m * sizeof(TPt)));
+    if (bsort_supported(m, c->ncells) && !getenv("FICP_GRID_ATOMIC")) {
+        // two-level bucket sort of the stems by cell (k_bsort.hip)
+        CHK(c->bs_tmp.ensure(bsort_tmp_bytes(m, c->ncells)));
+        const BSortGeom bg{x0, y0, g.inv_h, g.gx, g.gy, 0};
+        BSortOut bo{};
+        bo.pts = c->pts.as<TPt>();
+        bo.cell_start = c->cell_start.as<int32_t>();
+        HIPCHK(launch_bsort(c->tx.as<double>(), c->ty.as<double>(),
+                            c->md == 3 ? c->tz.as<double>() : nullptr, m, bg, c->ncells, bo,
+                            c->bs_tmp.p, c->stream));
+        g.pts = c->pts.as<TPt>();
+        g.cell_start = c->cell_start.as<int32_t>();
+        g.m = m;
+        c->gv = g;
+        c->grid_ready = true;
+        return FICP_OK;
+    }
+    // counting sort of the stems by cell with global atomics (grids bsort cannot plan)
     CHK(c->cell_of.ensure(m * 4));
     CHK(c->counts.ensure((c->ncells + 1) * 4));
     CHK(c->fill.ensure((c->ncells + 1) * 4));
@@ -147,7 +166,7 @@ unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long lo
 // every query from its previous match (grid mode, same work order within one run).
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
             bool want_keys, int warm = 0, const int *skip = nullptr,
-            const int *apply_flag = nullptr, bool reduce_range = true) {
+            const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true) {
     NNArgs a{};
     a.sx = sx;
     a.sy = sy;
@@ -156,7 +175,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.T = T;
     a.skip = skip;
     a.apply_flag = apply_flag;
-    a.idx = c->idx.as<int32_t>();
+    a.idx = want_idx ? c->idx.as<int32_t>() : nullptr;  // the run loop reads idx only for traces
     a.dist = want_keys ? nullptr : c->dist.as<double>();
     a.r = c->r.as<double>();
     a.key = want_keys ? c->key.as<unsigned long long>() : nullptr;
@@ -281,6 +300,19 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
     if (sz) CHK(c->wz.ensure(n * 8));
     CHK(c->worig.ensure(n * 4));
     ProfScope ps(c, P_MISC, "work_order");
+    const GridView &g = c->gv;
+    const int64_t nkeys = (int64_t)((g.gx + 7) / 8) * (int64_t)((g.gy + 7) / 8) * 64;
+    if (bsort_supported(n, nkeys) && !getenv("FICP_WORK_RADIX")) {
+        CHK(c->bs_tmp.ensure(bsort_tmp_bytes(n, nkeys)));
+        const BSortGeom bg{g.x0, g.y0, g.inv_h, g.gx, g.gy, 1};
+        BSortOut bo{};
+        bo.wx = c->wx.as<double>();
+        bo.wy = c->wy.as<double>();
+        bo.wz = sz ? c->wz.as<double>() : nullptr;
+        bo.worig = c->worig.as<uint32_t>();
+        HIPCHK(launch_bsort(sx, sy, sz, n, bg, nkeys, bo, c->bs_tmp.p, c->stream));
+        return FICP_OK;
+    }
     HIPCHK(launch_src_cellkey(sx, sy, n, c->gv, c->key.as<unsigned long long>(), c->stream));
     HIPCHK(launch_key_range(c->key.as<unsigned long long>(), n, range_ptr(c), c->stream));
     HIPCHK(launch_sort(c->key.as<unsigned long long>(), nullptr, n, range_ptr(c),
@@ -398,7 +430,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         const bool fused = sel && !tidx;
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, j == 0 ? 1 : 2, &dst->done, &dst->apply,
-                    !sel));
+                    !sel, tidx != nullptr || !sel));
         if (sel) {
             ProfScope ps(c, P_SORT, "select");
             HIPCHK(launch_select(c->key.as<unsigned long long>(), worig, c->r.as<double>(), n, 0.0,
@@ -562,7 +594,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
                       &c->bp,     &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
-                      &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats};
+                      &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp};
     for (DevBuf *b : bufs) b->release();
     batch_release(c->batch);
     c->batch = nullptr;

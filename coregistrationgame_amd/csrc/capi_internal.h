@@ -116,6 +116,7 @@ struct ficp_ctx {
     DevBuf bp;  // grid slot of each query's last match (warm start of the next NN call)
     DevBuf lams, tr_k, tr_f, tr_l, tr_T, tr_idx;  // device loop: lambdas and traces
     DevBuf sel_tmp, sel_stats;  // bucketed fraction selection (k_select.hip)
+    DevBuf bs_tmp;              // two-level bucket sort scratch (k_bsort.hip)
     unsigned sel_init_gen = 0;  // sel_tmp allocation whose atomic words are initialised
     unsigned fit_init_gen = 0;  // fit_tmp allocation whose arrival counter is zeroed
     unsigned sel_levels = 0, sel_radix = 0;  // selection statistics (cumulative)

@@ -257,6 +257,33 @@ hipError_t launch_deinterleave(const double *rows, int64_t n, int64_t ld, int nc
                                double *c0, double *c1, double *c2, hipStream_t s);
 hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, double *out_xy,
                                 hipStream_t s);
+// Two-level bucket sort of points by a grid key (k_bsort.hip).  mode 0: key = cell id
+// cy * gx + cx (grid layout: TPt records + cell_start); mode 1: 8x8-supertile order
+// (work order: SoA coordinates + caller index).  Order: (key, point index).
+struct BSortGeom {
+    double x0, y0, inv_h;
+    int gx, gy;
+    int mode;
+};
+struct BSortPlan {
+    int fs;         // fine bits (key & ((1 << fs) - 1))
+    int nbk;        // coarse buckets (key >> fs)
+    int nb1;        // slices of the count / scatter kernels
+    int64_t per;    // points per slice
+    int64_t nkeys;
+};
+struct BSortOut {
+    TPt *pts;             // mode 0: records in key order
+    int32_t *cell_start;  // mode 0: [nkeys + 1]
+    double *wx, *wy, *wz; // mode 1 (wz nullable)
+    uint32_t *worig;      // mode 1
+};
+BSortPlan bsort_plan(int64_t n, int64_t nkeys);
+bool bsort_supported(int64_t n, int64_t nkeys);
+int64_t bsort_tmp_bytes(int64_t n, int64_t nkeys);
+hipError_t launch_bsort(const double *x, const double *y, const double *z, int64_t n,
+                        const BSortGeom &g, int64_t nkeys, const BSortOut &o, void *tmp,
+                        hipStream_t s);
 // spatial work order of a source layer: key64 = (8x8-supertile cell order << 32) | i
 hipError_t launch_src_cellkey(const double *sx, const double *sy, int64_t n, const GridView &g,
                               unsigned long long *key, hipStream_t s);

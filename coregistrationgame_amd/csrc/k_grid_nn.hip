@@ -71,10 +71,12 @@ __device__ __forceinline__ Stems stems_of(const TPt *pts, int64_t m) {
     return st;
 }
 
-// best candidate so far: d2, stem index (tie-break), grid slot
+// best candidate so far: d2, stem index (tie-break), grid slot, and the stem's XY (the
+// correspondence written at the end: no reload of the matched record)
 struct Best {
     double d2;
     int id, slot;
+    double px, py;
 };
 
 template <int MD>
@@ -91,6 +93,8 @@ __device__ __forceinline__ void eval_slot(const Stems &S, int p, double qx, doub
     b.d2 = take ? s : b.d2;
     b.id = take ? id : b.id;
     b.slot = take ? p : b.slot;
+    b.px = take ? xy.x : b.px;
+    b.py = take ? xy.y : b.py;
 }
 
 // stems [p0, p1) of the cell-sorted layer, several loads in flight per step (a step past
@@ -147,6 +151,69 @@ __device__ __forceinline__ void disk_scan(const GridView &g, const Stems &S, dou
     }
 }
 
+// The same disk scan with its first three rows (cy - 1, cy, cy + 1) batched: their
+// chords come from the entry bound (a superset of what the shrinking disk needs, so the
+// scan stays exact), all six cell_start loads issue together and then all their stems,
+// FICP_NN_UNROLL loads in flight.  The row-by-row walk made every row's loads wait for
+// the previous row's stems (about 8 dependent memory latencies per query at C3; batched:
+// 4).  Rows at offset >= 2 follow row by row, as before.
+template <int MD>
+__device__ __forceinline__ void disk_scan_batched(const GridView &g, const Stems &S, double qx,
+                                                  double qy, double qz, int cy, double mq,
+                                                  Best &b) {
+    int p0[3], len[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        p0[r] = 0;
+        len[r] = 0;
+        const int yy = cy + r - 1;
+        if (yy < 0 || yy >= g.gy) continue;
+        const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
+        if (beyond(gy, b.d2)) continue;
+        const double gy0 = fmax(gy, 0.0);
+        const double w = sqrt(fmax(b.d2 - gy0 * gy0, 0.0)) + mq;
+        const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
+        const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
+        const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+        p0[r] = row[xl];
+        len[r] = row[xh + 1] - p0[r];
+    }
+    const int l01 = len[0] + len[1], tot = l01 + len[2];
+    for (int t = 0; t < tot; t += FICP_NN_UNROLL) {
+#pragma unroll
+        for (int u = 0; u < FICP_NN_UNROLL; ++u) {
+            const int q = min(t + u, tot - 1);
+            const int slot = q < len[0] ? p0[0] + q : (q < l01 ? p0[1] + (q - len[0]) : p0[2] + (q - l01));
+            eval_slot<MD>(S, slot, qx, qy, qz, b);
+        }
+    }
+#ifdef FICP_NN_NOFAR  // timing experiment only: drop the rows at offset >= 2 (inexact)
+    return;
+#endif
+    for (int k = 2;; ++k) {
+        bool any = false;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const int yy = side ? cy + k : cy - k;
+            if (yy < 0 || yy >= g.gy) continue;
+            const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
+            if (beyond(gy, b.d2)) continue;
+            any = true;
+            const double gy0 = fmax(gy, 0.0);
+            const double w = sqrt(fmax(b.d2 - gy0 * gy0, 0.0)) + mq;
+            const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
+            const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
+            const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+            scan_pts<MD>(S, row[xl], row[xh + 1], qx, qy, qz, b);
+        }
+        if (!any) break;
+    }
+}
+
+#ifndef FICP_NN_BATCHED
+#define FICP_NN_BATCHED 1
+#endif
+
 // Exact 1-NN: a finite first bound from q's own cell (or the warm-start stem, or the
 // first non-empty ring), then the disk-clipped rows.
 template <int MD>
@@ -174,7 +241,8 @@ __device__ __forceinline__ void grid_nn(const GridView &g, const Stems &S, doubl
         }
         if (!(b.d2 < INFINITY)) return;
     }
-    disk_scan<MD>(g, S, qx, qy, qz, cy, mq, b);
+    if (FICP_NN_BATCHED) disk_scan_batched<MD>(g, S, qx, qy, qz, cy, mq, b);
+    else disk_scan<MD>(g, S, qx, qy, qz, cy, mq, b);
 }
 
 // ---------------------------------------------------------------- k nearest (remove_matches)
@@ -292,7 +360,7 @@ __device__ __forceinline__ void apply_T(const double *__restrict__ T, double &x,
 // per-point outputs; returns the sort key
 __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t i, double best,
                                                         int bi) {
-    a.idx[i] = bi;
+    if (a.idx) a.idx[i] = bi;
     const double d = sqrt(best);
     const unsigned long long k = ordkey(d);
     if (a.dist) a.dist[i] = d;
@@ -307,11 +375,9 @@ __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t
 __device__ __forceinline__ void finish(const NNArgs &a, const Stems &S, int64_t i, const Best &b,
                                        unsigned long long &kmin_c, unsigned long long &kmax) {
     if (a.out_bp) a.out_bp[i] = b.slot;
-    if (a.cx) {  // the matched stem's XY from the grid record (L1/L2 hot)
-        const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, b.slot * 32, 0, 0);
-        const double2 c = __builtin_bit_cast(double2, lo);
-        a.cx[i] = c.x;
-        a.cy[i] = c.y;
+    if (a.cx) {  // the matched stem's XY (b.slot is 0 and px, py are 0 for an empty layer)
+        a.cx[i] = b.px;
+        a.cy[i] = b.py;
     }
     const unsigned long long k = write_out(a, i, b.d2, b.id);
     kmin_c = max(kmin_c, ~k);
@@ -331,7 +397,7 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
         a.sy[i] = qy;
     }
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
-    Best b{INFINITY, 0x7fffffff, 0};
+    Best b{INFINITY, 0x7fffffff, 0, 0.0, 0.0};
     if (a.prev_bp) {
         const int pb = a.prev_bp[i];
         if (pb >= 0) eval_slot<MD>(S, pb, qx, qy, qz, b);

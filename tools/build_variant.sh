@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build a variant of libficp.so with extra compile flags, for A/B runs through FICP_LIB:
+# usage: tools/build_variant.sh <name> <flags...>  ->  tools/ab/libficp_<name>.so
+set -e
+cd "$(dirname "$0")/.."
+name=$1; shift
+out=tools/ab/build_$name
+mkdir -p $out
+cd coregistrationgame_amd/csrc
+SRCS=$(sed -n 's/^SRCS = //p' Makefile)
+for f in $SRCS; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -fno-fast-math \
+    -I../../include "$@" -c $f -o ../../$out/${f%.hip}.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../../tools/ab/libficp_$name.so ../../$out/*.o
+echo tools/ab/libficp_$name.so

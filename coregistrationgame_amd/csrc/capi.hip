@@ -187,10 +187,11 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.range = want_keys ? range_ptr(c) : nullptr;
     if (use_grid(c, n)) {
         CHK(ensure_grid(c));
-        if (warm) {
-            CHK(c->bp.ensure(n * 4));
-            a.out_bp = c->bp.as<int32_t>();
-            a.prev_bp = warm == 2 ? c->bp.as<int32_t>() : nullptr;
+        if (warm && a.cx) {
+            // warm start from the previous call's match: (cx, cy) and dz^2 per query
+            CHK(c->dz2.ensure(n * 8));
+            a.dz2 = c->dz2.as<double>();
+            a.warm_c = warm == 2 ? 1 : 0;
         }
         {
             KernelEvents ke(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
@@ -462,7 +463,19 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             }
         }
     }
-    CHK(read_state(c));
+    // one host round trip for everything the run reports: the caller-order XY, the loop
+    // state, the sort's timeout flag and the selection's statistics (each separate sync
+    // cost ~40 us of idle device at C3)
+    if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_state, c->state_dev.p, sizeof(IterState), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(&c->h_misc[0], tflag, 4, hipMemcpyDeviceToHost, c->stream));
+    if (sel) {
+        HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
+        HIPCHK(hipMemcpyAsync(&c->h_misc[1], c->sel_stats.p, 12, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    CHK(sync(c));
     if (!c->h_state->done) return fail(FICP_EHIP, "device ICP loop did not finish");
     if (st) {
         const IterState &h = *c->h_state;
@@ -475,42 +488,33 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         st->frmsd_last[1] = h.frmsd_last[1];
         memcpy(st->T_total, h.Ttot, sizeof st->T_total);
         const int nc = std::min(h.n_nn, mt), nf = std::min(h.n_fit, mt);
-        if (nc > 0) {
-            if (st->trace_k)
+        if (nc > 0 || nf > 0) {
+            if (nc > 0 && st->trace_k)
                 HIPCHK(hipMemcpyAsync(st->trace_k, c->tr_k.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
-            if (st->trace_frmsd)
+            if (nc > 0 && st->trace_frmsd)
                 HIPCHK(hipMemcpyAsync(st->trace_frmsd, c->tr_f.p, nc * 8, hipMemcpyDeviceToHost,
                                       c->stream));
-            if (st->trace_lambda)
+            if (nc > 0 && st->trace_lambda)
                 HIPCHK(hipMemcpyAsync(st->trace_lambda, c->tr_l.p, nc * 8, hipMemcpyDeviceToHost,
                                       c->stream));
-            if (tidx)
+            if (nc > 0 && tidx)
                 HIPCHK(hipMemcpyAsync(st->trace_idx, tidx, (size_t)nc * (size_t)n * 4,
                                       hipMemcpyDeviceToHost, c->stream));
+            if (nf > 0 && st->trace_T)
+                HIPCHK(hipMemcpyAsync(st->trace_T, c->tr_T.p, (size_t)nf * 72, hipMemcpyDeviceToHost,
+                                      c->stream));
+            CHK(sync(c));
         }
-        if (nf > 0 && st->trace_T)
-            HIPCHK(hipMemcpyAsync(st->trace_T, c->tr_T.p, (size_t)nf * 72, hipMemcpyDeviceToHost,
-                                  c->stream));
-    }
-    if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
-    HIPCHK(hipEventRecord(c->ev1, c->stream));
-    CHK(sync(c));
-    if (st) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
         st->gpu_ms = ms;
     }
-    uint32_t tf = 0;
-    HIPCHK(hipMemcpy(&tf, tflag, 4, hipMemcpyDeviceToHost));
-    if (tf) return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", tf);
+    if (c->h_misc[0])
+        return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", c->h_misc[0]);
     if (sel) {
-        unsigned ss[3] = {0, 0, 0};
-        HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
-        HIPCHK(hipMemcpyAsync(ss, c->sel_stats.p, 12, hipMemcpyDeviceToHost, c->stream));
-        CHK(sync(c));
-        c->sel_levels = ss[1];
-        c->sel_radix = ss[2];
-        if (ss[0]) return fail(FICP_EHIP, "fraction selection raised error flag %u", ss[0]);
+        c->sel_levels = c->h_misc[2];
+        c->sel_radix = c->h_misc[3];
+        if (c->h_misc[1]) return fail(FICP_EHIP, "fraction selection raised error flag %u", c->h_misc[1]);
     }
     return FICP_OK;
 }
@@ -571,6 +575,7 @@ int ficp_create(int device, ficp_ctx **out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e == hipSuccess)
         e = hipHostMalloc((void **)&c->h_flags, kLoopRing * sizeof(int), hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_misc, 16 * sizeof(unsigned), hipHostMallocDefault);
     for (int k = 0; k < kLoopRing && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&c->loop_ev[k], hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -593,7 +598,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->ccx,    &c->ccy,        &c->rs,       &c->range,    &c->wx,
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
-                      &c->bp,     &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
+                      &c->bp,     &c->dz2,        &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
                       &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp};
     for (DevBuf *b : bufs) b->release();
     batch_release(c->batch);
@@ -607,6 +612,7 @@ void ficp_destroy(ficp_ctx *c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->h_flags) (void)hipHostFree(c->h_flags);
+    if (c->h_misc) (void)hipHostFree(c->h_misc);
     for (hipEvent_t &e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -114,6 +114,7 @@ struct ficp_ctx {
     DevBuf wx, wy, wz, worig, tidx;  // spatial work order of the source
     DevBuf stage, stage2, cx, cy, cz, state_dev;
     DevBuf bp;  // grid slot of each query's last match (warm start of the next NN call)
+    DevBuf dz2; // dz^2 of each query's last match (warm start from (ccx, ccy, dz2))
     DevBuf lams, tr_k, tr_f, tr_l, tr_T, tr_idx;  // device loop: lambdas and traces
     DevBuf sel_tmp, sel_stats;  // bucketed fraction selection (k_select.hip)
     DevBuf bs_tmp;              // two-level bucket sort scratch (k_bsort.hip)
@@ -121,6 +122,7 @@ struct ficp_ctx {
     unsigned fit_init_gen = 0;  // fit_tmp allocation whose arrival counter is zeroed
     unsigned sel_levels = 0, sel_radix = 0;  // selection statistics (cumulative)
     int *h_flags = nullptr;                        // pinned ring of per-iteration done flags
+    unsigned *h_misc = nullptr;                    // pinned: sort flag, selection stats
     hipEvent_t loop_ev[kLoopRing] = {};
     IterState *h_state = nullptr;  // pinned
 

@@ -110,6 +110,9 @@ struct NNArgs {
     const int32_t *prev_bp;     // grid kernels: grid slot matched by this query in the previous
                                 // call (warm start; nullable, entries < 0 ignored)
     int32_t *out_bp;            // grid kernels: out: grid slot matched (nullable; may alias)
+    double *dz2;                // grid kernels: out: dz^2 of the match (nullable; md 3)
+    int warm_c;                 // grid kernels: start from the previous match held in
+                                // (cx, cy, dz2): its d^2 to the moved query, no record reload
     const int *apply_flag;      // T is applied only while *apply_flag != 0 (nullable: always)
 };
 

@@ -32,7 +32,7 @@ constexpr int BT = 1024;        // threads of k_bs_count / k_bs_scatter
 constexpr int BMAXB = 16384;    // coarse buckets (max)
 constexpr int BMAXB_LOG = 14;
 constexpr int B4T = 256;        // threads of k_bs_bucket
-constexpr int BCAP = 1024;      // points ordered in LDS by one k_bs_bucket workgroup
+constexpr int BCAP = 512;       // points ordered in LDS by one k_bs_bucket workgroup
 constexpr int BMAXF_LOG = 12;   // fine digits per bucket (max 4096)
 constexpr int BMAXF = 1 << BMAXF_LOG;
 
@@ -60,8 +60,19 @@ __global__ __launch_bounds__(BT) void k_bs_count(const double *x, const double *
     for (int b = threadIdx.x; b < p.nbk; b += BT) h[b] = 0u;
     __syncthreads();
     const int64_t i0 = (int64_t)blockIdx.x * p.per, i1 = min(n, i0 + p.per);
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += BT)
-        atomicAdd(&h[bs_key(x[i], y[i], g) >> p.fs], 1u);
+    constexpr int U = 8;  // points in flight per thread
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * BT) {
+        double xv[U], yv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = i + (int64_t)u * BT;
+            xv[u] = q < i1 ? x[q] : 0.0;
+            yv[u] = q < i1 ? y[q] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + (int64_t)u * BT < i1) atomicAdd(&h[bs_key(xv[u], yv[u], g) >> p.fs], 1u);
+    }
     __syncthreads();
     uint32_t *c = counts + (int64_t)blockIdx.x * p.nbk;
     for (int b = threadIdx.x; b < p.nbk; b += BT) c[b] = h[b];
@@ -126,15 +137,34 @@ __global__ __launch_bounds__(BT) void k_bs_scatter(const double *x, const double
     if (blockIdx.x == 0 && threadIdx.x == 0) base_out[p.nbk] = (uint32_t)n;
     __syncthreads();
     const int64_t i0 = (int64_t)blockIdx.x * p.per, i1 = min(n, i0 + p.per);
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += BT) {
-        const double xv = x[i], yv = y[i];
-        const uint32_t slot = atomicAdd(&fill[bs_key(xv, yv, g) >> p.fs], 1u);
-        double4 r;
-        r.x = xv;
-        r.y = yv;
-        r.z = z ? z[i] : 0.0;
-        r.w = __longlong_as_double((long long)i);
-        *reinterpret_cast<double4 *>(rec + slot) = r;
+    constexpr int U = 8;  // points in flight per thread (the loop was load-latency bound)
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * BT) {
+        double xv[U], yv[U], zv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = i + (int64_t)u * BT;
+            const bool in = q < i1;
+            xv[u] = in ? x[q] : 0.0;
+            yv[u] = in ? y[q] : 0.0;
+            zv[u] = (in && z) ? z[q] : 0.0;
+        }
+        uint32_t slot[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            slot[u] = (i + (int64_t)u * BT < i1) ? atomicAdd(&fill[bs_key(xv[u], yv[u], g) >> p.fs], 1u)
+                                                  : 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = i + (int64_t)u * BT;
+            if (q < i1) {
+                double4 r;
+                r.x = xv[u];
+                r.y = yv[u];
+                r.z = zv[u];
+                r.w = __longlong_as_double((long long)q);
+                *reinterpret_cast<double4 *>(rec + slot[u]) = r;
+            }
+        }
     }
 }
 
@@ -160,15 +190,18 @@ __device__ __forceinline__ void bs_emit(const BSortOut &o, int64_t q, const TPt 
 __global__ __launch_bounds__(B4T) void k_bs_bucket(const TPt *rec, const uint32_t *base,
                                                    BSortGeom g, BSortPlan p, BSortOut o,
                                                    uint64_t *gcomp, uint32_t *gpos) {
-    __shared__ uint32_t fc[BMAXF];      // fine-digit counts, then bin starts
-    __shared__ uint32_t ff[BMAXF];      // fill counters
-    __shared__ uint64_t lcomp[BCAP];    // (fine << 32 | index) by bin slot
-    __shared__ uint16_t lsrc[BCAP];     // bin slot -> LDS record
-    __shared__ TPt lrec[BCAP];
+    // dynamic LDS sized by the plan (bs_bucket_lds): ~23 KB at 1M points, so several
+    // workgroups share a CU
+    extern __shared__ __align__(32) unsigned char dyn[];
+    const int nf = 1 << p.fs;
+    TPt *lrec = (TPt *)dyn;                                   // [BCAP]
+    uint64_t *lcomp = (uint64_t *)(dyn + BCAP * sizeof(TPt));  // [BCAP] (fine << 32 | index)
+    uint32_t *fc = (uint32_t *)(lcomp + BCAP);                // [nf] counts, then bin starts
+    uint32_t *ff = fc + nf;                                   // [nf] fill counters
+    uint16_t *lsrc = (uint16_t *)(ff + nf);                   // [BCAP] bin slot -> record
     __shared__ uint32_t s_w[B4T / 64];
     const int b = blockIdx.x;
     const uint32_t lo = base[b], hi = base[b + 1], cnt = hi - lo;
-    const int nf = 1 << p.fs;
     const uint32_t mask = (uint32_t)nf - 1u;
     for (int f = threadIdx.x; f < nf; f += B4T) {
         fc[f] = 0u;
@@ -309,7 +342,8 @@ hipError_t launch_bsort(const double *x, const double *y, const double *z, int64
     hipLaunchKernelGGL(k_bs_colscan, dim3((p.nbk + 3) / 4), dim3(256), 0, s, counts, p, totals);
     hipLaunchKernelGGL(k_bs_scatter, dim3(p.nb1), dim3(BT), 0, s, x, y, z, n, g, p, counts,
                        totals, base, rec);
-    hipLaunchKernelGGL(k_bs_bucket, dim3(p.nbk), dim3(B4T), 0, s, rec, base, g, p, o, gcomp, gpos);
+    const size_t lds = BCAP * (sizeof(TPt) + 8 + 2) + (size_t)2 * 4 * (1 << p.fs);
+    hipLaunchKernelGGL(k_bs_bucket, dim3(p.nbk), dim3(B4T), lds, s, rec, base, g, p, o, gcomp, gpos);
     return hipGetLastError();
 }
 

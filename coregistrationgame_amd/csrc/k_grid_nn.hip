@@ -55,6 +55,17 @@ __device__ __forceinline__ double sq_dist(double qx, double qy, double qz, doubl
 // The cell-sorted stems are read through a buffer descriptor: 32-bit per-lane byte
 // offsets, no 64-bit address arithmetic per candidate (cdna_hip_programming.md T8).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+
+// z and index of a record: 12 B (dwordx3).  A dwordx4 load of them left its unused 4th
+// dword free for the register allocator, which placed the next candidate's address there
+// and so made every candidate wait for the previous one's loads (s_waitcnt vmcnt(0)).
+__device__ __forceinline__ u32x3 load_zid(__amdgpu_buffer_rsrc_t r, int p) {
+    return __builtin_amdgcn_raw_buffer_load_b96(r, p * 32 + 16, 0, 0);
+}
+__device__ __forceinline__ double zid_z(const u32x3 &v) {
+    return __longlong_as_double((long long)(((unsigned long long)v.y << 32) | v.x));
+}
 
 #ifndef FICP_NN_UNROLL
 #define FICP_NN_UNROLL 2  // candidate loads in flight per lane (2: best of 1, 2, 4, 8 at C3)
@@ -71,30 +82,37 @@ __device__ __forceinline__ Stems stems_of(const TPt *pts, int64_t m) {
     return st;
 }
 
-// best candidate so far: d2, stem index (tie-break), grid slot, and the stem's XY (the
-// correspondence written at the end: no reload of the matched record)
+// best candidate so far: d2, stem index (tie-break), grid slot.  The kernel is VALU-bound
+// (~70 % busy at C3), so the loop carries only what the comparison needs; the matched
+// record is reloaded once at the end.
 struct Best {
     double d2;
     int id, slot;
-    double px, py;
 };
 
 template <int MD>
 __device__ __forceinline__ void eval_slot(const Stems &S, int p, double qx, double qy, double qz,
                                           Best &b) {
     const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32, 0, 0);
-    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32 + 16, 0, 0);
+    const u32x3 hi = load_zid(S.r, p);
     const double2 xy = __builtin_bit_cast(double2, lo);
-    const double pz = __builtin_bit_cast(double2, hi).x;
+    const double pz = zid_z(hi);
     const int id = (int)hi.z;
-    const double s = sq_dist<MD>(qx, qy, qz, xy.x, xy.y, pz);
+    // sq_dist's operations in its order, with dz^2 kept
+    const double dx = qx - xy.x, dy = qy - xy.y;
+    double s = dx * dx;
+    s = s + dy * dy;
+    double dzz = 0.0;
+    if (MD == 3) {
+        const double dz = qz - pz;
+        dzz = dz * dz;
+        s = s + dzz;
+    }
     // strict < keeps the best; an equal distance goes to the lower stem index
     const bool take = (s < b.d2) | ((s == b.d2) & (id < b.id));
     b.d2 = take ? s : b.d2;
     b.id = take ? id : b.id;
     b.slot = take ? p : b.slot;
-    b.px = take ? xy.x : b.px;
-    b.py = take ? xy.y : b.py;
 }
 
 // stems [p0, p1) of the cell-sorted layer, several loads in flight per step (a step past
@@ -257,11 +275,11 @@ __device__ __forceinline__ void knn_eval(const Stems &S, int p, double qx, doubl
                                          const uint8_t *removed, double (&kd)[KNN],
                                          int (&kid)[KNN]) {
     const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32, 0, 0);
-    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32 + 16, 0, 0);
+    const u32x3 hi = load_zid(S.r, p);
     const int id = (int)hi.z;
     if (removed && removed[id]) return;
     const double2 xy = __builtin_bit_cast(double2, lo);
-    const double dd = sqrt(sq_dist<MD>(qx, qy, qz, xy.x, xy.y, __builtin_bit_cast(double2, hi).x));
+    const double dd = sqrt(sq_dist<MD>(qx, qy, qz, xy.x, xy.y, zid_z(hi)));
     if (!(dd < kd[KNN - 1] || (dd == kd[KNN - 1] && id < kid[KNN - 1]))) return;
     kd[KNN - 1] = dd;
     kid[KNN - 1] = id;
@@ -372,12 +390,21 @@ __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t
 
 // Per-query finish: matched slot, correspondence XY, idx/dist/r/key; folds the key into
 // this thread's range accumulator.
-__device__ __forceinline__ void finish(const NNArgs &a, const Stems &S, int64_t i, const Best &b,
+__device__ __forceinline__ void finish(const NNArgs &a, const Stems &S, int64_t i, double qz,
+                                       const Best &b,
                                        unsigned long long &kmin_c, unsigned long long &kmax) {
     if (a.out_bp) a.out_bp[i] = b.slot;
-    if (a.cx) {  // the matched stem's XY (b.slot is 0 and px, py are 0 for an empty layer)
-        a.cx[i] = b.px;
-        a.cy[i] = b.py;
+    if (a.cx || a.dz2) {  // the matched record (L1-hot); slot 0 for an unmatched query
+        const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, b.slot * 32, 0, 0);
+        const double2 c = __builtin_bit_cast(double2, lo);
+        if (a.cx) {
+            a.cx[i] = c.x;
+            a.cy[i] = c.y;
+        }
+        if (a.dz2) {  // the next call's warm start: z never moves, d2 = dx^2 + dy^2 + dz2
+            const double dz = qz - zid_z(load_zid(S.r, b.slot));
+            a.dz2[i] = dz * dz;
+        }
     }
     const unsigned long long k = write_out(a, i, b.d2, b.id);
     kmin_c = max(kmin_c, ~k);
@@ -397,13 +424,33 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
         a.sy[i] = qy;
     }
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
-    Best b{INFINITY, 0x7fffffff, 0, 0.0, 0.0};
-    if (a.prev_bp) {
+    Best b{INFINITY, 0x7fffffff, 0};
+#ifdef FICP_NN_IOONLY  // timing experiments only (inexact)
+    b.d2 = qx * 1e-9;
+    b.id = (int)i;
+#else
+    if (a.warm_c) {
+        // the previous match as a finite bound: its exact d2 to the moved query (the
+        // operations of eval_slot), index unknown -- the scan meets it again and an
+        // equal d2 at a lower index still wins the tie
+        const double px = a.cx[i], py = a.cy[i];
+        const double dzz = (MD == 3) ? a.dz2[i] : 0.0;
+        const double dx = qx - px, dy = qy - py;
+        double s = dx * dx;
+        s = s + dy * dy;
+        if (MD == 3) s = s + dzz;
+        if (s < INFINITY) b.d2 = s;
+    } else if (a.prev_bp) {
         const int pb = a.prev_bp[i];
         if (pb >= 0) eval_slot<MD>(S, pb, qx, qy, qz, b);
     }
+#ifndef FICP_NN_WARMONLY
     grid_nn<MD>(g, S, qx, qy, qz, b);
-    finish(a, S, i, b, kmin_c, kmax);
+#else
+    if (!a.prev_bp) grid_nn<MD>(g, S, qx, qy, qz, b);
+#endif
+#endif
+    finish(a, S, i, qz, b, kmin_c, kmax);
 }
 
 template <int MD, bool APPLY>

@@ -28,14 +28,24 @@ thread_local std::string g_err;
 namespace {
 
 // bounding box of the CHM layer (grid geometry and the fit's pivot), once per target
+// Run the report kernel (device segments -> coherent pinned host memory) and poll its
+// flag: one short host wait instead of hipMemcpyAsync + hipStreamSynchronize.
+int poll_flag(ficp_ctx *c, int *flag, int &v);
+int report_wait(ficp_ctx *c, const ReportSeg &a, const ReportSeg &b, const ReportSeg &d) {
+    __atomic_store_n(&c->h_rep->flag, -1, __ATOMIC_RELAXED);
+    HIPCHK(launch_report(a, b, d, &c->h_rep->flag, c->stream));
+    int v = 0;
+    return poll_flag(c, &c->h_rep->flag, v);
+}
+
 int ensure_bbox(ficp_ctx *c) {
     if (c->bbox_ready) return FICP_OK;
     CHK(c->mm_part.ensure(1024 * 4 * 8));
     CHK(c->mm_out.ensure(4 * 8));
     HIPCHK(launch_minmax2(c->tx.as<double>(), c->ty.as<double>(), c->m, c->mm_part.as<double>(),
                           c->mm_out.as<double>(), c->stream));
-    HIPCHK(hipMemcpyAsync(c->bb, c->mm_out.p, sizeof c->bb, hipMemcpyDeviceToHost, c->stream));
-    CHK(sync(c));
+    CHK(report_wait(c, ReportSeg{c->mm_out.p, c->h_rep->bb, 8}, ReportSeg{}, ReportSeg{}));
+    memcpy(c->bb, c->h_rep->bb, sizeof c->bb);
     const double *bb = c->bb;
     if (!(std::isfinite(bb[0]) && std::isfinite(bb[1]) && std::isfinite(bb[2]) &&
           std::isfinite(bb[3])))
@@ -412,6 +422,9 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         }
     }
     HIPCHK(launch_loop_init(dst, lc, c->stream));
+    const FitSrc fsrc{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->pivot_x, c->pivot_y, 1,
+                      allow_refl};
+    const bool fuse_fit = getenv("FICP_FUSE_FIT") && atoi(getenv("FICP_FUSE_FIT")) != 0;
     // Iterations are enqueued `la` ahead of the one whose done flag the host reads, so
     // the device never waits for the host; the iterations enqueued past the end are
     // no-ops (every kernel tests the flags k_loop_update set).
@@ -421,14 +434,16 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     int64_t j = 0;
     bool finished = nstages <= 0;
     for (; j < cap && !finished; ++j) {
-        {
+        // selection path without traces: the selection's last kernel also runs the loop
+        // step and stores the done flag straight into the pinned ring.  FICP_FUSE_FIT=1
+        // also moves the rigid fit into gather + final (no k_fit_sums pass): measured
+        // slower at C3 (gather +7 us, final +8.5 us vs the 12 us pass), so off by default.
+        const bool fused = sel && !tidx;
+        if (!(fused && fuse_fit)) {
             ProfScope ps(c, P_FIT, "fit");
             HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, &dst->no_fit, c->stream));
         }
         const int slot = (int)(j % kLoopRing);
-        // selection path without traces: the selection's last kernel also runs the loop
-        // step and stores the done flag straight into the pinned ring
-        const bool fused = sel && !tidx;
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, j == 0 ? 1 : 2, &dst->done, &dst->apply,
                     !sel, tidx != nullptr || !sel));
@@ -437,7 +452,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             HIPCHK(launch_select(c->key.as<unsigned long long>(), worig, c->r.as<double>(), n, 0.0,
                                  &dst->lam_cur, range_ptr(c), nn_range_parts(n, c->m, use_grid(c, n)),
                                  c->sel_tmp.p, dst, &dst->done, fused ? &lc : nullptr,
-                                 fused ? &c->h_flags[slot] : nullptr, c->stream));
+                                 fused ? &c->h_flags[slot] : nullptr, c->stream,
+                                 (fused && fuse_fit) ? &fsrc : nullptr));
         } else {
             CHK(sort_and_select(c, n, n, 0.0, worig, &dst->done, &dst->lam_cur));
         }
@@ -467,15 +483,14 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // state, the sort's timeout flag and the selection's statistics (each separate sync
     // cost ~40 us of idle device at C3)
     if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_state, c->state_dev.p, sizeof(IterState), hipMemcpyDeviceToHost,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(&c->h_misc[0], tflag, 4, hipMemcpyDeviceToHost, c->stream));
-    if (sel) {
-        HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
-        HIPCHK(hipMemcpyAsync(&c->h_misc[1], c->sel_stats.p, 12, hipMemcpyDeviceToHost, c->stream));
-    }
+    if (sel) HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
     HIPCHK(hipEventRecord(c->ev1, c->stream));
-    CHK(sync(c));
+    c->h_rep->misc[1] = c->h_rep->misc[2] = c->h_rep->misc[3] = 0u;
+    CHK(report_wait(c, ReportSeg{c->state_dev.p, &c->h_rep->st, (int)(sizeof(IterState) / 4)},
+                    ReportSeg{tflag, &c->h_rep->misc[0], 1},
+                    sel ? ReportSeg{c->sel_stats.p, &c->h_rep->misc[1], 3} : ReportSeg{}));
+    memcpy(c->h_state, &c->h_rep->st, sizeof(IterState));
+    memcpy(c->h_misc, c->h_rep->misc, sizeof c->h_rep->misc);
     if (!c->h_state->done) return fail(FICP_EHIP, "device ICP loop did not finish");
     if (st) {
         const IterState &h = *c->h_state;
@@ -506,6 +521,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             CHK(sync(c));
         }
         float ms = 0.f;
+        (void)hipEventSynchronize(c->ev1);  // passed already (the report kernel ran after it)
         (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
         st->gpu_ms = ms;
     }
@@ -576,6 +592,7 @@ int ficp_create(int device, ficp_ctx **out) {
     if (e == hipSuccess)
         e = hipHostMalloc((void **)&c->h_flags, kLoopRing * sizeof(int), hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_misc, 16 * sizeof(unsigned), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_rep, sizeof(HostReport), hipHostMallocCoherent);
     for (int k = 0; k < kLoopRing && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&c->loop_ev[k], hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -613,6 +630,7 @@ void ficp_destroy(ficp_ctx *c) {
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->h_flags) (void)hipHostFree(c->h_flags);
     if (c->h_misc) (void)hipHostFree(c->h_misc);
+    if (c->h_rep) (void)hipHostFree(c->h_rep);
     for (hipEvent_t &e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);

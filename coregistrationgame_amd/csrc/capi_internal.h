@@ -91,6 +91,14 @@ struct BatchBufs;  // capi_batch.hip
 constexpr int kLoopRing = 16;  // in-flight iterations of the device ICP loop (>= lookahead + 1)
 void batch_release(BatchBufs *b);
 
+// coherent pinned block the report kernel writes (capi.hip report_wait)
+struct HostReport {
+    IterState st;
+    unsigned misc[4];  // sort flag, selection {error bits, levels, radix fallbacks}
+    double bb[4];      // CHM bbox
+    int flag;          // -1 while pending, 1 when the segments have landed
+};
+
 struct ficp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -123,6 +131,7 @@ struct ficp_ctx {
     unsigned sel_levels = 0, sel_radix = 0;  // selection statistics (cumulative)
     int *h_flags = nullptr;                        // pinned ring of per-iteration done flags
     unsigned *h_misc = nullptr;                    // pinned: sort flag, selection stats
+    HostReport *h_rep = nullptr;                   // coherent pinned (report kernel)
     hipEvent_t loop_ev[kLoopRing] = {};
     IterState *h_state = nullptr;  // pinned
 

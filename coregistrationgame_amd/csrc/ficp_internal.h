@@ -155,6 +155,85 @@ __device__ __forceinline__ double frmsd_of(long long k, long long N, double S, d
     return (1.0 / pow(frac, lam)) * sqrt(S / (double)k);
 }
 
+// one selected pair's contribution to the 8 fit sums (k_fit_sums' operations and order)
+__device__ __forceinline__ void fit_add(double (&c)[8], double xs, double ys, double xt,
+                                        double yt, double px, double py) {
+    const double dxs = xs - px, dys = ys - py;
+    const double dxt = xt - px, dyt = yt - py;
+    c[0] = c[0] + dxs;
+    c[1] = c[1] + dys;
+    c[2] = c[2] + dxt;
+    c[3] = c[3] + dyt;
+    c[4] = c[4] + dxs * dxt;
+    c[5] = c[5] + dxs * dyt;
+    c[6] = c[6] + dys * dxt;
+    c[7] = c[7] + dys * dyt;
+}
+
+// inputs of the fit fused into the selection (k_select.hip): the rows' positions and
+// correspondences in work order, the pivot, and allow_reflection
+struct FitSrc {
+    const double *sx, *sy, *cx, *cy;
+    double px, py;
+    int on, allow_refl;
+};
+
+// The rigid fit from the 8 sums of the pivot-shifted pairs (s' = s - pivot, t' = t -
+// pivot) over the k selected rows: sum s'x, s'y, t'x, t'y, s'x t'x, s'x t'y, s'y t'x,
+// s'y t'y.  Closed-form 2-D Kabsch (ficp.py:89-110); writes T, the
+// centroids and H into *st.
+__device__ inline void fit_solve(const double c[8], double k, double px, double py,
+                                 int allow_refl, IterState *st) {
+    // centroids of the pivot-shifted pairs, then H = sum s't'^T - k cs' ct'^T
+    const double csx = c[0] / k, csy = c[1] / k, ctx = c[2] / k, cty = c[3] / k;
+    double H[4];
+    H[0] = c[4] - c[0] * ctx;
+    H[1] = c[5] - c[0] * cty;
+    H[2] = c[6] - c[1] * ctx;
+    H[3] = c[7] - c[1] * cty;
+    double R00, R01, R10, R11;
+    const double det = H[0] * H[3] - H[1] * H[2];
+    if (allow_refl && det < 0.0) {
+        // SVD path without the det fix: R = V U^T is the reflection Rot(a1) diag(1,-1)
+        const double F = H[0] - H[3], G = H[2] + H[1];
+        const double nrm = hypot(F, G);
+        const double cc = F / nrm, ss = G / nrm;
+        R00 = cc;
+        R01 = ss;
+        R10 = ss;
+        R11 = -cc;
+    } else {
+        const double A = H[0] + H[3], B = H[1] - H[2];
+        const double nrm = hypot(A, B);
+        double cc = 1.0, ss = 0.0;  // H = 0 (k = 1): the SVD path gives R = I
+        if (nrm > 0.0) {
+            cc = A / nrm;
+            ss = B / nrm;
+        }
+        R00 = cc;
+        R01 = -ss;
+        R10 = ss;
+        R11 = cc;
+    }
+    // centroids in world coordinates, t = ct - cs @ R^T (ficp.py:105)
+    const double wsx = csx + px, wsy = csy + py;
+    const double wtx = ctx + px, wty = cty + py;
+    st->T[0] = R00;
+    st->T[1] = R01;
+    st->T[2] = wtx - (wsx * R00 + wsy * R01);
+    st->T[3] = R10;
+    st->T[4] = R11;
+    st->T[5] = wty - (wsx * R10 + wsy * R11);
+    st->T[6] = 0.0;
+    st->T[7] = 0.0;
+    st->T[8] = 1.0;
+    st->csx = csx;
+    st->csy = csy;
+    st->ctx = ctx;
+    st->cty = cty;
+    for (int e = 0; e < 4; ++e) st->H[e] = H[e];
+}
+
 // Loop parameters and optional trace buffers of the device-resident loop.
 struct LoopCtl {
     const double *lams;    // [nstages] on the device
@@ -234,6 +313,15 @@ __device__ __forceinline__ void loop_step(IterState *st, const LoopCtl &c) {
 }
 
 // ----------------------------------------------------------------- launchers
+// device -> coherent pinned host copies + a completion flag the host polls (k_loop.hip)
+struct ReportSeg {
+    const void *src;  // device, 4-B aligned
+    void *dst;        // coherent pinned host memory
+    int words;        // 32-bit words (0: unused)
+};
+hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg &c, int *flag,
+                         hipStream_t s);
+
 // grid build (k_grid_nn.hip)
 hipError_t launch_minmax2(const double *x, const double *y, int64_t m, double *partials,
                           double *out4, hipStream_t s);
@@ -342,7 +430,8 @@ hipError_t launch_select_stats(void *tmp, int64_t n, unsigned *out3, hipStream_t
 hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, const double *r,
                          int64_t n, double lam, const double *lam_dev, unsigned long long *range,
                          int64_t range_parts, void *tmp, IterState *st, const int *skip,
-                         const LoopCtl *loop, int *host_flag, hipStream_t s);
+                         const LoopCtl *loop, int *host_flag, hipStream_t s,
+                         const FitSrc *fit = nullptr);
 
 // selection + fit + apply (k_select_fit.hip)
 int64_t frac_tmp_bytes(int64_t n);

@@ -79,21 +79,34 @@ __global__ __launch_bounds__(BT) void k_bs_count(const double *x, const double *
 }
 
 // counts[blk][b] -> exclusive prefix over blk (in place); totals[b].  One wave per
-// bucket, lane k holding slice k (nb1 <= 64): all loads in flight at once (a thread
-// walking the 64 slices serially took ~17 us at 1M points)
+// bucket, lane k holding slices k, k + 64, ... (nb1 <= 256): every load in flight at once
+// (a thread walking the slices serially took ~17 us at 1M points)
 __global__ __launch_bounds__(256) void k_bs_colscan(uint32_t *counts, BSortPlan p,
                                                     uint32_t *totals) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (b >= p.nbk) return;
-    const uint32_t v = lane < p.nb1 ? counts[(int64_t)lane * p.nbk + b] : 0u;
-    uint32_t x = v;
+    constexpr int R = 4;  // slices per lane: lane * R + j (contiguous per lane)
+    uint32_t v[R], tot = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int k = lane * R + j;
+        v[j] = k < p.nb1 ? counts[(int64_t)k * p.nbk + b] : 0u;
+        tot += v[j];
+    }
+    uint32_t x = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t t = __shfl_up(x, o, 64);
         if (lane >= o) x += t;
     }
-    if (lane < p.nb1) counts[(int64_t)lane * p.nbk + b] = x - v;
+    uint32_t run = x - tot;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int k = lane * R + j;
+        if (k < p.nb1) counts[(int64_t)k * p.nbk + b] = run;
+        run += v[j];
+    }
     if (lane == 63) totals[b] = x;
 }
 
@@ -286,8 +299,8 @@ __global__ __launch_bounds__(B4T) void k_bs_bucket(const TPt *rec, const uint32_
 
 }  // namespace
 
-// coarse buckets of ~256 points on average (at most 2^14), slices of >= 16K points (at
-// most 64): the per-slice bucket counts stay ~1 MB at 1M points
+// coarse buckets of ~256 points on average (at most 2^14), slices of >= 4K points (at
+// most 256, one per CU): the per-slice bucket counts are ~4 MB at 1M points
 BSortPlan bsort_plan(int64_t n, int64_t nkeys) {
     BSortPlan p{};
     p.nkeys = nkeys;
@@ -297,7 +310,7 @@ BSortPlan bsort_plan(int64_t n, int64_t nkeys) {
     while (want < BMAXB_LOG && (((int64_t)256) << want) < n) ++want;
     p.fs = std::max(0, kb - want);
     p.nbk = (int)std::max<int64_t>(1, (nkeys + (((int64_t)1) << p.fs) - 1) >> p.fs);
-    p.nb1 = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + 16383) / 16384));
+    p.nb1 = (int)std::min<int64_t>(256, std::max<int64_t>(1, (n + 4095) / 4096));
     p.per = (n + p.nb1 - 1) / p.nb1;
     return p;
 }

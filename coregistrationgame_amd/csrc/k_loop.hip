@@ -52,6 +52,28 @@ __global__ __launch_bounds__(256) void k_trace_idx(const IterState *st, const in
 
 }  // namespace
 
+// Copies up to three device segments into coherent pinned host memory and then raises
+// *flag (system scope, after a system fence): the host polls the flag instead of a
+// stream synchronisation plus one hipMemcpyAsync per segment (those cost 40-50 us of idle
+// device each at C3, profiles/r1sel trace).
+__global__ void k_report(ReportSeg a, ReportSeg b, ReportSeg c, int *flag) {
+    const ReportSeg sg[3] = {a, b, c};
+    for (int q = 0; q < 3; ++q) {
+        const uint32_t *src = (const uint32_t *)sg[q].src;
+        uint32_t *dst = (uint32_t *)sg[q].dst;
+        for (int w = threadIdx.x; w < sg[q].words; w += blockDim.x) dst[w] = src[w];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg &c, int *flag,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_report, dim3(1), dim3(256), 0, s, a, b, c, flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_loop_init(IterState *st, const LoopCtl &c, hipStream_t s) {
     hipLaunchKernelGGL(k_loop_init, dim3(1), dim3(64), 0, s, st, c);
     return hipGetLastError();

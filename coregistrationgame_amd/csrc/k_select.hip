@@ -99,9 +99,11 @@ struct SelWS {
     u64 *pfix;       // [HBMAX][NB] per-block fixed-point sums
     SelCtl *ctl;
     double *parts;   // [gather blocks]
+    double *fparts;  // [gather blocks][8] fit sums of the rows below the candidates
     u64 *ka, *kb;    // candidate ping-pong buffers (n each)
     uint32_t *oa, *ob;
     double *ra, *rb;
+    uint32_t *pa, *pb;  // candidate row (work position): the fused fit reads its pair
 };
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
@@ -113,33 +115,38 @@ inline int gather_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + GT *
 constexpr int HBMAX = 64;
 inline int hist_blocks(int64_t n) { return (int)std::min<int64_t>(HBMAX, std::max<int64_t>(1, (n + 8191) / 8192)); }
 
-SelWS carve(void *tmp, int64_t n) {
-    char *p = (char *)tmp;
-    SelWS w;
-    w.hcnt = (unsigned *)p;
-    p += align_up(NB * 4, 256);
-    w.hfix = (u64 *)p;
-    p += align_up(NB * 8, 256);
-    w.pcnt = (unsigned *)p;
-    p += align_up((int64_t)HBMAX * NB * 4, 256);
-    w.pfix = (u64 *)p;
-    p += align_up((int64_t)HBMAX * NB * 8, 256);
-    w.ctl = (SelCtl *)p;
-    p += 256;
-    w.parts = (double *)p;
-    p += align_up((int64_t)gather_blocks(n) * 8, 256);
+// workspace layout; carve() and sel_tmp_bytes() share it
+int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
+    char *p = p0;
+    auto take = [&](int64_t bytes) {
+        char *q = p;
+        p += align_up(bytes, 256);
+        return q;
+    };
     const int64_t nn = std::max<int64_t>(n, 1);
-    w.ka = (u64 *)p;
-    p += align_up(nn * 8, 256);
-    w.kb = (u64 *)p;
-    p += align_up(nn * 8, 256);
-    w.ra = (double *)p;
-    p += align_up(nn * 8, 256);
-    w.rb = (double *)p;
-    p += align_up(nn * 8, 256);
-    w.oa = (uint32_t *)p;
-    p += align_up(nn * 4, 256);
-    w.ob = (uint32_t *)p;
+    SelWS x;
+    x.hcnt = (unsigned *)take(NB * 4);
+    x.hfix = (u64 *)take(NB * 8);
+    x.pcnt = (unsigned *)take((int64_t)HBMAX * NB * 4);
+    x.pfix = (u64 *)take((int64_t)HBMAX * NB * 8);
+    x.ctl = (SelCtl *)take(256);
+    x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
+    x.fparts = (double *)take((int64_t)gather_blocks(n) * 64);
+    x.ka = (u64 *)take(nn * 8);
+    x.kb = (u64 *)take(nn * 8);
+    x.ra = (double *)take(nn * 8);
+    x.rb = (double *)take(nn * 8);
+    x.oa = (uint32_t *)take(nn * 4);
+    x.ob = (uint32_t *)take(nn * 4);
+    x.pa = (uint32_t *)take(nn * 4);
+    x.pb = (uint32_t *)take(nn * 4);
+    if (w) *w = x;
+    return (int64_t)(p - p0) + 256;
+}
+
+SelWS carve(void *tmp, int64_t n) {
+    SelWS w;
+    carve_bytes(n, &w, (char *)tmp);
     return w;
 }
 
@@ -203,6 +210,7 @@ __device__ __forceinline__ bool better(double f, long long k, double bf, long lo
 
 // ------------------------------------------------- block primitives (HT threads)
 struct Scr {
+    double f[8 * NWAVE];  // blk_sum8_add
     double d[NWAVE];
     long long l[NWAVE];
     u64 u[NWAVE];
@@ -221,6 +229,32 @@ __device__ __forceinline__ double blk_sum(double x, Scr &s) {
     for (int w = 0; w < NWAVE; ++w) t = t + s.d[w];
     __syncthreads();
     return t;
+}
+
+// acc8[e] += block sum of c[e] (thread 0 adds; fixed tree: wave butterfly, waves in order)
+__device__ __forceinline__ void blk_sum8_add(double (&c)[8], double *acc8, Scr &s) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c[e] = c[e] + __shfl_xor(c[e], o, 64);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s.f[8 * (threadIdx.x >> 6) + e] = c[e];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            double t = 0.0;
+            for (int w = 0; w < NWAVE; ++w) t = t + s.f[8 * w + e];
+            acc8[e] = acc8[e] + t;
+        }
+    }
+    __syncthreads();
+}
+
+// fit contribution of work row i
+__device__ __forceinline__ void fit_row(double (&c)[8], const FitSrc &fs, uint32_t i) {
+    fit_add(c, fs.sx[i], fs.sy[i], fs.cx[i], fs.cy[i], fs.px, fs.py);
 }
 
 __device__ __forceinline__ double blk_min_d(double x, Scr &s) {
@@ -716,9 +750,10 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
 
 __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_t *orig,
                                                    const double *r, int64_t n, SelWS w,
-                                                   const int *skip) {
+                                                   const int *skip, FitSrc fs) {
     if (skip && *skip) return;
     __shared__ double s_w[GT / 64];
+    __shared__ double s_f[8 * (GT / 64)];
     const u64 kmin = w.ctl->kmin;
     const int s = w.ctl->s, b0 = w.ctl->b0, b1 = w.ctl->b1;
     const int lane = threadIdx.x & 63;
@@ -734,6 +769,7 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
     }
     double acc = 0.0;
     unsigned inm = 0;   // bit q: row q is a candidate
+    unsigned bel = 0;   // bit q: row q lies below the candidates (selected)
     unsigned wtot = 0;  // candidates of the wave
     u64 masks[GI];
 #pragma unroll
@@ -742,8 +778,12 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
         bool in = false;
         if (i < n) {
             const int b = (int)((kk[q] - kmin) >> s);
-            if (b < b0) acc = acc + rr[q];
-            else if (b <= b1) in = true;
+            if (b < b0) {
+                acc = acc + rr[q];
+                bel |= 1u << q;
+            } else if (b <= b1) {
+                in = true;
+            }
         }
         masks[q] = __ballot(in);
         inm |= (in ? 1u : 0u) << q;
@@ -776,19 +816,54 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
                 w.ka[p] = kk[q];
                 w.oa[p] = orig ? orig[i] : (uint32_t)i;
                 w.ra[p] = rr[q];
+                w.pa[p] = (uint32_t)i;
             }
             pos += (unsigned)__popcll(masks[q]);
+        }
+    }
+    // fused fit: the 8 sums of the rows below the candidates (all of them are selected)
+    double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (fs.on) {
+#pragma unroll
+        for (int q0 = 0; q0 < GI; q0 += 4) {
+            double xs[4], ys[4], xt[4], yt[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = base + (int64_t)(q0 + u) * GT;
+                const bool on = (bel >> (q0 + u)) & 1u;
+                xs[u] = on ? fs.sx[i] : 0.0;
+                ys[u] = on ? fs.sy[i] : 0.0;
+                xt[u] = on ? fs.cx[i] : 0.0;
+                yt[u] = on ? fs.cy[i] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if ((bel >> (q0 + u)) & 1u) fit_add(c, xs[u], ys[u], xt[u], yt[u], fs.px, fs.py);
         }
     }
     // fixed tree: wave butterfly, then the waves in order
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc = acc + __shfl_xor(acc, o, 64);
     if (lane == 0) s_w[threadIdx.x >> 6] = acc;
+    if (fs.on) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) c[e] = c[e] + __shfl_xor(c[e], o, 64);
+        if (lane == 0)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s_f[8 * (threadIdx.x >> 6) + e] = c[e];
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int q = 0; q < GT / 64; ++q) t = t + s_w[q];
         w.parts[blockIdx.x] = t;
+    }
+    if (fs.on && threadIdx.x < 8) {
+        double t = 0.0;
+        for (int q = 0; q < GT / 64; ++q) t = t + s_f[8 * q + threadIdx.x];
+        w.fparts[8 * blockIdx.x + threadIdx.x] = t;
     }
 }
 
@@ -797,6 +872,7 @@ struct Cand {
     u64 *k;
     uint32_t *o;
     double *r;
+    uint32_t *p;  // work row (fused fit)
 };
 
 struct FinalIn {
@@ -805,6 +881,8 @@ struct FinalIn {
     double S0;      // exact (deterministic) sum of every row sorted before the candidates
     long long K0;   // number of those rows
     double U;
+    FitSrc fs;      // fused fit (fs.on): rows whose sums go into fsum
+    double *fsum;   // [8] in LDS, thread 0 accumulates in a fixed order
 };
 
 // composite order key of one candidate: ((key - kmin) << ob) | (orig - omin) when that fits
@@ -984,6 +1062,11 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
     }
     SELPROF(4);
     blk_argmin(bf, bk, scr);
+    if (in.fs.on && bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
+        double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (unsigned q = t; q < (unsigned)(bk - in.K0); q += HT) fit_row(cf, in.fs, src.p[pos[q]]);
+        blk_sum8_add(cf, in.fsum, scr);
+    }
     if (t == 0) {
         u64 tk = 0;
         uint32_t to = 0;
@@ -1093,6 +1176,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     const int L = e - 96;
     u128 acc = 0;
     long long below = 0;
+    double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (unsigned i = t; i < c; i += HT) {
         const u64 k = src.k[i];
         const uint32_t o = src.o[i];
@@ -1100,6 +1184,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
         const int b = (int)(cmp(k, o) >> sh);
         if (b < bmin) {
             below += 1;
+            if (in.fs.on) fit_row(cf, in.fs, src.p[i]);
             const u64 bitsr = (u64)__double_as_longlong(rv);
             const int ex = (int)((bitsr >> 52) & 0x7ff);
             u64 m = bitsr & 0xfffffffffffffULL;
@@ -1118,6 +1203,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
             dst.k[slot] = k;
             dst.o[slot] = o;
             dst.r[slot] = rv;
+            dst.p[slot] = src.p[i];
         }
     }
     // integer sums are order-free: reduce hi/lo with carries through LDS
@@ -1144,6 +1230,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     const long long nbelow = cnt[0];
     const unsigned nc = *rn;
     __syncthreads();
+    if (in.fs.on) blk_sum8_add(cf, in.fsum, scr);
     in.S0 = in.S0 + add;
     in.K0 += nbelow;
     in.U = U;
@@ -1198,13 +1285,14 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
             const unsigned i = t0 + t;
             const bool valid = i < c;
             u64 k = 0;
-            uint32_t o = 0;
+            uint32_t o = 0, pw = 0;
             double rv = 0.0;
             unsigned d = 0;
             if (valid) {
                 k = src.k[i];
                 o = src.o[i];
                 rv = src.r[i];
+                pw = src.p[i];
                 d = digit(k, o, p);
             }
             u64 m = __ballot(valid);
@@ -1233,6 +1321,7 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
                 dst.k[q] = k;
                 dst.o[q] = o;
                 dst.r[q] = rv;
+                dst.p[q] = pw;
             }
             __syncthreads();
             if (t < 256) gb[t] += tt[t];
@@ -1265,6 +1354,11 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
         carry = carry + all;
     }
     blk_argmin(bf, bk, scr);
+    if (in.fs.on && bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
+        double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (unsigned q = t; q < (unsigned)(bk - in.K0); q += HT) fit_row(cf, in.fs, src.p[q]);
+        blk_sum8_add(cf, in.fsum, scr);
+    }
     if (t == 0) {
         u64 tk = 0;
         uint32_t to = 0;
@@ -1282,7 +1376,7 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
 __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N, double lam,
                                                   const double *lam_dev, IterState *st,
                                                   const int *skip, LoopCtl lc, int fuse_loop,
-                                                  int *host_flag) {
+                                                  int *host_flag, FitSrc fs) {
     if (skip && *skip) {
         if (host_flag && threadIdx.x == 0)
             __hip_atomic_store(host_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1292,15 +1386,26 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     __shared__ __align__(16) unsigned char sm[SMEM];
     __shared__ Scr scr;
     __shared__ IterState s_st;  // thread 0's working copy of the state (one load, one store)
+    __shared__ double s_fit[8];  // fused fit sums (thread 0)
     const int t = threadIdx.x;
     SELPROF(0);
     if (t == 0) s_st = *st;
+    if (t < 8) s_fit[t] = 0.0;
     double a = 0.0;
     for (int p = t; p < nparts; p += HT) a = a + w.parts[p];  // fixed order per thread
     FinalIn in;
     in.N = N;
     in.lam = lam;
+    in.fs = fs;
+    in.fsum = s_fit;
     in.S0 = blk_sum(a, scr);
+    if (fs.on) {  // the gather blocks' sums of the rows below the candidates
+        double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int p = t; p < nparts; p += HT)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cf[e] = cf[e] + w.fparts[8 * p + e];
+        blk_sum8_add(cf, s_fit, scr);
+    }
     in.K0 = w.ctl->kbase;
     in.U = w.ctl->U;
     unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
@@ -1313,7 +1418,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
             publish(&s_st, in, INFINITY, 0x7fffffffffffffffLL, 0, 0);
         }
     } else {
-        Cand src{w.ka, w.oa, w.ra}, dst{w.kb, w.ob, w.rb};
+        Cand src{w.ka, w.oa, w.ra, w.pa}, dst{w.kb, w.ob, w.rb, w.pb};
         int lev = 0;
         bool stalled = false;
         while (c > (unsigned)CAP && lev < MAXLEV && !stalled) {
@@ -1333,6 +1438,9 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     SELPROF(5);
     if (t == 0) {
         if (fuse_loop) loop_step(&s_st, lc);
+        // fused fit: T of the next loop body from this selection (k_fit_sums' work)
+        if (fs.on && !s_st.no_fit && s_st.k > 0)
+            fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
         *st = s_st;
         if (host_flag)
             __hip_atomic_store(host_flag, s_st.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1359,13 +1467,7 @@ __global__ void k_sel_read_stats(SelWS w, unsigned *out) {
 
 }  // namespace
 
-int64_t sel_tmp_bytes(int64_t n) {
-    const int64_t nn = std::max<int64_t>(n, 1);
-    return align_up(NB * 4, 256) + align_up(NB * 8, 256) + align_up((int64_t)HBMAX * NB * 4, 256) +
-           align_up((int64_t)HBMAX * NB * 8, 256) + 256 +
-           align_up((int64_t)gather_blocks(n) * 8, 256) + 4 * align_up(nn * 8, 256) +
-           2 * align_up(nn * 4, 256) + 256;
-}
+int64_t sel_tmp_bytes(int64_t n) { return carve_bytes(n, nullptr, nullptr); }
 
 hipError_t launch_select_init(void *tmp, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(1024), 0, s, carve(tmp, n));
@@ -1380,7 +1482,7 @@ hipError_t launch_select_stats(void *tmp, int64_t n, unsigned *out3, hipStream_t
 hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, const double *r,
                          int64_t n, double lam, const double *lam_dev, unsigned long long *range,
                          int64_t range_parts, void *tmp, IterState *st, const int *skip,
-                         const LoopCtl *loop, int *host_flag, hipStream_t s) {
+                         const LoopCtl *loop, int *host_flag, hipStream_t s, const FitSrc *fit) {
     if (n <= 0) return hipSuccess;
     const SelWS w = carve(tmp, n);
     hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
@@ -1389,11 +1491,13 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev,
                        (const unsigned long long *)range, skip);
     const int gb = gather_blocks(n);
-    hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip);
+    FitSrc fs{};
+    if (fit && loop) fs = *fit;  // the fused fit needs the fused loop step (it runs after it)
+    hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs);
     LoopCtl lc{};
     if (loop) lc = *loop;
     hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, gb, n, lam, lam_dev, st, skip, lc,
-                       loop ? 1 : 0, host_flag);
+                       loop ? 1 : 0, host_flag, fs);
     return hipGetLastError();
 }
 

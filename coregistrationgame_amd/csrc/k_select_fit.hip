@@ -360,54 +360,7 @@ __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow
 #pragma unroll
     for (int e = 0; e < 8; ++e) c[e] = ((s[e] + s[8 + e]) + s[16 + e]) + s[24 + e];
     const double k = a.key ? (double)a.st->k : (double)a.n;
-    // centroids of the pivot-shifted pairs, then H = sum s't'^T - k cs' ct'^T
-    const double csx = c[0] / k, csy = c[1] / k, ctx = c[2] / k, cty = c[3] / k;
-    double H[4];
-    H[0] = c[4] - c[0] * ctx;
-    H[1] = c[5] - c[0] * cty;
-    H[2] = c[6] - c[1] * ctx;
-    H[3] = c[7] - c[1] * cty;
-    double R00, R01, R10, R11;
-    const double det = H[0] * H[3] - H[1] * H[2];
-    if (allow_refl && det < 0.0) {
-        // SVD path without the det fix: R = V U^T is the reflection Rot(a1) diag(1,-1)
-        const double F = H[0] - H[3], G = H[2] + H[1];
-        const double nrm = hypot(F, G);
-        const double cc = F / nrm, ss = G / nrm;
-        R00 = cc;
-        R01 = ss;
-        R10 = ss;
-        R11 = -cc;
-    } else {
-        const double A = H[0] + H[3], B = H[1] - H[2];
-        const double nrm = hypot(A, B);
-        double cc = 1.0, ss = 0.0;  // H = 0 (k = 1): the SVD path gives R = I
-        if (nrm > 0.0) {
-            cc = A / nrm;
-            ss = B / nrm;
-        }
-        R00 = cc;
-        R01 = -ss;
-        R10 = ss;
-        R11 = cc;
-    }
-    // centroids in world coordinates, t = ct - cs @ R^T (ficp.py:105)
-    const double wsx = csx + a.px, wsy = csy + a.py;
-    const double wtx = ctx + a.px, wty = cty + a.py;
-    st->T[0] = R00;
-    st->T[1] = R01;
-    st->T[2] = wtx - (wsx * R00 + wsy * R01);
-    st->T[3] = R10;
-    st->T[4] = R11;
-    st->T[5] = wty - (wsx * R10 + wsy * R11);
-    st->T[6] = 0.0;
-    st->T[7] = 0.0;
-    st->T[8] = 1.0;
-    st->csx = csx;
-    st->csy = csy;
-    st->ctx = ctx;
-    st->cty = cty;
-    for (int e = 0; e < 4; ++e) st->H[e] = H[e];
+    fit_solve(c, k, a.px, a.py, allow_refl, st);
 }
 
 // --------------------------------------------------------------- frmsd (public API)

@@ -238,6 +238,22 @@ def test_run_vs_oracle_100k(oracle):
     np.testing.assert_array_equal(bits(final[:, 2]), bits(p.source[:, 2]))
 
 
+@pytest.mark.parametrize("fuse_fit", ["0", "1"])
+def test_run_untraced_vs_oracle_100k(oracle, fuse_fit, monkeypatch):
+    """The production loop (no traces: the selection's last kernel runs the loop step; with
+    FICP_FUSE_FIT=1 it also runs the rigid fit) against the pinned oracle at 100k."""
+    from coregistrationgame_amd import FractionalICP, synth
+    monkeypatch.setenv("FICP_FUSE_FIT", fuse_fit)
+    p = synth.make_plot(100_000, 100_000, 0.8, seed=100_000, md=3)
+    icp = FractionalICP(p.source, p.target)
+    final = icp.run()
+    ofinal, otr = oracle.run(p.source, p.target, nthreads=16)
+    assert icp.last_stats["n_nn_calls"] == len(otr["k"])
+    assert icp.last_stats["k_last"] == otr["k"][-1]
+    np.testing.assert_allclose(final[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(bits(final[:, 2]), bits(p.source[:, 2]))
+
+
 def test_run_1M_properties():
     """C3 (1M x 1M, f=0.6, to convergence): the run undoes the synthetic misregistration
     (size-independent property) and a second run from its output is a fixed point."""

@@ -135,11 +135,12 @@ int main(int argc, char **argv) {
                            (const unsigned long long *)drange, (const int *)nullptr);
         CK(hipEventRecord(ev[2], 0));
         hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
-                           (const int *)nullptr);
+                           (const int *)nullptr, FitSrc{});
         CK(hipEventRecord(ev[3], 0));
         LoopCtl lc{};
         hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, 0, w, gb, n, lam,
-                           (const double *)nullptr, st, (const int *)nullptr, lc, 0, (int *)nullptr);
+                           (const double *)nullptr, st, (const int *)nullptr, lc, 0, (int *)nullptr,
+                           FitSrc{});
         CK(hipEventRecord(ev[4], 0));
         CK(hipEventSynchronize(ev[4]));
         for (int q = 0; q < 4; ++q) {

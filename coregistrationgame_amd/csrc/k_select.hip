@@ -95,8 +95,7 @@ struct SelCtl {
 struct SelWS {
     unsigned *hcnt;  // [NB] reduced counts (plain stores, k_sel_reduce)
     u64 *hfix;       // [NB] reduced fixed-point sums (plain stores, k_sel_reduce)
-    unsigned *pcnt;  // [HBMAX][NB] per-block counts of k_sel_hist (plain stores)
-    u64 *pfix;       // [HBMAX][NB] per-block fixed-point sums
+    u64 *ppk;        // [HBMAX][NB] per-block (count << shift) + fixed-point sum (plain stores)
     SelCtl *ctl;
     double *parts;   // [gather blocks]
     double *fparts;  // [gather blocks][8] fit sums of the rows below the candidates
@@ -112,8 +111,26 @@ inline int gather_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + GT *
 // stores and k_sel_reduce sums them.  Global atomics execute at the memory side at one
 // wave-instruction per ~50 ns per CU (MI355X_MICROARCH.md, global atomics), so flushing
 // 8192 buckets with atomics cost ~15 us and reading + resetting them from one CU ~25 us.
-constexpr int HBMAX = 64;
+constexpr int HBMAX = 128;
 inline int hist_blocks(int64_t n) { return (int)std::min<int64_t>(HBMAX, std::max<int64_t>(1, (n + 8191) / 8192)); }
+
+// One 64-bit LDS atomic per row: (1 << shift) + m, the count in the top cbits (a block
+// holds at most `per` rows) and the fixed-point value m < 2^fixb below it with room for
+// per of them.  fixb = 37 up to ~8K rows per block (relative truncation < 2^-35); the
+// bracket [fx, fx + c) stays rigorous for any fixb, a smaller one only widens it.
+struct HistPack {
+    int shift, fixb;
+};
+inline HistPack hist_pack(int64_t n) {
+    const int64_t nhb = hist_blocks(n);
+    const int64_t per = (std::max<int64_t>(n, 1) + nhb - 1) / nhb;
+    int cb = 1;
+    while ((((int64_t)1) << cb) <= per) ++cb;
+    HistPack h;
+    h.shift = 64 - cb;
+    h.fixb = std::min(37, h.shift - cb);
+    return h;
+}
 
 // workspace layout; carve() and sel_tmp_bytes() share it
 int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
@@ -127,8 +144,7 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     SelWS x;
     x.hcnt = (unsigned *)take(NB * 4);
     x.hfix = (u64 *)take(NB * 8);
-    x.pcnt = (unsigned *)take((int64_t)HBMAX * NB * 4);
-    x.pfix = (u64 *)take((int64_t)HBMAX * NB * 8);
+    x.ppk = (u64 *)take((int64_t)HBMAX * NB * 8);
     x.ctl = (SelCtl *)take(256);
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
     x.fparts = (double *)take((int64_t)gather_blocks(n) * 64);
@@ -175,7 +191,6 @@ __device__ __forceinline__ int bucket_exp(u64 kmin, u64 kmax, int s, int b) {
     if (rhi == 0.0) return 0;
     return ilogb(rhi) + 1;
 }
-constexpr int FIXB = 37;  // bits of one row's fixed-point value
 
 // Bounds work on h(k, S) = log2(S) - p log2(k), p = 2 lambda + 1, a monotone function of
 // FRMSD(k) = N^lambda k^-lambda sqrt(S / k) (no pow per bucket).  lg2 is exact in the
@@ -476,10 +491,9 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, Scr &s) {
 // block_range_store) and block 0 stores range[0..1] for the kernels that follow.
 __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *r, int64_t n,
                                                  u64 *range, int64_t nparts, SelWS w,
-                                                 const int *skip) {
+                                                 const int *skip, HistPack hp) {
     if (skip && *skip) return;
-    __shared__ unsigned sc[NB];
-    __shared__ u64 sf[NB];
+    __shared__ u64 sp[NB];
     __shared__ short se[NB];
     __shared__ u64 s_u[HHT / 64], s_v[HHT / 64];
     u64 kmin, kmax;
@@ -504,10 +518,10 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
     }
     const int s = sel_shift(kmin, kmax);
     for (int b = threadIdx.x; b < NB; b += HHT) {
-        sc[b] = 0u;
-        sf[b] = 0ULL;
+        sp[b] = 0ULL;
         se[b] = (short)bucket_exp(kmin, kmax, s, b);
     }
+    const u64 one = 1ULL << hp.shift;
     __syncthreads();
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * per, i1 = min(n, i0 + per);
@@ -526,45 +540,39 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
             if (i + (int64_t)u * HHT < i1) {
                 const int b = (int)((kk[u] - kmin) >> s);
                 const int e = se[b];
-                const u64 m = (e < 1024 && rv[u] < INFINITY) ? (u64)ldexp(rv[u], FIXB - e) : 0ULL;
-                atomicAdd(&sc[b], 1u);
-                atomicAdd(&sf[b], m);
+                const u64 m = (e < 1024 && rv[u] < INFINITY) ? (u64)ldexp(rv[u], hp.fixb - e) : 0ULL;
+                atomicAdd(&sp[b], one + m);
             }
         }
     }
     __syncthreads();
-    unsigned *pc = w.pcnt + (int64_t)blockIdx.x * NB;
-    u64 *pf = w.pfix + (int64_t)blockIdx.x * NB;
-    for (int b = threadIdx.x; b < NB; b += HHT) {
-        pc[b] = sc[b];
-        pf[b] = sf[b];
-    }
+    u64 *pp = w.ppk + (int64_t)blockIdx.x * NB;
+    for (int b = threadIdx.x; b < NB; b += HHT) pp[b] = sp[b];
 }
 
 // sum of the per-block histograms, one bucket per thread (integer sums: exact, order-free)
-__global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int *skip) {
+__global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int *skip,
+                                                   HistPack hp) {
     if (skip && *skip) return;
     const int b = blockIdx.x * 256 + threadIdx.x;
+    const u64 mask = (1ULL << hp.shift) - 1ULL;
     unsigned c = 0;
     u64 f = 0;
     int q = 0;
     for (; q + 8 <= nhb; q += 8) {
-        unsigned cv[8];
-        u64 fv[8];
+        u64 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = w.ppk[(int64_t)(q + u) * NB + b];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            cv[u] = w.pcnt[(int64_t)(q + u) * NB + b];
-            fv[u] = w.pfix[(int64_t)(q + u) * NB + b];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            c += cv[u];
-            f += fv[u];
+            c += (unsigned)(v[u] >> hp.shift);
+            f += v[u] & mask;
         }
     }
     for (; q < nhb; ++q) {
-        c += w.pcnt[(int64_t)q * NB + b];
-        f += w.pfix[(int64_t)q * NB + b];
+        const u64 v = w.ppk[(int64_t)q * NB + b];
+        c += (unsigned)(v >> hp.shift);
+        f += v & mask;
     }
     w.hcnt[b] = c;
     w.hfix[b] = f;
@@ -577,7 +585,7 @@ __global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int 
 constexpr int MAXACT = HT / (NB / HT);  // active chunks evaluated one bucket per lane
 __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double lam,
                                                    const double *lam_dev, const u64 *range,
-                                                   const int *skip) {
+                                                   const int *skip, int fixb) {
     if (skip && *skip) return;
     if (lam_dev) lam = *lam_dev;
     constexpr int PER = NB / HT;
@@ -593,14 +601,14 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     const u64 kmin = ~range[0], kmax = range[1];
     const int s = sel_shift(kmin, kmax);
     // per bucket: count, and the sum of its rows bracketed by the truncated fixed-point
-    // sum (each row loses < 1 unit): fx * 2^(e - FIXB) <= sum < (fx + c) * 2^(e - FIXB)
+    // sum (each row loses < 1 unit): fx * 2^(e - fixb) <= sum < (fx + c) * 2^(e - fixb)
     auto sums = [&](int b, unsigned c, u64 fx, double &lo, double &hi) {
         const int e = bucket_exp(kmin, kmax, s, b);
         if (e >= 1024) {
             lo = hi = c ? INFINITY : 0.0;
         } else {
-            lo = ldexp((double)fx, e - FIXB);
-            hi = ldexp((double)(fx + c), e - FIXB);
+            lo = ldexp((double)fx, e - fixb);
+            hi = ldexp((double)(fx + c), e - fixb);
         }
     };
     SELPROF(8);
@@ -1485,11 +1493,12 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
                          const LoopCtl *loop, int *host_flag, hipStream_t s, const FitSrc *fit) {
     if (n <= 0) return hipSuccess;
     const SelWS w = carve(tmp, n);
+    const HistPack hp = hist_pack(n);
     hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
-                       range_parts, w, skip);
-    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, s, w, hist_blocks(n), skip);
+                       range_parts, w, skip, hp);
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, s, w, hist_blocks(n), skip, hp);
     hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev,
-                       (const unsigned long long *)range, skip);
+                       (const unsigned long long *)range, skip, hp.fixb);
     const int gb = gather_blocks(n);
     FitSrc fs{};
     if (fit && loop) fs = *fit;  // the fused fit needs the fused loop step (it runs after it)

@@ -127,12 +127,13 @@ int main(int argc, char **argv) {
     for (int it = 0; it < reps; ++it) {
         CK(hipEventRecord(ev[0], 0));
         hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, 0, dkey, dr, n, drange,
-                           (int64_t)0, w, (const int *)nullptr);
+                           (int64_t)0, w, (const int *)nullptr, hist_pack(n));
         hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, 0, w, hist_blocks(n),
-                           (const int *)nullptr);
+                           (const int *)nullptr, hist_pack(n));
         CK(hipEventRecord(ev[1], 0));
         hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam, (const double *)nullptr,
-                           (const unsigned long long *)drange, (const int *)nullptr);
+                           (const unsigned long long *)drange, (const int *)nullptr,
+                           hist_pack(n).fixb);
         CK(hipEventRecord(ev[2], 0));
         hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
                            (const int *)nullptr, FitSrc{});

@@ -34,7 +34,6 @@ constexpr int BMAXB_LOG = 14;
 constexpr int B4T = 256;        // threads of k_bs_bucket
 constexpr int BCAP = 512;       // points ordered in LDS by one k_bs_bucket workgroup
 constexpr int BMAXF_LOG = 12;   // fine digits per bucket (max 4096)
-constexpr int BMAXF = 1 << BMAXF_LOG;
 
 __device__ __forceinline__ int bs_coord(double v, double v0, double inv_h, int g) {
     double f = (v - v0) * inv_h;

@@ -94,7 +94,8 @@ struct SelCtl {
 
 struct SelWS {
     unsigned *hcnt;  // [NB] reduced counts (plain stores, k_sel_reduce)
-    u64 *hfix;       // [NB] reduced fixed-point sums (plain stores, k_sel_reduce)
+    double *hlo;     // [NB] bracket of each bucket's sum of r (plain stores, k_sel_reduce)
+    double *hhi;
     u64 *ppk;        // [HBMAX][NB] per-block (count << shift) + fixed-point sum (plain stores)
     SelCtl *ctl;
     double *parts;   // [gather blocks]
@@ -143,7 +144,8 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     const int64_t nn = std::max<int64_t>(n, 1);
     SelWS x;
     x.hcnt = (unsigned *)take(NB * 4);
-    x.hfix = (u64 *)take(NB * 8);
+    x.hlo = (double *)take(NB * 8);
+    x.hhi = (double *)take(NB * 8);
     x.ppk = (u64 *)take((int64_t)HBMAX * NB * 8);
     x.ctl = (SelCtl *)take(256);
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
 
 // sum of the per-block histograms, one bucket per thread (integer sums: exact, order-free)
 __global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int *skip,
-                                                   HistPack hp) {
+                                                   HistPack hp, const u64 *range) {
     if (skip && *skip) return;
     const int b = blockIdx.x * 256 + threadIdx.x;
     const u64 mask = (1ULL << hp.shift) - 1ULL;
@@ -574,8 +576,21 @@ __global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int 
         c += (unsigned)(v >> hp.shift);
         f += v & mask;
     }
+    // the bucket's sum bracketed by the truncated fixed-point sum (each row loses < 1
+    // unit): f * 2^(e - fixb) <= sum < (f + c) * 2^(e - fixb); computed here, one bucket
+    // per thread, instead of 16 per thread in the one-workgroup bounds kernel
+    const u64 kmin = ~range[0], kmax = range[1];
+    const int e = bucket_exp(kmin, kmax, sel_shift(kmin, kmax), b);
+    double lo, hi;
+    if (e >= 1024) {
+        lo = hi = c ? INFINITY : 0.0;
+    } else {
+        lo = ldexp((double)f, e - hp.fixb);
+        hi = ldexp((double)(f + c), e - hp.fixb);
+    }
     w.hcnt[b] = c;
-    w.hfix[b] = f;
+    w.hlo[b] = lo;
+    w.hhi[b] = hi;
 }
 
 // Bounds of the FRMSD curve over the level-0 buckets (one workgroup).  Per-thread
@@ -590,45 +605,45 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     if (lam_dev) lam = *lam_dev;
     constexpr int PER = NB / HT;
     __shared__ Scr scr;
-    __shared__ unsigned lc[NB];
-    __shared__ u64 lf[NB];
+    __shared__ int s_act[MAXACT];
+    __shared__ int s_nact;
     __shared__ long long eC[MAXACT * PER];  // rows before bucket j of active chunk a
     __shared__ double eLo[MAXACT * PER];    // lower sum before it
     __shared__ double eHi[MAXACT * PER];    // upper sum through it
-    __shared__ int s_act[MAXACT];
-    __shared__ int s_nact;
     const int t = threadIdx.x;
     const u64 kmin = ~range[0], kmax = range[1];
     const int s = sel_shift(kmin, kmax);
-    // per bucket: count, and the sum of its rows bracketed by the truncated fixed-point
-    // sum (each row loses < 1 unit): fx * 2^(e - fixb) <= sum < (fx + c) * 2^(e - fixb)
-    auto sums = [&](int b, unsigned c, u64 fx, double &lo, double &hi) {
-        const int e = bucket_exp(kmin, kmax, s, b);
-        if (e >= 1024) {
-            lo = hi = c ? INFINITY : 0.0;
-        } else {
-            lo = ldexp((double)fx, e - fixb);
-            hi = ldexp((double)(fx + c), e - fixb);
-        }
-    };
     SELPROF(8);
     if (t == 0) s_nact = 0;
-    for (int j = 0; j < PER; ++j) {  // coalesced: bucket j * HT + t
-        const int b = j * HT + t;
-        lc[b] = w.hcnt[b];
-        lf[b] = w.hfix[b];
+    // this thread's PER consecutive buckets: counts and sum brackets (k_sel_reduce)
+    unsigned cc[PER];
+    double blo[PER], bhi[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j += 4) {
+        const uint4 c4 = *reinterpret_cast<const uint4 *>(w.hcnt + t * PER + j);
+        const double2 l0 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j);
+        const double2 l1 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j + 2);
+        const double2 h0 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j);
+        const double2 h1 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j + 2);
+        cc[j] = c4.x;
+        cc[j + 1] = c4.y;
+        cc[j + 2] = c4.z;
+        cc[j + 3] = c4.w;
+        blo[j] = l0.x;
+        blo[j + 1] = l0.y;
+        blo[j + 2] = l1.x;
+        blo[j + 3] = l1.y;
+        bhi[j] = h0.x;
+        bhi[j + 1] = h0.y;
+        bhi[j + 2] = h1.x;
+        bhi[j + 3] = h1.y;
     }
     __syncthreads();
     SELPROF(9);
     long long ct = 0;
     double tlo = 0.0, thi = 0.0;
-    unsigned cc[PER];
-    double blo[PER], bhi[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const int b = t * PER + j;
-        cc[j] = lc[b];
-        sums(b, cc[j], lf[b], blo[j], bhi[j]);
         ct += cc[j];
         tlo = tlo + blo[j];
         thi = thi + bhi[j];
@@ -679,14 +694,14 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
         // one bucket per lane: work item q = (active chunk q / PER, bucket q % PER)
         for (int q = t; q < nact * PER; q += HT) {
             const int b = s_act[q / PER] * PER + (q % PER);
-            const unsigned c = lc[b];
+            const unsigned c = w.hcnt[b];
             if (c) U = fmin(U, h_of(eC[q] + c, eHi[q], p) + kMarg);
         }
         U = fmin(blk_min_d(U, scr), U1);
         SELPROF(12);
         for (int q = t; q < nact * PER; q += HT) {
             const int b = s_act[q / PER] * PER + (q % PER);
-            const unsigned c = lc[b];
+            const unsigned c = w.hcnt[b];
             if (c) {
                 const double lb = block_lb(eC[q], c, eLo[q], lo_r(kmin + ((u64)b << s)), p);
                 if (!(lb > U) || !(p >= 1.0)) {
@@ -1496,7 +1511,8 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     const HistPack hp = hist_pack(n);
     hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
                        range_parts, w, skip, hp);
-    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, s, w, hist_blocks(n), skip, hp);
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, s, w, hist_blocks(n), skip, hp,
+                       (const unsigned long long *)range);
     hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev,
                        (const unsigned long long *)range, skip, hp.fixb);
     const int gb = gather_blocks(n);

@@ -32,8 +32,10 @@ constexpr int FI = 4;
 constexpr int FTILE = FB * FI;
 // k_fit_sums: 16 rows per thread, ~245 workgroups at 1M rows; each workgroup arrives once
 // at the finishing counter, and one word takes only ~88 atomics/us
-constexpr int FIT_I = 16;
-constexpr int FIT_TILE = FB * FIT_I;
+constexpr int FIT_I = 8;
+constexpr int FIT_B = 512;  // threads of k_fit_sums: 8 waves per CU for the streaming loads
+constexpr int FIT_W = FIT_B / 64;
+constexpr int FIT_TILE = FIT_B * FIT_I;
 
 __device__ __forceinline__ double block_sum_d(double v, double *s /*[256]*/) {
     // fixed-order tree: deterministic
@@ -256,7 +258,7 @@ __device__ __forceinline__ bool fit_threshold(const FitIn &a, unsigned long long
 __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow_refl,
                            IterState *st, double *s);
 
-__global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, unsigned *ctr,
+__global__ __launch_bounds__(FIT_B) void k_fit_sums(FitIn a, double *part, unsigned *ctr,
                                                  int allow_refl, IterState *st,
                                                  const int *skip) {
     if (skip && *skip) return;
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, unsigned
         double xs[4], ys[4], xt[4], yt[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int64_t i = i0 + (int64_t)(q0 + u) * FB;
+            const int64_t i = i0 + (int64_t)(q0 + u) * FIT_B;
             const bool in = i < a.n;
             kv[u] = (in && !all) ? a.key[i] : 0ULL;
             xs[u] = in ? a.sx[i] : 0.0;
@@ -286,7 +288,7 @@ __global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, unsigned
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int64_t i = i0 + (int64_t)(q0 + u) * FB;
+            const int64_t i = i0 + (int64_t)(q0 + u) * FIT_B;
             if (i < a.n) {
                 bool sel = all;
                 if (!all) {
@@ -320,7 +322,8 @@ __global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, unsigned
     __syncthreads();
     if (threadIdx.x < 8) {
         const int e = threadIdx.x;
-        const double t = ((s[e] + s[8 + e]) + s[16 + e]) + s[24 + e];
+        double t = s[e];
+        for (int w = 1; w < FIT_W; ++w) t = t + s[8 * w + e];
         __hip_atomic_store(&part[8 * blockIdx.x + e], t, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(FB) void k_fit_sums(FitIn a, double *part, unsigned
 __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow_refl,
                            IterState *st, double *s) {
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int b = threadIdx.x; b < nb; b += 256) {  // fixed order per thread
+    for (int b = threadIdx.x; b < nb; b += FIT_B) {  // fixed order per thread
         double v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -358,7 +361,11 @@ __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow
     __syncthreads();
     if (threadIdx.x != 0) return;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) c[e] = ((s[e] + s[8 + e]) + s[16 + e]) + s[24 + e];
+    for (int e = 0; e < 8; ++e) {
+        double t = s[e];
+        for (int w = 1; w < FIT_W; ++w) t = t + s[8 * w + e];
+        c[e] = t;
+    }
     const double k = a.key ? (double)a.st->k : (double)a.n;
     fit_solve(c, k, a.px, a.py, allow_refl, st);
 }
@@ -450,7 +457,7 @@ hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState
     const int nb = (int)std::max<int64_t>(1, (a.n + FIT_TILE - 1) / FIT_TILE);
     unsigned *ctr = (unsigned *)tmp;
     double *part = (double *)((char *)tmp + 256);
-    hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FB), 0, s, a, part, ctr, allow_reflection, st,
+    hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FIT_B), 0, s, a, part, ctr, allow_reflection, st,
                        skip);
     return hipGetLastError();
 }

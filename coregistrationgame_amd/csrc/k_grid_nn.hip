@@ -241,9 +241,31 @@ __device__ __forceinline__ void grid_nn(const GridView &g, const Stems &S, doubl
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
     const double mq = query_margin(g, qx, qy);
     if (!(b.d2 < INFINITY)) {
-        const int32_t *row = g.cell_start + (int64_t)cy * g.gx;
-        scan_pts<MD>(S, row[cx], row[cx + 1], qx, qy, qz, b);
-        for (int r = 1; !(b.d2 < INFINITY); ++r) {  // empty cell: grow square rings
+        // cold start (no previous match): the 3x3 cells around q as one batch -- a bound
+        // near the true distance (the own cell's stem alone was often 5-13 m away in 3-D,
+        // which widened every chord of the disk scan)
+        int p0[3], len[3];
+        const int xa = max(cx - 1, 0), xb = min(cx + 1, g.gx - 1);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            p0[r] = 0;
+            len[r] = 0;
+            const int yy = cy + r - 1;
+            if (yy < 0 || yy >= g.gy) continue;
+            const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
+            p0[r] = rw[xa];
+            len[r] = rw[xb + 1] - p0[r];
+        }
+        const int l01 = len[0] + len[1], tot = l01 + len[2];
+        for (int t = 0; t < tot; t += FICP_NN_UNROLL) {
+#pragma unroll
+            for (int u = 0; u < FICP_NN_UNROLL; ++u) {
+                const int q = min(t + u, tot - 1);
+                const int slot = q < len[0] ? p0[0] + q : (q < l01 ? p0[1] + (q - len[0]) : p0[2] + (q - l01));
+                eval_slot<MD>(S, slot, qx, qy, qz, b);
+            }
+        }
+        for (int r = 2; !(b.d2 < INFINITY); ++r) {  // empty 3x3 block: grow square rings
             const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
             if (xa < 0 && ya < 0 && xb >= g.gx && yb >= g.gy) break;  // empty layer
             const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);

@@ -187,11 +187,10 @@ __device__ __forceinline__ int bucket_exp(u64 kmin, u64 kmax, int s, int b) {
     const u64 wdt = ((u64)(b + 1) << s) - 1ULL;  // wraps to ~0 for the top bucket at s = 51
     const u64 khi = wdt > kmax - kmin ? kmax : kmin + wdt;
     if (!(khi >> 63)) return 0;
-    const double d = __longlong_as_double((long long)(khi & 0x7fffffffffffffffULL));
-    const double rhi = d * d * (1.0 + 1e-15);
-    if (!(rhi < INFINITY)) return 1024;
-    if (rhi == 0.0) return 0;
-    return ilogb(rhi) + 1;
+    // from the bits of d_hi alone (no fp64 work): d < 2^(ex - 1022) for biased exponent ex,
+    // so r = d^2 < 2^(2 ex - 2044); at most one bit looser than the exponent of d_hi^2
+    const int ex = (int)((khi >> 52) & 0x7ffULL);
+    return min(2 * ex - 2044, 1024);  // 1024: the bucket may hold inf / NaN or overflow
 }
 
 // Bounds work on h(k, S) = log2(S) - p log2(k), p = 2 lambda + 1, a monotone function of

@@ -8,10 +8,12 @@ out=tools/ab/build_$name
 mkdir -p $out
 cd coregistrationgame_amd/csrc
 SRCS=$(sed -n 's/^SRCS = //p' Makefile)
+pids=""
 for f in $SRCS; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -fno-fast-math \
     -I../../include "$@" -c $f -o ../../$out/${f%.hip}.o &
+  pids="$pids $!"
 done
-wait
+for p in $pids; do wait $p || { echo "compile failed"; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../../tools/ab/libficp_$name.so ../../$out/*.o
 echo tools/ab/libficp_$name.so

@@ -112,6 +112,47 @@ def test_grid_edge_layouts(ctx, oracle):
     ctx.set_nn_mode(_lib.NN_AUTO)
 
 
+def test_grid_clustered_layers(ctx, oracle):
+    """Clustered layers: thousands of stems (and trees) in one grid cell, so the grid
+    build's and the work order's bucket sort take their oversized-bucket path (global
+    scratch, k_bsort.hip); NN bit-exact vs brute force, and a whole run vs the oracle."""
+    from coregistrationgame_amd import FractionalICP, _lib
+    rng = np.random.default_rng(11)
+    clump = rng.normal(0.0, 0.2, (4000, 2)) + np.array([300.0, 300.0])
+    spread = rng.uniform(0, 1000, (3000, 2))
+    tgt = np.column_stack([np.vstack([clump, spread]), rng.uniform(5, 30, 7000)])
+    src = tgt[rng.permutation(7000)[:5000]].copy()
+    src[:, :2] += rng.normal(0.0, 0.05, (5000, 2))
+    ctx.set_nn_mode(_lib.NN_GRID)
+    ctx.set_target(tgt, 3)
+    idx, dist = ctx.nn(src)
+    oi, od, _ = oracle.nn(src, tgt, 3, "brute")
+    np.testing.assert_array_equal(idx, oi)
+    np.testing.assert_array_equal(bits(dist), bits(od))
+    ctx.set_nn_mode(_lib.NN_AUTO)
+    icp = FractionalICP(src, tgt, nn_mode="grid")
+    final = icp.run()
+    ofinal, otr = oracle.run(src, tgt, nthreads=16)
+    assert icp.last_stats["n_nn_calls"] == len(otr["k"])
+    np.testing.assert_allclose(final[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+
+
+def test_selection_selfcheck():
+    """tools/selcheck: the bucketed FRMSD selection (k_select.hip) against a CPU sort on
+    residual distributions that exercise its refinement and radix paths (zeros, all
+    equal, five distinct values, 20 decades)."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "tools" / "selcheck"
+    if not exe.exists():
+        pytest.skip("tools/selcheck not built (make -C coregistrationgame_amd/csrc selcheck)")
+    for args in (["200000", "3", "0", "3.0"], ["200000", "3", "0", "0.95"], ["100000", "3", "1", "3.0"],
+                 ["50000", "2", "2", "3.0"], ["100000", "2", "3", "0.95"], ["200000", "3", "5", "1.3"],
+                 ["3000", "3", "4", "3.0"]):
+        r = subprocess.run([str(exe)] + args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+
+
 # ------------------------------------------------------------------ sort / fraction
 def test_argsort_stable(ctx):
     rng = np.random.default_rng(3)

@@ -314,14 +314,20 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
     const GridView &g = c->gv;
     const int64_t nkeys = (int64_t)((g.gx + 7) / 8) * (int64_t)((g.gy + 7) / 8) * 64;
     if (bsort_supported(n, nkeys) && !getenv("FICP_WORK_RADIX")) {
-        CHK(c->bs_tmp.ensure(bsort_tmp_bytes(n, nkeys)));
+        // on the side stream, beside the grid build (both are a few hundred workgroups
+        // wide): it waits for c->ev_fork (the sources are ready, recorded by run_core
+        // before the grid build) and the main stream waits for it before the loop
+        CHK(c->bs_tmp2.ensure(bsort_tmp_bytes(n, nkeys)));
         const BSortGeom bg{g.x0, g.y0, g.inv_h, g.gx, g.gy, 1};
         BSortOut bo{};
         bo.wx = c->wx.as<double>();
         bo.wy = c->wy.as<double>();
         bo.wz = sz ? c->wz.as<double>() : nullptr;
         bo.worig = c->worig.as<uint32_t>();
-        HIPCHK(launch_bsort(sx, sy, sz, n, bg, nkeys, bo, c->bs_tmp.p, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+        HIPCHK(launch_bsort(sx, sy, sz, n, bg, nkeys, bo, c->bs_tmp2.p, c->stream2));
+        HIPCHK(hipEventRecord(c->ev_join, c->stream2));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
         return FICP_OK;
     }
     HIPCHK(launch_src_cellkey(sx, sy, n, c->gv, c->key.as<unsigned long long>(), c->stream));
@@ -380,6 +386,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     const double *wz = sz;
     const uint32_t *worig = nullptr;
     if (use_grid(c, n)) {
+        HIPCHK(hipEventRecord(c->ev_fork, c->stream));  // the sources are ready (work order)
         CHK(ensure_grid(c));
         CHK(build_work_order(c, sx, sy, sz, n));
         wx = c->wx.as<double>();
@@ -585,6 +592,9 @@ int ficp_create(int device, ficp_ctx **out) {
     c->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipHostMalloc((void **)&c->h_state, sizeof(IterState), hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -616,7 +626,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
                       &c->bp,     &c->dz2,        &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
-                      &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp};
+                      &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp, &c->bs_tmp2};
     for (DevBuf *b : bufs) b->release();
     batch_release(c->batch);
     c->batch = nullptr;
@@ -634,6 +644,9 @@ void ficp_destroy(ficp_ctx *c) {
     for (hipEvent_t &e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 

@@ -102,6 +102,8 @@ struct HostReport {
 struct ficp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;  // side stream: the work order beside the grid build
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int nn_mode = 0;
 
     // target (CHM layer)
@@ -125,7 +127,7 @@ struct ficp_ctx {
     DevBuf dz2; // dz^2 of each query's last match (warm start from (ccx, ccy, dz2))
     DevBuf lams, tr_k, tr_f, tr_l, tr_T, tr_idx;  // device loop: lambdas and traces
     DevBuf sel_tmp, sel_stats;  // bucketed fraction selection (k_select.hip)
-    DevBuf bs_tmp;              // two-level bucket sort scratch (k_bsort.hip)
+    DevBuf bs_tmp, bs_tmp2;     // two-level bucket sort scratch (k_bsort.hip): grid, work order
     unsigned sel_init_gen = 0;  // sel_tmp allocation whose atomic words are initialised
     unsigned fit_init_gen = 0;  // fit_tmp allocation whose arrival counter is zeroed
     unsigned sel_levels = 0, sel_radix = 0;  // selection statistics (cumulative)

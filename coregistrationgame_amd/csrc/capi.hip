@@ -170,6 +170,12 @@ bool use_select() {
 
 unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long long>(); }
 
+// FICP_NN_CERT=0: no certified match reuse (every warm query scans)
+static bool nn_cert_on() {
+    static const bool on = !getenv("FICP_NN_CERT") || atoi(getenv("FICP_NN_CERT")) != 0;
+    return on;
+}
+
 // NN of the device source (sx, sy, sz) against the target; optional pending transform.
 // With want_keys the sort inputs (key, range, r, matched XY) are produced too (and dist
 // is not).  warm: 0 = cold search, 1 = record the matched grid slots, 2 = also start
@@ -202,6 +208,15 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             CHK(c->dz2.ensure(n * 8));
             a.dz2 = c->dz2.as<double>();
             a.warm_c = warm == 2 ? 1 : 0;
+            // certified reuse of the match (nn_query_cert): the bound G and the match slot
+            if (nn_cert_on()) {
+                CHK(c->gap.ensure(n * 8));
+                CHK(c->bp.ensure(n * 4));
+                a.gap = c->gap.as<double>();
+                a.out_bp = c->bp.as<int32_t>();
+            }
+            static const int cblk = getenv("FICP_CERT_BLOCK") ? atoi(getenv("FICP_CERT_BLOCK")) : 8;
+            a.cert_block = cblk;
         }
         {
             KernelEvents ke(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
@@ -627,7 +642,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->ccx,    &c->ccy,        &c->rs,       &c->range,    &c->wx,
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
-                      &c->bp,     &c->dz2,        &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
+                      &c->bp,     &c->dz2,        &c->gap,      &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
                       &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp, &c->bs_tmp2};
     for (DevBuf *b : bufs) b->release();
     batch_release(c->batch);

@@ -111,6 +111,11 @@ struct NNArgs {
                                 // call (warm start; nullable, entries < 0 ignored)
     int32_t *out_bp;            // grid kernels: out: grid slot matched (nullable; may alias)
     double *dz2;                // grid kernels: out: dz^2 of the match (nullable; md 3)
+    double *gap;                // grid kernels: in/out: certified-reuse bound (nullable;
+                                // needs cx, cy, dz2, out_bp; k_grid_nn.hip nn_query_cert)
+    int cert_block;             // grid kernels, with gap and warm_c: > 0 packs each workgroup's
+                                // uncertified queries onto its first lanes, up to this many
+                                // lanes per query (1, 4 or 8) when they are few
     int warm_c;                 // grid kernels: start from the previous match held in
                                 // (cx, cy, dz2): its d^2 to the moved query, no record reload
     const int *apply_flag;      // T is applied only while *apply_flag != 0 (nullable: always)

@@ -433,6 +433,298 @@ __device__ __forceinline__ void finish(const NNArgs &a, const Stems &S, int64_t 
     kmax = max(kmax, k);
 }
 
+// ------------------------------------------------------- certified reuse of the match
+// Between ICP iterations a query moves by a small rigid step and its nearest stem rarely
+// changes.  A full scan here covers every stem within sqrt(cover2) of q, cover2 =
+// (d_match + pad)^2, and records G = a lower bound on the distance from q to every stem
+// other than the match: min(runner-up distance among the scanned stems, sqrt(cover2)
+// less the margins).  At the next call the query has moved by delta (XY only; z never
+// moves), so every other stem is at >= G - delta (triangle inequality) while the match
+// is at the recomputed d_new (the exact eval_slot operations on its stored XY and dz^2).
+// d_new + eps < G - delta - eps proves the match is still the unique nearest stem: the
+// result is the scan's, bit for bit, with no candidate read.  G then carries over as
+// G - delta - eps until a step fails the test and the query scans again.
+struct Best2 {
+    double d2;
+    int id, slot;  // slot -1: the bound is not (yet) a scanned stem
+    double s2;     // smallest d2 among scanned stems other than the best
+};
+
+template <int MD>
+__device__ __forceinline__ void eval2(const Stems &S, int p, double qx, double qy, double qz,
+                                      Best2 &b) {
+    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32, 0, 0);
+    const u32x3 hi = load_zid(S.r, p);
+    const double2 xy = __builtin_bit_cast(double2, lo);
+    const int id = (int)hi.z;
+    const double dx = qx - xy.x, dy = qy - xy.y;
+    double s = dx * dx;
+    s = s + dy * dy;
+    if (MD == 3) {
+        const double dz = qz - zid_z(hi);
+        s = s + dz * dz;
+    }
+    const bool take = (s < b.d2) | ((s == b.d2) & (id < b.id));
+    // the runner-up: a displaced best that was a scanned stem, or this stem unless it is
+    // the best itself (evaluated twice)
+    const double other = take ? (b.slot >= 0 ? b.d2 : INFINITY) : (p == b.slot ? INFINITY : s);
+    b.s2 = fmin(b.s2, other);
+    b.d2 = take ? s : b.d2;
+    b.id = take ? id : b.id;
+    b.slot = take ? p : b.slot;
+}
+
+template <int MD>
+__device__ __forceinline__ void scan2(const Stems &S, int p0, int p1, double qx, double qy,
+                                      double qz, Best2 &b) {
+    for (int p = p0; p < p1; p += FICP_NN_UNROLL) {
+#pragma unroll
+        for (int u = 0; u < FICP_NN_UNROLL; ++u) eval2<MD>(S, min(p + u, p1 - 1), qx, qy, qz, b);
+    }
+}
+
+// every stem within sqrt(cover2) of q (XY) evaluated: rows cy-1..cy+1 batched, then the
+// rows beyond while their band is within sqrt(cover2); chords from cover2
+template <int MD>
+__device__ __forceinline__ void cover_scan(const GridView &g, const Stems &S, double qx, double qy,
+                                           double qz, int cy, double mq, double cover2, Best2 &b) {
+    int p0[3], len[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        p0[r] = 0;
+        len[r] = 0;
+        const int yy = cy + r - 1;
+        if (yy < 0 || yy >= g.gy) continue;
+        const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
+        if (beyond(gy, cover2)) continue;
+        const double gy0 = fmax(gy, 0.0);
+        const double w = sqrt(fmax(cover2 - gy0 * gy0, 0.0)) + mq;
+        const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
+        const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
+        const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+        p0[r] = row[xl];
+        len[r] = row[xh + 1] - p0[r];
+    }
+    const int l01 = len[0] + len[1], tot = l01 + len[2];
+    for (int t = 0; t < tot; t += FICP_NN_UNROLL) {
+#pragma unroll
+        for (int u = 0; u < FICP_NN_UNROLL; ++u) {
+            const int q = min(t + u, tot - 1);
+            const int slot = q < len[0] ? p0[0] + q : (q < l01 ? p0[1] + (q - len[0]) : p0[2] + (q - l01));
+            eval2<MD>(S, slot, qx, qy, qz, b);
+        }
+    }
+    for (int k = 2;; ++k) {
+        bool any = false;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const int yy = side ? cy + k : cy - k;
+            if (yy < 0 || yy >= g.gy) continue;
+            const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
+            if (beyond(gy, cover2)) continue;
+            any = true;
+            const double gy0 = fmax(gy, 0.0);
+            const double w = sqrt(fmax(cover2 - gy0 * gy0, 0.0)) + mq;
+            const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
+            const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
+            const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+            scan2<MD>(S, row[xl], row[xh + 1], qx, qy, qz, b);
+        }
+        if (!any) break;
+    }
+}
+
+#ifndef FICP_CERT_PAD
+#define FICP_CERT_PAD 0.10  // full scans cover d_match + 0.1 cell sizes (best of 0.05-0.5 at C3)
+#endif
+
+#ifdef FICP_CERT_STATS
+__device__ unsigned long long g_cstat[4];
+__device__ unsigned g_cdone;
+#endif
+
+// rounding allowance of the certificate's distances (coordinates up to ~1e7 m: ulp ~2e-9 m)
+__device__ __forceinline__ double cert_eps(const GridView &g, double qx, double qy) {
+    return 2.0 * g.margin + 1e-12 * (fabs(qx) + fabs(qy)) + 1e-9;
+}
+
+// the stored match's exact d2 at the (moved) query: eval_slot's operations on (cx, cy, dz2)
+template <int MD>
+__device__ __forceinline__ double warm_d2(const NNArgs &a, int64_t i, double qx, double qy) {
+    const double dx = qx - a.cx[i], dy = qy - a.cy[i];
+    double d2 = dx * dx;
+    d2 = d2 + dy * dy;
+    if (MD == 3) d2 = d2 + a.dz2[i];
+    return d2;
+}
+
+// Step 1 (warm calls): apply T, then try the certificate.  Returns true when the stored
+// match stands (outputs written, no scan); false leaves the moved query for cert_scan.
+template <int MD>
+__device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, const Stems &S,
+                                         int64_t i, const double *T, unsigned long long &kmin_c,
+                                         unsigned long long &kmax) {
+    const double ox = a.sx[i], oy = a.sy[i];
+    double qx = ox, qy = oy;
+    if (T) {
+        apply_T(T, qx, qy);
+        a.sx[i] = qx;
+        a.sy[i] = qy;
+    }
+    const double eps = cert_eps(g, qx, qy);
+    const double d2w = warm_d2<MD>(a, i, qx, qy);
+    const double mx = qx - ox, my = qy - oy;
+    const double G = a.gap[i] - sqrt(mx * mx + my * my) - eps;
+#ifndef FICP_CERT_MUTANT
+#define FICP_CERT_MUTANT 0.0  // > 0 only in the mutation check of the tests (unsound)
+#endif
+    if (!(d2w < INFINITY && sqrt(d2w) + eps < G + FICP_CERT_MUTANT)) return false;
+    a.gap[i] = G;
+    if (a.idx) a.idx[i] = (int)load_zid(S.r, a.out_bp[i]).z;
+    const double d = sqrt(d2w);
+    const unsigned long long k = ordkey(d);
+    if (a.dist) a.dist[i] = d;
+    if (a.r) a.r[i] = d2w;
+    if (a.key) a.key[i] = k;
+    if (a.val) a.val[i] = (uint32_t)i;
+    kmin_c = max(kmin_c, ~k);
+    kmax = max(kmax, k);
+    return true;
+}
+
+// Step 2: the full scan of an uncertified query at its (already moved) position: warm
+// bound from the stored match (or the cold 3x3 start), every stem within d + pad
+// evaluated, the new bound G and the match slot stored, outputs written.
+template <int MD>
+__device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, const Stems &S,
+                                          int64_t i, bool warm, unsigned long long &kmin_c,
+                                          unsigned long long &kmax) {
+    const double qx = a.sx[i], qy = a.sy[i];
+    const double qz = (MD == 3) ? a.sz[i] : 0.0;
+    const double eps = cert_eps(g, qx, qy);
+    Best2 b{INFINITY, 0x7fffffff, -1, INFINITY};
+    if (warm) {
+        const double d2w = warm_d2<MD>(a, i, qx, qy);
+        if (d2w < INFINITY) b.d2 = d2w;  // a stem's exact d2, its slot unknown (-1)
+    }
+    const int cx = cell_coord(qx, g.x0, g.inv_h, g.gx);
+    const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
+    const double mq = query_margin(g, qx, qy);
+    if (!(b.d2 < INFINITY)) {  // cold start: the 3x3 cells around q, then rings
+        for (int yy = max(cy - 1, 0); yy <= min(cy + 1, g.gy - 1); ++yy) {
+            const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
+            scan2<MD>(S, rw[max(cx - 1, 0)], rw[min(cx + 1, g.gx - 1) + 1], qx, qy, qz, b);
+        }
+        for (int r = 2; !(b.d2 < INFINITY); ++r) {
+            const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
+            if (xa < 0 && ya < 0 && xb >= g.gx && yb >= g.gy) break;  // empty layer
+            const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);
+            for (int yy = max(ya, 0); yy <= min(yb, g.gy - 1); ++yy) {
+                const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
+                if (yy == ya || yy == yb) {
+                    scan2<MD>(S, rw[xlo], rw[xhi + 1], qx, qy, qz, b);
+                } else {
+                    if (xa >= 0) scan2<MD>(S, rw[xa], rw[xa + 1], qx, qy, qz, b);
+                    if (xb < g.gx) scan2<MD>(S, rw[xb], rw[xb + 1], qx, qy, qz, b);
+                }
+            }
+        }
+    }
+    double gnew = 0.0;
+    if (b.d2 < INFINITY) {
+        const double rc = sqrt(b.d2) + FICP_CERT_PAD * g.h;
+        cover_scan<MD>(g, S, qx, qy, qz, cy, mq, rc * rc, b);
+        gnew = fmin(sqrt(b.s2), rc - mq) - eps;
+    }
+    a.gap[i] = b.slot >= 0 ? gnew : 0.0;
+    a.out_bp[i] = b.slot;
+    finish(a, S, i, qz, Best{b.d2, b.id, max(b.slot, 0)}, kmin_c, kmax);
+}
+
+// cert_scan with the candidate stems of one query split over a group of GS lanes
+// (stride GS over each row segment), then a butterfly merge of the partial Best2s:
+// lowest (d2, id) among real stems wins; the runner-up takes every lane's s2 and each
+// losing lane's real best.  Lane lg == 0 writes the outputs.  Every lane of a group runs
+// the same row bounds (same query, same cover), so the group stays convergent.
+template <int MD, int GS>
+__device__ __forceinline__ void group_eval(const Stems &S, int p0, int p1, int lg, double qx,
+                                           double qy, double qz, Best2 &b) {
+    for (int p = p0 + lg; p < p1; p += GS) eval2<MD>(S, p, qx, qy, qz, b);
+}
+
+template <int MD, int GS>
+__device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView &g, const Stems &S,
+                                                int64_t i, int lg, unsigned long long &kmin_c,
+                                                unsigned long long &kmax) {
+    const double qx = a.sx[i], qy = a.sy[i];
+    const double qz = (MD == 3) ? a.sz[i] : 0.0;
+    const double eps = cert_eps(g, qx, qy);
+    const double d2w = warm_d2<MD>(a, i, qx, qy);
+    if (!(d2w < INFINITY)) {  // no finite previous match: the serial cold search
+        if (lg == 0) cert_scan<MD>(a, g, S, i, false, kmin_c, kmax);
+        return;
+    }
+    Best2 b{d2w, 0x7fffffff, -1, INFINITY};
+    const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
+    const double mq = query_margin(g, qx, qy);
+    const double rc = sqrt(d2w) + FICP_CERT_PAD * g.h;
+    const double cover2 = rc * rc;
+    for (int k = -1;; ++k) {  // rows cy-1, cy, cy+1, then cy -+ 2, 3, ... while in cover
+        bool any = false;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const int yy = k <= 1 ? (side ? -1 : cy + k) : (side ? cy + k : cy - k);
+            if (yy < 0 || yy >= g.gy) continue;
+            const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
+            if (beyond(gy, cover2)) continue;
+            any = true;
+            const double gy0 = fmax(gy, 0.0);
+            const double w = sqrt(fmax(cover2 - gy0 * gy0, 0.0)) + mq;
+            const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
+            const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
+            const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
+            group_eval<MD, GS>(S, row[xl], row[xh + 1], lg, qx, qy, qz, b);
+        }
+        if (!any && k >= 2) break;
+    }
+#pragma unroll
+    for (int off = GS / 2; off > 0; off >>= 1) {
+        const double od2 = __shfl_xor(b.d2, off, GS);
+        const int oid = __shfl_xor(b.id, off, GS);
+        const int oslot = __shfl_xor(b.slot, off, GS);
+        const double os2 = __shfl_xor(b.s2, off, GS);
+        const bool mine_real = b.slot >= 0, other_real = oslot >= 0;
+        const bool take = other_real &&
+                          (!mine_real || od2 < b.d2 || (od2 == b.d2 && oid < b.id));
+        const double lose = take ? (mine_real ? b.d2 : INFINITY) : (other_real ? od2 : INFINITY);
+        b.s2 = fmin(fmin(b.s2, os2), lose);
+        b.d2 = take ? od2 : b.d2;
+        b.id = take ? oid : b.id;
+        b.slot = take ? oslot : b.slot;
+    }
+    if (lg != 0) return;
+    double gnew = 0.0;
+    if (b.slot >= 0) gnew = fmin(sqrt(b.s2), rc - mq) - eps;
+    a.gap[i] = gnew;
+    finish(a, S, i, qz, Best{b.d2, b.id, max(b.slot, 0)}, kmin_c, kmax);
+}
+
+// one query of the certified path, both steps inline; returns true when certified
+template <int MD>
+__device__ __forceinline__ bool nn_query_cert(const NNArgs &a, const GridView &g, const Stems &S,
+                                              int64_t i, const double *T,
+                                              unsigned long long &kmin_c, unsigned long long &kmax) {
+    if (a.warm_c && cert_try<MD>(a, g, S, i, T, kmin_c, kmax)) return true;
+    if (!a.warm_c && T) {
+        double qx = a.sx[i], qy = a.sy[i];
+        apply_T(T, qx, qy);
+        a.sx[i] = qx;
+        a.sy[i] = qy;
+    }
+    cert_scan<MD>(a, g, S, i, a.warm_c != 0, kmin_c, kmax);
+    return false;
+}
+
 // Exact 1-NN of one query (lane): warm start from the stem it matched in the previous
 // call, then the disk-clipped row scan of grid_nn.
 template <int MD>
@@ -481,7 +773,70 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     unsigned long long kmin_c = 0, kmax = 0;
     const double *T = (APPLY && (!a.apply_flag || *a.apply_flag)) ? a.T : nullptr;
-    if (i < a.n) nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
+#ifdef FICP_CERT_STATS  // diagnostics only (tools/build_variant.sh certstats -DFICP_CERT_STATS)
+    bool certified = false;
+    if (i < a.n) {
+        if (a.gap) certified = nn_query_cert<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
+        else nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
+    }
+    {
+        const unsigned long long m = __ballot(certified), v = __ballot(i < a.n);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&g_cstat[0], (unsigned long long)__popcll(m));
+            atomicAdd(&g_cstat[1], (unsigned long long)__popcll(v));
+            atomicAdd(&g_cstat[2], (m == v && v) ? 1ULL : 0ULL);
+            atomicAdd(&g_cstat[3], 1ULL);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            const unsigned prev = atomicAdd(&g_cdone, 1u);
+            if (prev == gridDim.x - 1) {
+                __threadfence();
+                printf("CERT certified %llu / %llu lanes, %llu / %llu waves all certified\n",
+                       atomicAdd(&g_cstat[0], 0ULL), atomicAdd(&g_cstat[1], 0ULL),
+                       atomicAdd(&g_cstat[2], 0ULL), atomicAdd(&g_cstat[3], 0ULL));
+                for (int q = 0; q < 4; ++q) atomicExch(&g_cstat[q], 0ULL);
+                atomicExch(&g_cdone, 0u);
+            }
+        }
+    }
+#else
+    if (a.cert_block && a.gap && a.warm_c) {
+        // block-compacted: certificates first, then the workgroup's uncertified queries
+        // packed densely onto its lanes (GS lanes per query when there are few of them)
+        __shared__ int s_list[256];
+        __shared__ int s_n;
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        const Stems S = stems_of(g.pts, g.m);
+        const bool pend = i < a.n && !cert_try<MD>(a, g, S, i, T, kmin_c, kmax);
+        const unsigned long long m = __ballot(pend);
+        const int lane = threadIdx.x & 63;
+        int base = 0;
+        if (lane == 0 && m) base = atomicAdd(&s_n, __popcll(m));
+        base = __shfl(base, 0);
+        if (pend) s_list[base + __popcll(m & ((1ULL << lane) - 1))] = (int)(i & 255);
+        __syncthreads();
+        const int tot = s_n;
+        const int64_t i0 = i - threadIdx.x;
+        const int t = threadIdx.x;
+        if (a.cert_block >= 16 && tot <= 16) {
+            if (t < tot * 16) cert_scan_group<MD, 16>(a, g, S, i0 + s_list[t >> 4], t & 15, kmin_c, kmax);
+        } else if (a.cert_block >= 8 && tot <= 32) {
+            if (t < tot * 8) cert_scan_group<MD, 8>(a, g, S, i0 + s_list[t >> 3], t & 7, kmin_c, kmax);
+        } else if (a.cert_block >= 4 && tot <= 64) {
+            if (t < tot * 4) cert_scan_group<MD, 4>(a, g, S, i0 + s_list[t >> 2], t & 3, kmin_c, kmax);
+        } else if (a.cert_block >= 2 && tot <= 128) {
+            if (t < tot * 2) cert_scan_group<MD, 2>(a, g, S, i0 + s_list[t >> 1], t & 1, kmin_c, kmax);
+        } else if (t < tot) {
+            cert_scan<MD>(a, g, S, i0 + s_list[threadIdx.x], true, kmin_c, kmax);
+        }
+    } else if (i < a.n) {
+        if (a.gap) nn_query_cert<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
+        else nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
+    }
+#endif
     if (a.range) block_range_store(a.range, true, kmin_c, kmax);
 }
 

@@ -295,6 +295,42 @@ def test_run_untraced_vs_oracle_100k(oracle, fuse_fit, monkeypatch):
     np.testing.assert_array_equal(bits(final[:, 2]), bits(p.source[:, 2]))
 
 
+@pytest.mark.parametrize("md", [2, 3])
+def test_run_certified_reuse_near_ties(oracle, md):
+    """Certified match reuse (k_grid_nn.hip cert_try / cert_scan_group) on a layout built
+    for near-ties: stems on a 2 m lattice (a tenth of them duplicated), sources at lattice
+    midpoints and points +-1 mm from them, under a small rigid misregistration.  Every NN
+    call's idx must equal the oracle's, call by call."""
+    from coregistrationgame_amd import FractionalICP
+    rng = np.random.default_rng(77 + md)
+    gx, gy = np.meshgrid(np.arange(160) * 2.0, np.arange(160) * 2.0)
+    stems = np.c_[gx.ravel() + 5.0e5, gy.ravel() + 6.5e6]
+    stems = np.r_[stems, stems[rng.choice(len(stems), len(stems) // 10, replace=False)]]
+    tgt = np.c_[stems, rng.uniform(10, 30, len(stems)).round(1)]
+    pick = rng.choice(len(gx.ravel()), 20_000, replace=False)
+    src = tgt[pick].copy()
+    src[:5000, :2] += 1.0                                   # midpoints of four stems
+    src[5000:10000, 0] += 1.0 + rng.choice([-1e-3, 1e-3], 5000)   # near-midpoint of two
+    src[10000:, :2] += rng.normal(0, 0.2, (10000, 2))
+    th = 0.004
+    R = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+    c0 = src[:, :2].mean(0)
+    src[:, :2] = (src[:, :2] - c0) @ R.T + c0 + [0.7, -0.4]
+    if md == 2:
+        src, tgt = src[:, :2].copy(), tgt[:, :2].copy()
+    icp = FractionalICP(src, tgt, nn_mode="grid")
+    final = icp.run(trace=True, trace_idx=True)
+    tr = icp.last_stats
+    ofinal, otr = oracle.run(src, tgt, nthreads=16, trace_idx=True)
+    ncall = min(len(tr["k"]), len(otr["k"]))
+    same = np.flatnonzero(tr["k"][:ncall] != otr["k"][:ncall])
+    upto = int(same[0]) + 1 if len(same) else ncall  # trajectories agree through here
+    assert upto >= 3
+    np.testing.assert_array_equal(tr["idx"][:upto], otr["idx"][:upto])
+    if not len(same):
+        np.testing.assert_allclose(final[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+
+
 def test_run_1M_properties():
     """C3 (1M x 1M, f=0.6, to convergence): the run undoes the synthetic misregistration
     (size-independent property) and a second run from its output is a fixed point."""

@@ -535,7 +535,7 @@ __device__ __forceinline__ void cover_scan(const GridView &g, const Stems &S, do
 }
 
 #ifndef FICP_CERT_PAD
-#define FICP_CERT_PAD 0.10  // full scans cover d_match + 0.1 cell sizes (best of 0.05-0.5 at C3)
+#define FICP_CERT_PAD 0.25  // scans cover d_match + 0.25 cell sizes (0.1-0.4 within 1 % at C3)
 #endif
 
 #ifdef FICP_CERT_STATS

@@ -61,6 +61,10 @@ def main(tag, prefix="r1"):
                 "an estimate: raw fetch + write is the lower bound",
     }
     (dst / f"{prefix}_pmc_c3_nn.json").write_text(json.dumps(nn_json, indent=1))
+    # the bench line read the previous traffic file: carry this run's PMC bytes into it
+    bj = json.loads((dst / f"{prefix}_c3_bench.json").read_text())
+    bj["roofline"]["traffic"] = nn_json["hbm_bytes_per_launch"]
+    (dst / f"{prefix}_c3_bench.json").write_text(json.dumps(bj) + "\n")
     print(json.dumps({k: summ[k]["active_avg_us"] for k in summ if k.startswith("k_nn")}))
     print("hbm bytes per NN launch", nn_json["hbm_bytes_per_launch"])
 

@@ -77,36 +77,35 @@ __global__ __launch_bounds__(BT) void k_bs_count(const double *x, const double *
     for (int b = threadIdx.x; b < p.nbk; b += BT) c[b] = h[b];
 }
 
-// counts[blk][b] -> exclusive prefix over blk (in place); totals[b].  One wave per
-// bucket, lane k holding slices k, k + 64, ... (nb1 <= 256): every load in flight at once
-// (a thread walking the slices serially took ~17 us at 1M points)
-__global__ __launch_bounds__(256) void k_bs_colscan(uint32_t *counts, BSortPlan p,
-                                                    uint32_t *totals) {
-    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (b >= p.nbk) return;
-    constexpr int R = 4;  // slices per lane: lane * R + j (contiguous per lane)
+// counts[blk][b] -> exclusive prefix over blk (in place); totals[b].  One workgroup per
+// 64 buckets: thread (c, l) holds slices 16c..16c+15 of bucket l, so every load and store
+// is a coalesced 256-B row segment (a wave per bucket with lanes over slices read 4 B per
+// 16 KB stride: 17 us at 1M points), and the 16 chunk sums are scanned through LDS.
+__global__ __launch_bounds__(1024) void k_bs_colscan(uint32_t *counts, BSortPlan p,
+                                                     uint32_t *totals) {
+    __shared__ uint32_t s_c[16][64];
+    const int l = threadIdx.x & 63, c = threadIdx.x >> 6;
+    const int b = blockIdx.x * 64 + l;
+    const bool ok = b < p.nbk;
+    constexpr int R = 16;  // slices per thread (nb1 <= 256)
     uint32_t v[R], tot = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const int k = lane * R + j;
-        v[j] = k < p.nb1 ? counts[(int64_t)k * p.nbk + b] : 0u;
+        const int k = c * R + j;
+        v[j] = (ok && k < p.nb1) ? counts[(int64_t)k * p.nbk + b] : 0u;
         tot += v[j];
     }
-    uint32_t x = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(x, o, 64);
-        if (lane >= o) x += t;
-    }
-    uint32_t run = x - tot;
+    s_c[c][l] = tot;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int q = 0; q < c; ++q) run += s_c[q][l];
+    if (c == 15 && ok) totals[b] = run + tot;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const int k = lane * R + j;
-        if (k < p.nb1) counts[(int64_t)k * p.nbk + b] = run;
+        const int k = c * R + j;
+        if (ok && k < p.nb1) counts[(int64_t)k * p.nbk + b] = run;
         run += v[j];
     }
-    if (lane == 63) totals[b] = x;
 }
 
 __global__ __launch_bounds__(BT) void k_bs_scatter(const double *x, const double *y,
@@ -351,7 +350,7 @@ hipError_t launch_bsort(const double *x, const double *y, const double *z, int64
     q += al(n * 8);
     uint32_t *gpos = (uint32_t *)q;
     hipLaunchKernelGGL(k_bs_count, dim3(p.nb1), dim3(BT), 0, s, x, y, n, g, p, counts);
-    hipLaunchKernelGGL(k_bs_colscan, dim3((p.nbk + 3) / 4), dim3(256), 0, s, counts, p, totals);
+    hipLaunchKernelGGL(k_bs_colscan, dim3((p.nbk + 63) / 64), dim3(1024), 0, s, counts, p, totals);
     hipLaunchKernelGGL(k_bs_scatter, dim3(p.nb1), dim3(BT), 0, s, x, y, z, n, g, p, counts,
                        totals, base, rec);
     const size_t lds = BCAP * (sizeof(TPt) + 8 + 2) + (size_t)2 * 4 * (1 << p.fs);

@@ -365,6 +365,7 @@ struct BSortPlan {
     int fs;         // fine bits (key & ((1 << fs) - 1))
     int nbk;        // coarse buckets (key >> fs)
     int nb1;        // slices of the count / scatter kernels
+    int bcap;       // points ordered in LDS by one k_bs_bucket workgroup
     int64_t per;    // points per slice
     int64_t nkeys;
 };

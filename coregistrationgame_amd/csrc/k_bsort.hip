@@ -32,7 +32,6 @@ constexpr int BT = 1024;        // threads of k_bs_count / k_bs_scatter
 constexpr int BMAXB = 16384;    // coarse buckets (max)
 constexpr int BMAXB_LOG = 14;
 constexpr int B4T = 256;        // threads of k_bs_bucket
-constexpr int BCAP = 512;       // points ordered in LDS by one k_bs_bucket workgroup
 constexpr int BMAXF_LOG = 12;   // fine digits per bucket (max 4096)
 
 __device__ __forceinline__ int bs_coord(double v, double v0, double inv_h, int g) {
@@ -205,11 +204,11 @@ __global__ __launch_bounds__(B4T) void k_bs_bucket(const TPt *rec, const uint32_
     // workgroups share a CU
     extern __shared__ __align__(32) unsigned char dyn[];
     const int nf = 1 << p.fs;
-    TPt *lrec = (TPt *)dyn;                                   // [BCAP]
-    uint64_t *lcomp = (uint64_t *)(dyn + BCAP * sizeof(TPt));  // [BCAP] (fine << 32 | index)
-    uint32_t *fc = (uint32_t *)(lcomp + BCAP);                // [nf] counts, then bin starts
+    TPt *lrec = (TPt *)dyn;                                     // [bcap]
+    uint64_t *lcomp = (uint64_t *)(dyn + p.bcap * sizeof(TPt));  // [bcap] (fine << 32 | index)
+    uint32_t *fc = (uint32_t *)(lcomp + p.bcap);                // [nf] counts, then bin starts
     uint32_t *ff = fc + nf;                                   // [nf] fill counters
-    uint16_t *lsrc = (uint16_t *)(ff + nf);                   // [BCAP] bin slot -> record
+    uint16_t *lsrc = (uint16_t *)(ff + nf);                     // [bcap] bin slot -> record
     __shared__ uint32_t s_w[B4T / 64];
     const int b = blockIdx.x;
     const uint32_t lo = base[b], hi = base[b + 1], cnt = hi - lo;
@@ -219,7 +218,7 @@ __global__ __launch_bounds__(B4T) void k_bs_bucket(const TPt *rec, const uint32_
         ff[f] = 0u;
     }
     __syncthreads();
-    const bool small = cnt <= (uint32_t)BCAP;
+    const bool small = cnt <= (uint32_t)p.bcap;
     for (uint32_t e = threadIdx.x; e < cnt; e += B4T) {
         const TPt t = rec[lo + e];
         if (small) lrec[e] = t;
@@ -304,11 +303,15 @@ BSortPlan bsort_plan(int64_t n, int64_t nkeys) {
     p.nkeys = nkeys;
     int kb = 0;
     while (kb < 40 && (((int64_t)1) << kb) < nkeys) ++kb;
+    // FICP_BS_BPTS / FICP_BS_SLICE: bucket and slice sizes (A/B runs)
+    static const int64_t bpts = getenv("FICP_BS_BPTS") ? atoll(getenv("FICP_BS_BPTS")) : 256;
+    static const int64_t slice = getenv("FICP_BS_SLICE") ? atoll(getenv("FICP_BS_SLICE")) : 4096;
     int want = 0;
-    while (want < BMAXB_LOG && (((int64_t)256) << want) < n) ++want;
+    while (want < BMAXB_LOG && (bpts << want) < n) ++want;
     p.fs = std::max(0, kb - want);
     p.nbk = (int)std::max<int64_t>(1, (nkeys + (((int64_t)1) << p.fs) - 1) >> p.fs);
-    p.nb1 = (int)std::min<int64_t>(256, std::max<int64_t>(1, (n + 4095) / 4096));
+    p.nb1 = (int)std::min<int64_t>(256, std::max<int64_t>(1, (n + slice - 1) / slice));
+    p.bcap = (int)std::min<int64_t>(4096, 2 * bpts);
     p.per = (n + p.nb1 - 1) / p.nb1;
     return p;
 }
@@ -353,7 +356,7 @@ hipError_t launch_bsort(const double *x, const double *y, const double *z, int64
     hipLaunchKernelGGL(k_bs_colscan, dim3((p.nbk + 63) / 64), dim3(1024), 0, s, counts, p, totals);
     hipLaunchKernelGGL(k_bs_scatter, dim3(p.nb1), dim3(BT), 0, s, x, y, z, n, g, p, counts,
                        totals, base, rec);
-    const size_t lds = BCAP * (sizeof(TPt) + 8 + 2) + (size_t)2 * 4 * (1 << p.fs);
+    const size_t lds = (size_t)p.bcap * (sizeof(TPt) + 8 + 2) + (size_t)2 * 4 * (1 << p.fs);
     hipLaunchKernelGGL(k_bs_bucket, dim3(p.nbk), dim3(B4T), lds, s, rec, base, g, p, o, gcomp, gpos);
     return hipGetLastError();
 }

@@ -805,7 +805,8 @@ int ficp_frmsd(ficp_ctx *c, const double *src, int64_t lds, const double *corr, 
     CHK(c->stage2.ensure(64));
     HIPCHK(launch_sum_sq_diff(c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(),
                               c->cx.as<double>(), c->cy.as<double>(), c->cz.as<double>(), k, md,
-                              (char *)c->fit_tmp.p + 256, c->stage2.as<double>(), c->stream));
+                              (char *)c->fit_tmp.p + fit_scratch_offset(), c->stage2.as<double>(),
+                              c->stream));
     double S = 0.0;
     HIPCHK(hipMemcpyAsync(&S, c->stage2.p, 8, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));

@@ -481,6 +481,8 @@ struct FitIn {
     const IterState *st;
 };
 int64_t fit_tmp_bytes(int64_t n);
+// byte offset past the fit's arrival counters: free scratch for other reductions
+int64_t fit_scratch_offset();
 // zero the scratch's arrival counter: once per (re)allocation of the scratch
 hipError_t launch_fit_init(void *tmp, hipStream_t s);
 hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,

@@ -30,10 +30,20 @@ namespace {
 constexpr int FB = 256;
 constexpr int FI = 4;
 constexpr int FTILE = FB * FI;
-// k_fit_sums: 16 rows per thread, ~245 workgroups at 1M rows; each workgroup arrives once
-// at the finishing counter, and one word takes only ~88 atomics/us
-constexpr int FIT_I = 8;
-constexpr int FIT_B = 512;  // threads of k_fit_sums: 8 waves per CU for the streaming loads
+// k_fit_sums: FIT_I rows per thread.  Each workgroup arrives once at one of 8 group
+// counters (blockIdx % 8: one per XCD under round-robin dispatch) and the last of each
+// group at the top counter: one word takes only ~88 atomics/us, so ~245 arrivals on one
+// word serialised ~2.8 us
+#ifndef FICP_FIT_I
+#define FICP_FIT_I 8
+#endif
+#ifndef FICP_FIT_B
+#define FICP_FIT_B 512
+#endif
+constexpr int FIT_I = FICP_FIT_I;
+constexpr int FIT_B = FICP_FIT_B;  // threads of k_fit_sums
+constexpr int FIT_CTR = 64;        // counter stride (u32 words: 256 B apart)
+constexpr int FIT_PART = 4096;     // byte offset of the partial sums in the scratch
 constexpr int FIT_W = FIT_B / 64;
 constexpr int FIT_TILE = FIT_B * FIT_I;
 
@@ -329,10 +339,16 @@ __global__ __launch_bounds__(FIT_B) void k_fit_sums(FitIn a, double *part, unsig
     }
     if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prev =
-            __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == gridDim.x - 1;
-        if (s_last) __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned grp = blockIdx.x & 7u, ng = min(gridDim.x, 8u);
+        const unsigned gsz = (gridDim.x - grp + 7u) / 8u;  // workgroups of this group
+        unsigned *gc = ctr + FIT_CTR * (1 + grp);
+        bool last = false;
+        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
+            __hip_atomic_exchange(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+            if (last) __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
@@ -445,18 +461,20 @@ hipError_t launch_fraction(const double *rs, int64_t n, int64_t n_src, double la
 // launch_fit_init), then 8 partial sums per block
 int64_t fit_tmp_bytes(int64_t n) {
     const int64_t nb = (n + FTILE - 1) / FTILE + 1;
-    return 256 + align_up(nb * 8 * 8, 256);
+    return FIT_PART + align_up(nb * 8 * 8, 256);
 }
 
+int64_t fit_scratch_offset() { return FIT_PART; }
+
 hipError_t launch_fit_init(void *tmp, hipStream_t s) {
-    return launch_atomic_zero32((uint32_t *)tmp, 1, s);
+    return launch_atomic_zero32((uint32_t *)tmp, FIT_PART / 4, s);
 }
 
 hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,
                       const int *skip, hipStream_t s) {
     const int nb = (int)std::max<int64_t>(1, (a.n + FIT_TILE - 1) / FIT_TILE);
     unsigned *ctr = (unsigned *)tmp;
-    double *part = (double *)((char *)tmp + 256);
+    double *part = (double *)((char *)tmp + FIT_PART);
     hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FIT_B), 0, s, a, part, ctr, allow_reflection, st,
                        skip);
     return hipGetLastError();

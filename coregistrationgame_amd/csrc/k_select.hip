@@ -551,16 +551,28 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
     for (int b = threadIdx.x; b < NB; b += HHT) pp[b] = sp[b];
 }
 
-// sum of the per-block histograms, one bucket per thread (integer sums: exact, order-free)
-__global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int *skip,
-                                                   HistPack hp, const u64 *range) {
+// sum of the per-block histograms (integer sums: exact, order-free).  RG thread groups
+// per bucket each add a quarter of the copies, then LDS combines them: 32 copies per
+// thread instead of 128 (the 32 workgroups of one thread per bucket were load-latency
+// bound).
+#ifndef FICP_SEL_RG
+#define FICP_SEL_RG 16
+#endif
+constexpr int RG = FICP_SEL_RG;
+constexpr int RBPB = 1024 / RG;  // buckets per workgroup
+__global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int *skip,
+                                                     HistPack hp, const u64 *range) {
     if (skip && *skip) return;
-    const int b = blockIdx.x * 256 + threadIdx.x;
+    __shared__ unsigned s_c[RG][RBPB];
+    __shared__ u64 s_f[RG][RBPB];
+    const int bl = threadIdx.x % RBPB, g = threadIdx.x / RBPB;
+    const int b = blockIdx.x * RBPB + bl;
     const u64 mask = (1ULL << hp.shift) - 1ULL;
+    const int per = (nhb + RG - 1) / RG, q0 = g * per, q1 = min(nhb, q0 + per);
     unsigned c = 0;
     u64 f = 0;
-    int q = 0;
-    for (; q + 8 <= nhb; q += 8) {
+    int q = q0;
+    for (; q + 8 <= q1; q += 8) {
         u64 v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = w.ppk[(int64_t)(q + u) * NB + b];
@@ -570,10 +582,19 @@ __global__ __launch_bounds__(256) void k_sel_reduce(SelWS w, int nhb, const int 
             f += v[u] & mask;
         }
     }
-    for (; q < nhb; ++q) {
+    for (; q < q1; ++q) {
         const u64 v = w.ppk[(int64_t)q * NB + b];
         c += (unsigned)(v >> hp.shift);
         f += v & mask;
+    }
+    s_c[g][bl] = c;
+    s_f[g][bl] = f;
+    __syncthreads();
+    if (g != 0) return;
+#pragma unroll
+    for (int h = 1; h < RG; ++h) {
+        c += s_c[h][bl];
+        f += s_f[h][bl];
     }
     // the bucket's sum bracketed by the truncated fixed-point sum (each row loses < 1
     // unit): f * 2^(e - fixb) <= sum < (f + c) * 2^(e - fixb); computed here, one bucket
@@ -1510,7 +1531,7 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     const HistPack hp = hist_pack(n);
     hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
                        range_parts, w, skip, hp);
-    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / 256), dim3(256), 0, s, w, hist_blocks(n), skip, hp,
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip, hp,
                        (const unsigned long long *)range);
     hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev,
                        (const unsigned long long *)range, skip, hp.fixb);

@@ -543,10 +543,7 @@ int64_t scan_tmp_elems(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; 
 hipError_t launch_scan_i32(const int32_t *in, int32_t *out, int64_t n, int32_t *tmp,
                            bool atomic_in, hipStream_t s) {
     const int nb = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
-    if (nb == 0) {
-        hipMemsetAsync(out, 0, sizeof(int32_t), s);
-        return hipGetLastError();
-    }
+    if (nb == 0) return hipMemsetAsync(out, 0, sizeof(int32_t), s);
     if (atomic_in)
         hipLaunchKernelGGL(k_scan_partial<true>, dim3(nb), dim3(256), 0, s, in, n, tmp);
     else

@@ -75,8 +75,15 @@ constexpr int NSB_LOG = 11;
 constexpr int NS = 4096;     // sub-bins of one refinement level
 constexpr int NS_LOG = 12;
 constexpr int MAXLEV = 4;
-constexpr int GT = 256;      // gather: threads per block
-constexpr int GI = 16;       // gather: rows per thread (~1 block per CU at 1M rows)
+#ifndef FICP_GT
+#define FICP_GT 512
+#endif
+#ifndef FICP_GI
+#define FICP_GI 8
+#endif
+constexpr int GT = FICP_GT;  // gather: threads per block
+constexpr int GI = FICP_GI;  // gather: rows per thread (~1 block per CU at 1M rows; 512 x 8
+                             // measured +1 % over 256 x 16 and 256 x 8)
 
 // error bits of SelCtl::err (sticky; the host checks them after a run)
 constexpr unsigned ERR_EMPTY = 1u;  // candidate set empty (cannot happen with finite r)
@@ -112,8 +119,15 @@ inline int gather_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + GT *
 // stores and k_sel_reduce sums them.  Global atomics execute at the memory side at one
 // wave-instruction per ~50 ns per CU (MI355X_MICROARCH.md, global atomics), so flushing
 // 8192 buckets with atomics cost ~15 us and reading + resetting them from one CU ~25 us.
-constexpr int HBMAX = 128;
-inline int hist_blocks(int64_t n) { return (int)std::min<int64_t>(HBMAX, std::max<int64_t>(1, (n + 8191) / 8192)); }
+#ifndef FICP_HIST_ROWS
+#define FICP_HIST_ROWS 8192
+#endif
+#ifndef FICP_HBMAX
+#define FICP_HBMAX 128
+#endif
+constexpr int HBMAX = FICP_HBMAX;
+constexpr int HROWS = FICP_HIST_ROWS;  // rows per histogram block (target)
+inline int hist_blocks(int64_t n) { return (int)std::min<int64_t>(HBMAX, std::max<int64_t>(1, (n + HROWS - 1) / HROWS)); }
 
 // One 64-bit LDS atomic per row: (1 << shift) + m, the count in the top cbits (a block
 // holds at most `per` rows) and the fixed-point value m < 2^fixb below it with room for

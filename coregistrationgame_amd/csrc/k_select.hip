@@ -103,6 +103,9 @@ struct SelWS {
     unsigned *hcnt;  // [NB] reduced counts (plain stores, k_sel_reduce)
     double *hlo;     // [NB] bracket of each bucket's sum of r (plain stores, k_sel_reduce)
     double *hhi;
+    unsigned *acnt;  // [NB / 16] per 16-bucket chunk: count and the two sums, in bucket order
+    double *alo;     //   (k_sel_reduce; the bounds kernel's per-thread chunk totals)
+    double *ahi;
     u64 *ppk;        // [HBMAX][NB] per-block (count << shift) + fixed-point sum (plain stores)
     SelCtl *ctl;
     double *parts;   // [gather blocks]
@@ -160,6 +163,9 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.hcnt = (unsigned *)take(NB * 4);
     x.hlo = (double *)take(NB * 8);
     x.hhi = (double *)take(NB * 8);
+    x.acnt = (unsigned *)take(NB / 16 * 4);
+    x.alo = (double *)take(NB / 16 * 8);
+    x.ahi = (double *)take(NB / 16 * 8);
     x.ppk = (u64 *)take((int64_t)HBMAX * NB * 8);
     x.ctl = (SelCtl *)take(256);
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
@@ -625,6 +631,23 @@ __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int
     w.hcnt[b] = c;
     w.hlo[b] = lo;
     w.hhi[b] = hi;
+    // chunk totals of 16 consecutive buckets (lanes 16m..16m+15 of this wave), added in
+    // bucket order by the chunk's first lane
+    static_assert(RBPB == 64, "one wave of buckets per workgroup");
+    const int l0 = bl & ~15;
+    unsigned cs = 0;
+    double ls = 0.0, hs = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        cs += (unsigned)__shfl((int)c, l0 + u, 64);
+        ls = ls + __shfl(lo, l0 + u, 64);
+        hs = hs + __shfl(hi, l0 + u, 64);
+    }
+    if ((bl & 15) == 0) {
+        w.acnt[b >> 4] = cs;
+        w.alo[b >> 4] = ls;
+        w.ahi[b >> 4] = hs;
+    }
 }
 
 // Bounds of the FRMSD curve over the level-0 buckets (one workgroup).  Per-thread
@@ -649,39 +672,12 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     const int s = sel_shift(kmin, kmax);
     SELPROF(8);
     if (t == 0) s_nact = 0;
-    // this thread's PER consecutive buckets: counts and sum brackets (k_sel_reduce)
-    unsigned cc[PER];
-    double blo[PER], bhi[PER];
-#pragma unroll
-    for (int j = 0; j < PER; j += 4) {
-        const uint4 c4 = *reinterpret_cast<const uint4 *>(w.hcnt + t * PER + j);
-        const double2 l0 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j);
-        const double2 l1 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j + 2);
-        const double2 h0 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j);
-        const double2 h1 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j + 2);
-        cc[j] = c4.x;
-        cc[j + 1] = c4.y;
-        cc[j + 2] = c4.z;
-        cc[j + 3] = c4.w;
-        blo[j] = l0.x;
-        blo[j + 1] = l0.y;
-        blo[j + 2] = l1.x;
-        blo[j + 3] = l1.y;
-        bhi[j] = h0.x;
-        bhi[j + 1] = h0.y;
-        bhi[j + 2] = h1.x;
-        bhi[j + 3] = h1.y;
-    }
-    __syncthreads();
+    static_assert(PER == 16, "chunk totals of k_sel_reduce");
+    // this thread's chunk of PER consecutive buckets: totals from k_sel_reduce; the
+    // buckets themselves are loaded only by the chunks that stay active below
+    const long long ct = w.acnt[t];
+    const double tlo = w.alo[t], thi = w.ahi[t];
     SELPROF(9);
-    long long ct = 0;
-    double tlo = 0.0, thi = 0.0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        ct += cc[j];
-        tlo = tlo + blo[j];
-        thi = thi + bhi[j];
-    }
     long long Cex = ct;
     double Plo = tlo, Phi = thi;
     blk_excl_scan3(Cex, Plo, Phi, scr);
@@ -692,9 +688,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     // lo_r) exceeds U1 can neither hold the minimising bucket end nor a candidate bucket;
     // (3) only the remaining chunks (a few, near the minimum) evaluate their buckets.
     const double p = 2.0 * lam + 1.0;
-    double Pend = Phi;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) Pend = Pend + bhi[j];
+    const double Pend = Phi + thi;
     double U1 = ct ? h_of(Cex + ct, Pend, p) + kMarg : INFINITY;
     U1 = blk_min_d(U1, scr);
     SELPROF(11);
@@ -703,7 +697,29 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     const bool active = ct && (!(block_lb(Cex, ct, Plo, lo_r(kmin + ((u64)(t * PER) << s)), p) -
                                        1e-9 > U1) ||
                                !(p >= 1.0));
+    unsigned cc[PER];
+    double blo[PER], bhi[PER];
     if (active) {
+#pragma unroll
+        for (int j = 0; j < PER; j += 4) {
+            const uint4 c4 = *reinterpret_cast<const uint4 *>(w.hcnt + t * PER + j);
+            const double2 l0 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j);
+            const double2 l1 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j + 2);
+            const double2 h0 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j);
+            const double2 h1 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j + 2);
+            cc[j] = c4.x;
+            cc[j + 1] = c4.y;
+            cc[j + 2] = c4.z;
+            cc[j + 3] = c4.w;
+            blo[j] = l0.x;
+            blo[j + 1] = l0.y;
+            blo[j + 2] = l1.x;
+            blo[j + 3] = l1.y;
+            bhi[j] = h0.x;
+            bhi[j + 1] = h0.y;
+            bhi[j + 2] = h1.x;
+            bhi[j + 3] = h1.y;
+        }
         const int a = atomicAdd(&s_nact, 1);
         if (a < MAXACT) {
             s_act[a] = t;

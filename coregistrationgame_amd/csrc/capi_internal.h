@@ -96,6 +96,7 @@ struct HostReport {
     IterState st;
     unsigned misc[4];  // sort flag, selection {error bits, levels, radix fallbacks}
     double bb[4];      // CHM bbox
+    unsigned long long t[2];  // device clock (100 MHz) at run start / at the final report
     int flag;          // -1 while pending, 1 when the segments have landed
 };
 

@@ -241,7 +241,8 @@ __device__ inline void fit_solve(const double c[8], double k, double px, double 
 
 // Loop parameters and optional trace buffers of the device-resident loop.
 struct LoopCtl {
-    const double *lams;    // [nstages] on the device
+    const double *lams;    // [nstages] on the device (read only past the first kLamIn)
+    double lam_in[4];      // the first kLamIn lambdas, carried in the kernel arguments
     int nstages;
     int max_iter;
     double threshold;
@@ -252,6 +253,11 @@ struct LoopCtl {
     double *tl;            // [max_trace] lambda per call
     double *tT;            // [max_trace * 9] fits in order
 };
+
+constexpr int kLamIn = 4;
+__host__ __device__ __forceinline__ double lam_of(const LoopCtl &c, int i) {
+    return i < kLamIn ? c.lam_in[i] : c.lams[i];
+}
 
 // ---------------------------------------------- device-resident loop (k_loop.hip)
 __device__ __forceinline__ void loop_set_flags(IterState &s) {
@@ -266,7 +272,7 @@ __device__ __forceinline__ void loop_end_stage(IterState &s, const LoopCtl &c) {
     s.it = 0;
     if (s.stage < c.nstages) {  // ficp.py:152-153: next lambda, next _iterate
         s.phase = PH_HEAD;
-        s.lam_cur = c.lams[s.stage];
+        s.lam_cur = lam_of(c, s.stage);
     } else {
         s.phase = PH_DONE;
     }
@@ -325,7 +331,9 @@ struct ReportSeg {
     int words;        // 32-bit words (0: unused)
 };
 hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg &c, int *flag,
-                         hipStream_t s);
+                         unsigned long long *t_end, hipStream_t s);
+// zero the sort timeout flag and stamp the device clock (100 MHz) into *t0 (host)
+hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s);
 
 // grid build (k_grid_nn.hip)
 hipError_t launch_minmax2(const double *x, const double *y, int64_t m, double *partials,

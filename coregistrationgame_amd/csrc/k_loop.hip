@@ -27,7 +27,7 @@ __global__ void k_loop_init(IterState *st, LoopCtl c) {
     s.n_nn = s.n_fit = 0;
     s.iters[0] = s.iters[1] = 0;
     s.phase = c.nstages > 0 ? PH_HEAD : PH_DONE;
-    s.lam_cur = c.nstages > 0 ? c.lams[0] : 0.0;
+    s.lam_cur = c.nstages > 0 ? lam_of(c, 0) : 0.0;
     loop_set_flags(s);
 }
 
@@ -56,21 +56,42 @@ __global__ __launch_bounds__(256) void k_trace_idx(const IterState *st, const in
 // *flag (system scope, after a system fence): the host polls the flag instead of a
 // stream synchronisation plus one hipMemcpyAsync per segment (those cost 40-50 us of idle
 // device each at C3, profiles/r1sel trace).
-__global__ void k_report(ReportSeg a, ReportSeg b, ReportSeg c, int *flag) {
+// run start: zero the sort's timeout flag and stamp the device clock (100 MHz) into
+// coherent host memory; the report kernel stamps the end (ficp_stats::gpu_ms without
+// event records, each of which left ~5 us of idle queue)
+__global__ void k_run_start(uint32_t *tflag, unsigned long long *t0) {
+    if (threadIdx.x == 0) {
+        __hip_atomic_exchange(tflag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s) {
+    hipLaunchKernelGGL(k_run_start, dim3(1), dim3(64), 0, s, tflag, t0);
+    return hipGetLastError();
+}
+
+__global__ void k_report(ReportSeg a, ReportSeg b, ReportSeg c, int *flag,
+                         unsigned long long *t_end) {
     const ReportSeg sg[3] = {a, b, c};
     for (int q = 0; q < 3; ++q) {
         const uint32_t *src = (const uint32_t *)sg[q].src;
         uint32_t *dst = (uint32_t *)sg[q].dst;
         for (int w = threadIdx.x; w < sg[q].words; w += blockDim.x) dst[w] = src[w];
     }
+    if (t_end && threadIdx.x == 0)
+        __hip_atomic_store(t_end, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg &c, int *flag,
+                         unsigned long long *t_end,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_report, dim3(1), dim3(256), 0, s, a, b, c, flag);
+    hipLaunchKernelGGL(k_report, dim3(1), dim3(256), 0, s, a, b, c, flag, t_end);
     return hipGetLastError();
 }
 

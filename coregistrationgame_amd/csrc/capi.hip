@@ -57,7 +57,9 @@ int ensure_bbox(ficp_ctx *c) {
     return FICP_OK;
 }
 
-int ensure_grid(ficp_ctx *c) {
+// job: with the bucket-sort path, the build is returned as a job (launched by the caller
+// together with the work order) instead of being launched here
+int ensure_grid(ficp_ctx *c, BSJob *job = nullptr) {
     if (c->grid_ready) return FICP_OK;
     const int64_t m = c->m;
     ProfScope ps(c, P_GRID, "grid_build");
@@ -84,9 +86,14 @@ int ensure_grid(ficp_ctx *c) {
         BSortOut bo{};
         bo.pts = c->pts.as<TPt>();
         bo.cell_start = c->cell_start.as<int32_t>();
-        HIPCHK(launch_bsort(c->tx.as<double>(), c->ty.as<double>(),
-                            c->md == 3 ? c->tz.as<double>() : nullptr, m, bg, c->ncells, bo,
-                            c->bs_tmp.p, c->stream));
+        if (job && m > 0)
+            *job = bsort_job(c->tx.as<double>(), c->ty.as<double>(),
+                             c->md == 3 ? c->tz.as<double>() : nullptr, m, bg, c->ncells, bo,
+                             c->bs_tmp.p);
+        else
+            HIPCHK(launch_bsort(c->tx.as<double>(), c->ty.as<double>(),
+                                c->md == 3 ? c->tz.as<double>() : nullptr, m, bg, c->ncells, bo,
+                                c->bs_tmp.p, c->stream));
         g.pts = c->pts.as<TPt>();
         g.cell_start = c->cell_start.as<int32_t>();
         g.m = m;
@@ -320,8 +327,9 @@ int read_state(ficp_ctx *c) {
 
 // Spatial work order: the source permuted into 8x8-cell supertile order of the CHM grid
 // (ties by index), so each wave's queries scan neighbouring cells.
+// job: as in ensure_grid (the bucket-sort path returns its job instead of launching)
 int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const double *sz,
-                     int64_t n) {
+                     int64_t n, BSJob *job = nullptr) {
     CHK(c->wx.ensure(n * 8));
     CHK(c->wy.ensure(n * 8));
     if (sz) CHK(c->wz.ensure(n * 8));
@@ -330,9 +338,8 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
     const GridView &g = c->gv;
     const int64_t nkeys = (int64_t)((g.gx + 7) / 8) * (int64_t)((g.gy + 7) / 8) * 64;
     if (bsort_supported(n, nkeys) && !getenv("FICP_WORK_RADIX")) {
-        // on the side stream, beside the grid build (both are a few hundred workgroups
-        // wide): it waits for c->ev_fork (the sources are ready, recorded by run_core
-        // before the grid build) and the main stream waits for it before the loop
+        // run_core launches it with the grid build as one two-job bucket sort (it ran on a
+        // side stream beside the build before: fork/join events and four more launches)
         CHK(c->bs_tmp2.ensure(bsort_tmp_bytes(n, nkeys)));
         const BSortGeom bg{g.x0, g.y0, g.inv_h, g.gx, g.gy, 1};
         BSortOut bo{};
@@ -340,10 +347,11 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
         bo.wy = c->wy.as<double>();
         bo.wz = sz ? c->wz.as<double>() : nullptr;
         bo.worig = c->worig.as<uint32_t>();
-        HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-        HIPCHK(launch_bsort(sx, sy, sz, n, bg, nkeys, bo, c->bs_tmp2.p, c->stream2));
-        HIPCHK(hipEventRecord(c->ev_join, c->stream2));
-        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+        if (job) {
+            *job = bsort_job(sx, sy, sz, n, bg, nkeys, bo, c->bs_tmp2.p);
+            return FICP_OK;
+        }
+        HIPCHK(launch_bsort(sx, sy, sz, n, bg, nkeys, bo, c->bs_tmp2.p, c->stream));
         return FICP_OK;
     }
     HIPCHK(launch_src_cellkey(sx, sy, n, c->gv, c->key.as<unsigned long long>(), c->stream));
@@ -401,9 +409,12 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     const double *wz = sz;
     const uint32_t *worig = nullptr;
     if (use_grid(c, n)) {
-        HIPCHK(hipEventRecord(c->ev_fork, c->stream));  // the sources are ready (work order)
-        CHK(ensure_grid(c));
-        CHK(build_work_order(c, sx, sy, sz, n));
+        // the grid build and the work order: one bucket sort of two jobs (four launches)
+        BSJob gj{}, wj{};
+        CHK(ensure_grid(c, &gj));
+        CHK(build_work_order(c, sx, sy, sz, n, &wj));
+        if (gj.n > 0 || wj.n > 0)
+            HIPCHK(launch_bsort2(gj.n > 0 ? gj : wj, gj.n > 0 ? wj : BSJob{}, c->stream));
         wx = c->wx.as<double>();
         wy = c->wy.as<double>();
         wz = sz ? c->wz.as<double>() : nullptr;
@@ -610,9 +621,6 @@ int ficp_create(int device, ficp_ctx **out) {
     c->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipHostMalloc((void **)&c->h_state, sizeof(IterState), hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -662,9 +670,6 @@ void ficp_destroy(ficp_ctx *c) {
     for (hipEvent_t &e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 

@@ -103,8 +103,6 @@ struct HostReport {
 struct ficp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;  // side stream: the work order beside the grid build
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int nn_mode = 0;
 
     // target (CHM layer)

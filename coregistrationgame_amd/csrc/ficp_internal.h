@@ -383,9 +383,29 @@ struct BSortOut {
     double *wx, *wy, *wz; // mode 1 (wz nullable)
     uint32_t *worig;      // mode 1
 };
+// one sort job of k_bsort.hip: inputs, geometry, plan, outputs and its carved scratch
+struct BSJob {
+    const double *x, *y, *z;
+    int64_t n;
+    BSortGeom g;
+    BSortPlan p;
+    BSortOut o;
+    uint32_t *counts, *totals, *base;
+    TPt *rec;
+    uint64_t *gcomp;
+    uint32_t *gpos;
+};
+struct BSPair {
+    BSJob a, b;
+    int split[4];  // workgroups of job a in each of the four kernels
+};
 BSortPlan bsort_plan(int64_t n, int64_t nkeys);
 bool bsort_supported(int64_t n, int64_t nkeys);
 int64_t bsort_tmp_bytes(int64_t n, int64_t nkeys);
+BSJob bsort_job(const double *x, const double *y, const double *z, int64_t n, const BSortGeom &g,
+                int64_t nkeys, const BSortOut &o, void *tmp);
+// two jobs in the same four launches (b.n == 0: job a alone); both must be supported
+hipError_t launch_bsort2(const BSJob &a, const BSJob &b, hipStream_t s);
 hipError_t launch_bsort(const double *x, const double *y, const double *z, int64_t n,
                         const BSortGeom &g, int64_t nkeys, const BSortOut &o, void *tmp,
                         hipStream_t s);

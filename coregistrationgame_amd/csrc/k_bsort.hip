@@ -52,12 +52,25 @@ __device__ __forceinline__ uint32_t bs_key(double x, double y, const BSortGeom &
     return (st << 6) | ((uint32_t)(cy & 7) << 3) | (uint32_t)(cx & 7);
 }
 
-__global__ __launch_bounds__(BT) void k_bs_count(const double *x, const double *y, int64_t n,
-                                                 BSortGeom g, BSortPlan p, uint32_t *counts) {
+// Every kernel runs one or two sort jobs side by side (the grid build and the work
+// order): workgroups [0, split) take job a, the rest job b.  J is the workgroup's job,
+// bid its workgroup index inside that job.
+#define BS_PICK(SPLIT)                                         \
+    const bool bs_b = (int)blockIdx.x >= (SPLIT);              \
+    const BSJob &J = bs_b ? P.b : P.a;                         \
+    const int bid = (int)blockIdx.x - (bs_b ? (SPLIT) : 0);    \
+    const BSortGeom g = J.g;                                   \
+    const BSortPlan p = J.p;
+
+__global__ __launch_bounds__(BT) void k_bs_count(BSPair P) {
+    BS_PICK(P.split[0])
+    const double *x = J.x, *y = J.y;
+    const int64_t n = J.n;
+    uint32_t *counts = J.counts;
     __shared__ uint32_t h[BMAXB];
     for (int b = threadIdx.x; b < p.nbk; b += BT) h[b] = 0u;
     __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * p.per, i1 = min(n, i0 + p.per);
+    const int64_t i0 = (int64_t)bid * p.per, i1 = min(n, i0 + p.per);
     constexpr int U = 8;  // points in flight per thread
     for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * BT) {
         double xv[U], yv[U];
@@ -72,7 +85,7 @@ __global__ __launch_bounds__(BT) void k_bs_count(const double *x, const double *
             if (i + (int64_t)u * BT < i1) atomicAdd(&h[bs_key(xv[u], yv[u], g) >> p.fs], 1u);
     }
     __syncthreads();
-    uint32_t *c = counts + (int64_t)blockIdx.x * p.nbk;
+    uint32_t *c = counts + (int64_t)bid * p.nbk;
     for (int b = threadIdx.x; b < p.nbk; b += BT) c[b] = h[b];
 }
 
@@ -80,11 +93,13 @@ __global__ __launch_bounds__(BT) void k_bs_count(const double *x, const double *
 // 64 buckets: thread (c, l) holds slices 16c..16c+15 of bucket l, so every load and store
 // is a coalesced 256-B row segment (a wave per bucket with lanes over slices read 4 B per
 // 16 KB stride: 17 us at 1M points), and the 16 chunk sums are scanned through LDS.
-__global__ __launch_bounds__(1024) void k_bs_colscan(uint32_t *counts, BSortPlan p,
-                                                     uint32_t *totals) {
+__global__ __launch_bounds__(1024) void k_bs_colscan(BSPair P) {
+    BS_PICK(P.split[1])
+    (void)g;
+    uint32_t *counts = J.counts, *totals = J.totals;
     __shared__ uint32_t s_c[16][64];
     const int l = threadIdx.x & 63, c = threadIdx.x >> 6;
-    const int b = blockIdx.x * 64 + l;
+    const int b = bid * 64 + l;
     const bool ok = b < p.nbk;
     constexpr int R = 16;  // slices per thread (nb1 <= 256)
     uint32_t v[R], tot = 0;
@@ -107,11 +122,13 @@ __global__ __launch_bounds__(1024) void k_bs_colscan(uint32_t *counts, BSortPlan
     }
 }
 
-__global__ __launch_bounds__(BT) void k_bs_scatter(const double *x, const double *y,
-                                                   const double *z, int64_t n, BSortGeom g,
-                                                   BSortPlan p, const uint32_t *colpref,
-                                                   const uint32_t *totals, uint32_t *base_out,
-                                                   TPt *rec) {
+__global__ __launch_bounds__(BT) void k_bs_scatter(BSPair P) {
+    BS_PICK(P.split[2])
+    const double *x = J.x, *y = J.y, *z = J.z;
+    const int64_t n = J.n;
+    const uint32_t *colpref = J.counts, *totals = J.totals;
+    uint32_t *base_out = J.base;
+    TPt *rec = J.rec;
     __shared__ uint32_t fill[BMAXB];
     __shared__ uint32_t s_w[BT / 64];
     // bases: exclusive scan of the bucket totals (each workgroup redoes it: 16 KB)
@@ -139,14 +156,14 @@ __global__ __launch_bounds__(BT) void k_bs_scatter(const double *x, const double
     for (int j = 0; j < PB; ++j) {
         const int b = threadIdx.x * PB + j;
         if (b < p.nbk) {
-            fill[b] = run + colpref[(int64_t)blockIdx.x * p.nbk + b];
-            if (blockIdx.x == 0) base_out[b] = run;
+            fill[b] = run + colpref[(int64_t)bid * p.nbk + b];
+            if (bid == 0) base_out[b] = run;
         }
         run += v[j];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) base_out[p.nbk] = (uint32_t)n;
+    if (bid == 0 && threadIdx.x == 0) base_out[p.nbk] = (uint32_t)n;
     __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * p.per, i1 = min(n, i0 + p.per);
+    const int64_t i0 = (int64_t)bid * p.per, i1 = min(n, i0 + p.per);
     constexpr int U = 8;  // points in flight per thread (the loop was load-latency bound)
     for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * BT) {
         double xv[U], yv[U], zv[U];
@@ -197,9 +214,13 @@ __device__ __forceinline__ void bs_emit(const BSortOut &o, int64_t q, const TPt 
     }
 }
 
-__global__ __launch_bounds__(B4T) void k_bs_bucket(const TPt *rec, const uint32_t *base,
-                                                   BSortGeom g, BSortPlan p, BSortOut o,
-                                                   uint64_t *gcomp, uint32_t *gpos) {
+__global__ __launch_bounds__(B4T) void k_bs_bucket(BSPair P) {
+    BS_PICK(P.split[3])
+    const TPt *rec = J.rec;
+    const uint32_t *base = J.base;
+    const BSortOut o = J.o;
+    uint64_t *gcomp = J.gcomp;
+    uint32_t *gpos = J.gpos;
     // dynamic LDS sized by the plan (bs_bucket_lds): ~23 KB at 1M points, so several
     // workgroups share a CU
     extern __shared__ __align__(32) unsigned char dyn[];
@@ -210,7 +231,7 @@ __global__ __launch_bounds__(B4T) void k_bs_bucket(const TPt *rec, const uint32_
     uint32_t *ff = fc + nf;                                   // [nf] fill counters
     uint16_t *lsrc = (uint16_t *)(ff + nf);                     // [bcap] bin slot -> record
     __shared__ uint32_t s_w[B4T / 64];
-    const int b = blockIdx.x;
+    const int b = bid;
     const uint32_t lo = base[b], hi = base[b + 1], cnt = hi - lo;
     const uint32_t mask = (uint32_t)nf - 1u;
     for (int f = threadIdx.x; f < nf; f += B4T) {
@@ -328,6 +349,60 @@ int64_t bsort_tmp_bytes(int64_t n, int64_t nkeys) {
            nn * (int64_t)sizeof(TPt) + nn * 8 + nn * 4 + 256;
 }
 
+// a job's scratch carved from tmp (bsort_tmp_bytes(n, nkeys) bytes)
+BSJob bsort_job(const double *x, const double *y, const double *z, int64_t n, const BSortGeom &g,
+                int64_t nkeys, const BSortOut &o, void *tmp) {
+    BSJob j{};
+    j.x = x;
+    j.y = y;
+    j.z = z;
+    j.n = n;
+    j.g = g;
+    j.p = bsort_plan(n, nkeys);
+    j.o = o;
+    auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
+    char *q = (char *)tmp;
+    q += 256;
+    j.counts = (uint32_t *)q;
+    q += al((int64_t)j.p.nb1 * j.p.nbk * 4);
+    j.totals = (uint32_t *)q;
+    q += al((int64_t)(j.p.nbk + 1) * 4);
+    j.base = (uint32_t *)q;
+    q += al((int64_t)(j.p.nbk + 1) * 4);
+    j.rec = (TPt *)q;
+    q += al(n * (int64_t)sizeof(TPt));
+    j.gcomp = (uint64_t *)q;
+    q += al(n * 8);
+    j.gpos = (uint32_t *)q;
+    return j;
+}
+
+// one or two jobs (b.n == 0: a alone), four launches for both
+hipError_t launch_bsort2(const BSJob &a, const BSJob &b, hipStream_t s) {
+    BSPair P{a, b, {0, 0, 0, 0}};
+    const bool two = b.n > 0;
+    auto blocks = [](const BSJob &j, int k) -> int {
+        if (j.n <= 0) return 0;
+        if (k == 0 || k == 2) return j.p.nb1;
+        if (k == 1) return (j.p.nbk + 63) / 64;
+        return j.p.nbk;
+    };
+    int tot[4];
+    for (int k = 0; k < 4; ++k) {
+        P.split[k] = blocks(a, k);
+        tot[k] = P.split[k] + (two ? blocks(b, k) : 0);
+    }
+    auto lds_of = [](const BSJob &j) {
+        return (size_t)j.p.bcap * (sizeof(TPt) + 8 + 2) + (size_t)2 * 4 * (1 << j.p.fs);
+    };
+    const size_t lds = std::max(lds_of(a), two ? lds_of(b) : (size_t)0);
+    hipLaunchKernelGGL(k_bs_count, dim3(tot[0]), dim3(BT), 0, s, P);
+    hipLaunchKernelGGL(k_bs_colscan, dim3(tot[1]), dim3(1024), 0, s, P);
+    hipLaunchKernelGGL(k_bs_scatter, dim3(tot[2]), dim3(BT), 0, s, P);
+    hipLaunchKernelGGL(k_bs_bucket, dim3(tot[3]), dim3(B4T), lds, s, P);
+    return hipGetLastError();
+}
+
 hipError_t launch_bsort(const double *x, const double *y, const double *z, int64_t n,
                         const BSortGeom &g, int64_t nkeys, const BSortOut &o, void *tmp,
                         hipStream_t s) {
@@ -336,29 +411,8 @@ hipError_t launch_bsort(const double *x, const double *y, const double *z, int64
             return hipMemsetAsync(o.cell_start, 0, (size_t)(nkeys + 1) * 4, s);
         return hipSuccess;
     }
-    const BSortPlan p = bsort_plan(n, nkeys);
     if (!bsort_supported(n, nkeys)) return hipErrorInvalidValue;
-    auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
-    char *q = (char *)tmp;
-    q += 256;
-    uint32_t *counts = (uint32_t *)q;
-    q += al((int64_t)p.nb1 * p.nbk * 4);
-    uint32_t *totals = (uint32_t *)q;
-    q += al((int64_t)(p.nbk + 1) * 4);
-    uint32_t *base = (uint32_t *)q;
-    q += al((int64_t)(p.nbk + 1) * 4);
-    TPt *rec = (TPt *)q;
-    q += al(n * (int64_t)sizeof(TPt));
-    uint64_t *gcomp = (uint64_t *)q;
-    q += al(n * 8);
-    uint32_t *gpos = (uint32_t *)q;
-    hipLaunchKernelGGL(k_bs_count, dim3(p.nb1), dim3(BT), 0, s, x, y, n, g, p, counts);
-    hipLaunchKernelGGL(k_bs_colscan, dim3((p.nbk + 63) / 64), dim3(1024), 0, s, counts, p, totals);
-    hipLaunchKernelGGL(k_bs_scatter, dim3(p.nb1), dim3(BT), 0, s, x, y, z, n, g, p, counts,
-                       totals, base, rec);
-    const size_t lds = (size_t)p.bcap * (sizeof(TPt) + 8 + 2) + (size_t)2 * 4 * (1 << p.fs);
-    hipLaunchKernelGGL(k_bs_bucket, dim3(p.nbk), dim3(B4T), lds, s, rec, base, g, p, o, gcomp, gpos);
-    return hipGetLastError();
+    return launch_bsort2(bsort_job(x, y, z, n, g, nkeys, o, tmp), BSJob{}, s);
 }
 
 }  // namespace ficp

@@ -43,8 +43,10 @@ int ensure_bbox(ficp_ctx *c) {
     if (c->bbox_ready) return FICP_OK;
     CHK(c->mm_part.ensure(1024 * 4 * 8));
     CHK(c->mm_out.ensure(4 * 8));
-    HIPCHK(launch_minmax2(c->tx.as<double>(), c->ty.as<double>(), c->m, c->mm_part.as<double>(),
-                          c->mm_out.as<double>(), c->stream));
+    if (!c->bbox_dev)
+        HIPCHK(launch_minmax2(c->tx.as<double>(), c->ty.as<double>(), c->m,
+                              c->mm_part.as<double>(), c->mm_out.as<double>(), c->stream));
+    c->bbox_dev = false;
     CHK(report_wait(c, ReportSeg{c->mm_out.p, c->h_rep->bb, 8}, ReportSeg{}, ReportSeg{}));
     memcpy(c->bb, c->h_rep->bb, sizeof c->bb);
     const double *bb = c->bb;
@@ -585,6 +587,7 @@ void reset_target(ficp_ctx *c, int64_t m, int md) {
     c->has_target = true;
     c->grid_ready = false;
     c->bbox_ready = false;
+    c->bbox_dev = false;
     c->m = m;
     c->md = md;
 }
@@ -739,10 +742,14 @@ int ficp_set_target_device(ficp_ctx *c, const double *x, const double *y, const 
     CHK(c->ty.ensure(m * 8));
     CHK(c->tz.ensure(m * 8));
     if (m > 0) {
-        HIPCHK(hipMemcpyAsync(c->tx.p, x, m * 8, hipMemcpyDeviceToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->ty.p, y, m * 8, hipMemcpyDeviceToDevice, c->stream));
-        if (md == 3)
-            HIPCHK(hipMemcpyAsync(c->tz.p, z, m * 8, hipMemcpyDeviceToDevice, c->stream));
+        // one kernel copies the columns and reduces the bbox (three copies + the bbox
+        // pass were four launches); ensure_bbox reads the result
+        CHK(c->mm_part.ensure(1024 * 4 * 8));
+        CHK(c->mm_out.ensure(4 * 8));
+        HIPCHK(launch_minmax2(x, y, m, c->mm_part.as<double>(), c->mm_out.as<double>(), c->stream,
+                              md == 3 ? z : nullptr, c->tx.as<double>(), c->ty.as<double>(),
+                              md == 3 ? c->tz.as<double>() : nullptr));
+        c->bbox_dev = true;
     }
     return FICP_OK;  // stream-ordered; the grid is built on first use
 }

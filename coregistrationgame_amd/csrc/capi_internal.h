@@ -124,6 +124,7 @@ struct ficp_ctx {
     DevBuf stage, stage2, cx, cy, cz, state_dev;
     DevBuf bp;  // grid slot of each query's last match (warm start of the next NN call)
     DevBuf dz2; // dz^2 of each query's last match (warm start from (ccx, ccy, dz2))
+    bool bbox_dev = false;  // the bbox is in mm_out already (set_target_device), not read yet
     DevBuf gap; // certified-reuse bound of each query's match (k_grid_nn.hip nn_query_cert)
     DevBuf lams, tr_k, tr_f, tr_l, tr_T, tr_idx;  // device loop: lambdas and traces
     DevBuf sel_tmp, sel_stats;  // bucketed fraction selection (k_select.hip)

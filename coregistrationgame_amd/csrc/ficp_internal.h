@@ -336,8 +336,10 @@ hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg
 hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s);
 
 // grid build (k_grid_nn.hip)
+// bbox of (x, y) -> out4 {xmin, xmax, ymin, ymax}; with ox, also copies x, y (z) there
 hipError_t launch_minmax2(const double *x, const double *y, int64_t m, double *partials,
-                          double *out4, hipStream_t s);
+                          double *out4, hipStream_t s, const double *z = nullptr,
+                          double *ox = nullptr, double *oy = nullptr, double *oz = nullptr);
 hipError_t launch_grid_count(const double *x, const double *y, int64_t m, double x0, double y0,
                              double inv_h, int gx, int gy, int32_t *cell_of, int32_t *counts,
                              hipStream_t s);

@@ -986,12 +986,20 @@ __global__ __launch_bounds__(256) void k_apply_inplace(double *x, double *y, int
 }
 
 // ---------------------------------------------------------------- grid build
+// ox non-null: also copies x, y (and z when both non-null) to ox, oy, oz on the way
 __global__ __launch_bounds__(256) void k_minmax2_partial(const double *x, const double *y,
-                                                         int64_t m, double *partials) {
+                                                         int64_t m, double *partials,
+                                                         const double *z, double *ox, double *oy,
+                                                         double *oz) {
     __shared__ double s[4][256];
     double a0 = INFINITY, a1 = -INFINITY, b0 = INFINITY, b1 = -INFINITY;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (int64_t)gridDim.x * 256) {
         const double vx = x[i], vy = y[i];
+        if (ox) {
+            ox[i] = vx;
+            oy[i] = vy;
+            if (z && oz) oz[i] = z[i];
+        }
         a0 = fmin(a0, vx);
         a1 = fmax(a1, vx);
         b0 = fmin(b0, vy);
@@ -1193,9 +1201,11 @@ inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b
 }  // namespace
 
 hipError_t launch_minmax2(const double *x, const double *y, int64_t m, double *partials,
-                          double *out4, hipStream_t s) {
+                          double *out4, hipStream_t s, const double *z, double *ox, double *oy,
+                          double *oz) {
     int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (m + 255) / 256));
-    hipLaunchKernelGGL(k_minmax2_partial, dim3(nb), dim3(256), 0, s, x, y, m, partials);
+    hipLaunchKernelGGL(k_minmax2_partial, dim3(nb), dim3(256), 0, s, x, y, m, partials, z, ox, oy,
+                       oz);
     hipLaunchKernelGGL(k_minmax2_final, dim3(1), dim3(256), 0, s, partials, nb, out4);
     return hipGetLastError();
 }

@@ -331,6 +331,53 @@ def test_run_certified_reuse_near_ties(oracle, md):
         np.testing.assert_allclose(final[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
 
 
+@pytest.mark.parametrize("md", [2, 3])
+def test_device_resident_path_matches_host_path(md):
+    """The bench's path (ficp_set_target_device: one kernel copies the target and reduces
+    its bbox; ficp_run_device on device columns) gives the host path's bits, twice in a
+    row on one context (the second target set replaces the first)."""
+    from coregistrationgame_amd import _lib, synth
+    C = _lib.C
+    lib = _lib.lib()
+    ctx = _lib.Context(0)
+    bufs = []
+
+    def dev(a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        p = C.c_void_p()
+        _lib._check(lib.ficp_dev_alloc(ctx.h, a.nbytes, C.byref(p)))
+        _lib._check(lib.ficp_memcpy_h2d(ctx.h, p, a.ctypes.data_as(C.c_void_p), a.nbytes))
+        bufs.append(p)
+        return p.value
+
+    def back(ptr, n):
+        out = np.empty(n)
+        _lib._check(lib.ficp_memcpy_d2h(ctx.h, out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), 8 * n))
+        return out
+
+    try:
+        lam = [3.0, 0.95 if md == 3 else 1.3]
+        for seed in (5, 6):
+            p = synth.make_plot(50_000, 60_000, 0.7, seed=seed, md=md)
+            ref = _lib.Context(0)
+            want = p.source.copy()
+            ref.set_target(p.target, md)
+            ref.run(want, lam, 1e-6, 1000, False)
+            ref.close()
+            sx, sy = dev(p.source[:, 0]), dev(p.source[:, 1])
+            sz = dev(p.source[:, 2]) if md == 3 else 0
+            tx, ty = dev(p.target[:, 0]), dev(p.target[:, 1])
+            tz = dev(p.target[:, 2]) if md == 3 else 0
+            ctx.set_target_device(tx, ty, tz, len(p.target), md)
+            ctx.run_device(sx, sy, sz, len(p.source), lam, 1e-6, 1000)
+            np.testing.assert_array_equal(bits(back(sx, len(p.source))), bits(want[:, 0]))
+            np.testing.assert_array_equal(bits(back(sy, len(p.source))), bits(want[:, 1]))
+    finally:
+        for b in bufs:
+            lib.ficp_dev_free(ctx.h, b)
+        ctx.close()
+
+
 def test_run_1M_properties():
     """C3 (1M x 1M, f=0.6, to convergence): the run undoes the synthetic misregistration
     (size-independent property) and a second run from its output is a fixed point."""

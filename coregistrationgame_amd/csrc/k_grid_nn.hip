@@ -548,6 +548,22 @@ __device__ __forceinline__ double cert_eps(const GridView &g, double qx, double 
     return 2.0 * g.margin + 1e-12 * (fabs(qx) + fabs(qy)) + 1e-9;
 }
 
+#ifndef FICP_CERT_DMUL
+#define FICP_CERT_DMUL 4.0
+#endif
+#ifndef FICP_CERT_PADMIN
+#define FICP_CERT_PADMIN 0.02
+#endif
+// how far beyond the match a full scan reaches: pad h, or DMUL times this call's move
+// when that is smaller (but at least PADMIN h).  The next certificate needs the cover to
+// exceed about twice the next move, and ICP moves shrink call by call: a cover sized
+// from the move is enough and cheaper in the later calls (C3: +1 % for DMUL 2-8)
+__device__ __forceinline__ double cert_pad(const GridView &g, double mv) {
+    const double p = FICP_CERT_PAD * g.h;
+    if (!(FICP_CERT_DMUL > 0.0)) return p;
+    return fmin(p, fmax(FICP_CERT_DMUL * mv, FICP_CERT_PADMIN * g.h));
+}
+
 // the stored match's exact d2 at the (moved) query: eval_slot's operations on (cx, cy, dz2)
 template <int MD>
 __device__ __forceinline__ double warm_d2(const NNArgs &a, int64_t i, double qx, double qy) {
@@ -563,7 +579,7 @@ __device__ __forceinline__ double warm_d2(const NNArgs &a, int64_t i, double qx,
 template <int MD>
 __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, const Stems &S,
                                          int64_t i, const double *T, unsigned long long &kmin_c,
-                                         unsigned long long &kmax) {
+                                         unsigned long long &kmax, double &mv) {
     const double ox = a.sx[i], oy = a.sy[i];
     double qx = ox, qy = oy;
     if (T) {
@@ -574,7 +590,8 @@ __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, con
     const double eps = cert_eps(g, qx, qy);
     const double d2w = warm_d2<MD>(a, i, qx, qy);
     const double mx = qx - ox, my = qy - oy;
-    const double G = a.gap[i] - sqrt(mx * mx + my * my) - eps;
+    mv = sqrt(mx * mx + my * my);
+    const double G = a.gap[i] - mv - eps;
 #ifndef FICP_CERT_MUTANT
 #define FICP_CERT_MUTANT 0.0  // > 0 only in the mutation check of the tests (unsound)
 #endif
@@ -597,8 +614,8 @@ __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, con
 // evaluated, the new bound G and the match slot stored, outputs written.
 template <int MD>
 __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, const Stems &S,
-                                          int64_t i, bool warm, unsigned long long &kmin_c,
-                                          unsigned long long &kmax) {
+                                          int64_t i, bool warm, double pad,
+                                          unsigned long long &kmin_c, unsigned long long &kmax) {
     const double qx = a.sx[i], qy = a.sy[i];
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
     const double eps = cert_eps(g, qx, qy);
@@ -632,7 +649,7 @@ __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, co
     }
     double gnew = 0.0;
     if (b.d2 < INFINITY) {
-        const double rc = sqrt(b.d2) + FICP_CERT_PAD * g.h;
+        const double rc = sqrt(b.d2) + pad;
         cover_scan<MD>(g, S, qx, qy, qz, cy, mq, rc * rc, b);
         gnew = fmin(sqrt(b.s2), rc - mq) - eps;
     }
@@ -654,20 +671,20 @@ __device__ __forceinline__ void group_eval(const Stems &S, int p0, int p1, int l
 
 template <int MD, int GS>
 __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView &g, const Stems &S,
-                                                int64_t i, int lg, unsigned long long &kmin_c,
-                                                unsigned long long &kmax) {
+                                                int64_t i, int lg, double pad,
+                                                unsigned long long &kmin_c, unsigned long long &kmax) {
     const double qx = a.sx[i], qy = a.sy[i];
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
     const double eps = cert_eps(g, qx, qy);
     const double d2w = warm_d2<MD>(a, i, qx, qy);
     if (!(d2w < INFINITY)) {  // no finite previous match: the serial cold search
-        if (lg == 0) cert_scan<MD>(a, g, S, i, false, kmin_c, kmax);
+        if (lg == 0) cert_scan<MD>(a, g, S, i, false, pad, kmin_c, kmax);
         return;
     }
     Best2 b{d2w, 0x7fffffff, -1, INFINITY};
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
     const double mq = query_margin(g, qx, qy);
-    const double rc = sqrt(d2w) + FICP_CERT_PAD * g.h;
+    const double rc = sqrt(d2w) + pad;
     const double cover2 = rc * rc;
     for (int k = -1;; ++k) {  // rows cy-1, cy, cy+1, then cy -+ 2, 3, ... while in cover
         bool any = false;
@@ -714,14 +731,15 @@ template <int MD>
 __device__ __forceinline__ bool nn_query_cert(const NNArgs &a, const GridView &g, const Stems &S,
                                               int64_t i, const double *T,
                                               unsigned long long &kmin_c, unsigned long long &kmax) {
-    if (a.warm_c && cert_try<MD>(a, g, S, i, T, kmin_c, kmax)) return true;
+    double mv = 0.0;
+    if (a.warm_c && cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv)) return true;
     if (!a.warm_c && T) {
         double qx = a.sx[i], qy = a.sy[i];
         apply_T(T, qx, qy);
         a.sx[i] = qx;
         a.sy[i] = qy;
     }
-    cert_scan<MD>(a, g, S, i, a.warm_c != 0, kmin_c, kmax);
+    cert_scan<MD>(a, g, S, i, a.warm_c != 0, cert_pad(g, a.warm_c ? mv : INFINITY), kmin_c, kmax);
     return false;
 }
 
@@ -806,31 +824,37 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
         // block-compacted: certificates first, then the workgroup's uncertified queries
         // packed densely onto its lanes (GS lanes per query when there are few of them)
         __shared__ int s_list[256];
+        __shared__ double s_mv[256];
         __shared__ int s_n;
         if (threadIdx.x == 0) s_n = 0;
         __syncthreads();
         const Stems S = stems_of(g.pts, g.m);
-        const bool pend = i < a.n && !cert_try<MD>(a, g, S, i, T, kmin_c, kmax);
+        double mv = 0.0;
+        const bool pend = i < a.n && !cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv);
         const unsigned long long m = __ballot(pend);
         const int lane = threadIdx.x & 63;
         int base = 0;
         if (lane == 0 && m) base = atomicAdd(&s_n, __popcll(m));
         base = __shfl(base, 0);
-        if (pend) s_list[base + __popcll(m & ((1ULL << lane) - 1))] = (int)(i & 255);
+        if (pend) {
+            const int q = base + __popcll(m & ((1ULL << lane) - 1));
+            s_list[q] = (int)(i & 255);
+            s_mv[q] = mv;
+        }
         __syncthreads();
         const int tot = s_n;
         const int64_t i0 = i - threadIdx.x;
         const int t = threadIdx.x;
         if (a.cert_block >= 16 && tot <= 16) {
-            if (t < tot * 16) cert_scan_group<MD, 16>(a, g, S, i0 + s_list[t >> 4], t & 15, kmin_c, kmax);
+            if (t < tot * 16) cert_scan_group<MD, 16>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
         } else if (a.cert_block >= 8 && tot <= 32) {
-            if (t < tot * 8) cert_scan_group<MD, 8>(a, g, S, i0 + s_list[t >> 3], t & 7, kmin_c, kmax);
+            if (t < tot * 8) cert_scan_group<MD, 8>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
         } else if (a.cert_block >= 4 && tot <= 64) {
-            if (t < tot * 4) cert_scan_group<MD, 4>(a, g, S, i0 + s_list[t >> 2], t & 3, kmin_c, kmax);
+            if (t < tot * 4) cert_scan_group<MD, 4>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
         } else if (a.cert_block >= 2 && tot <= 128) {
-            if (t < tot * 2) cert_scan_group<MD, 2>(a, g, S, i0 + s_list[t >> 1], t & 1, kmin_c, kmax);
+            if (t < tot * 2) cert_scan_group<MD, 2>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
         } else if (t < tot) {
-            cert_scan<MD>(a, g, S, i0 + s_list[threadIdx.x], true, kmin_c, kmax);
+            cert_scan<MD>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
         }
     } else if (i < a.n) {
         if (a.gap && !a.warm_c) {

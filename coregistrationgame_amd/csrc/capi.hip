@@ -474,20 +474,25 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1);
     int64_t j = 0;
     bool finished = nstages <= 0;
-    for (; j < cap && !finished; ++j) {
-        // selection path without traces: the selection's last kernel also runs the loop
-        // step and stores the done flag straight into the pinned ring.  FICP_FUSE_FIT=1
-        // also moves the rigid fit into gather + final (no k_fit_sums pass): measured
-        // slower at C3 (gather +7 us, final +8.5 us vs the 12 us pass), so off by default.
-        const bool fused = sel && !tidx;
+    // selection path without traces: the selection's last kernel also runs the loop step
+    // and stores the done flag straight into the pinned ring.  FICP_FUSE_FIT=1 also moves
+    // the rigid fit into gather + final (no k_fit_sums pass): measured slower at C3
+    // (gather +7 us, final +8.5 us vs the 12 us pass), so off by default.
+    const bool fused = sel && !tidx;
+    // part A of iteration i: the fit and the NN call; part B: the selection (and, not
+    // fused, the loop step and the flag copy)
+    auto enq_a = [&](int64_t i) -> int {
         if (!(fused && fuse_fit)) {
             ProfScope ps(c, P_FIT, "fit");
             HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, &dst->no_fit, c->stream));
         }
-        const int slot = (int)(j % kLoopRing);
-        if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
-        CHK(nn_call(c, wx, wy, wz, n, dst->T, true, j == 0 ? 1 : 2, &dst->done, &dst->apply,
+        CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
                     !sel, tidx != nullptr || !sel));
+        return FICP_OK;
+    };
+    auto enq_b = [&](int64_t i) -> int {
+        const int slot = (int)(i % kLoopRing);
+        if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
         if (sel) {
             ProfScope ps(c, P_SORT, "select");
             HIPCHK(launch_select(c->key.as<unsigned long long>(), worig, c->r.as<double>(), n, 0.0,
@@ -504,20 +509,41 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             HIPCHK(launch_loop_update(dst, lc, c->stream));
             HIPCHK(hipMemcpyAsync(&c->h_flags[slot], &dst->done, 4, hipMemcpyDeviceToHost,
                                   c->stream));
+            // (fused: the final kernel stores the flag itself and the host polls the
+            // pinned word; no event record, each one costs an idle gap in the queue)
+            HIPCHK(hipEventRecord(c->loop_ev[slot], c->stream));
         }
-        // fused: the final kernel stores the flag itself, so the host polls the pinned word
-        // (no event record: each one costs an idle gap in the queue)
-        if (!fused) HIPCHK(hipEventRecord(c->loop_ev[slot], c->stream));
-        if (j >= la) {
-            const int old = (int)((j - la) % kLoopRing);
-            if (fused) {
-                int v = 0;
-                CHK(poll_flag(c, &c->h_flags[old], v));
-                finished = v != 0;
-            } else {
-                HIPCHK(hipEventSynchronize(c->loop_ev[old]));
-                finished = c->h_flags[old] != 0;
-            }
+        return FICP_OK;
+    };
+    auto wait_flag = [&](int64_t i) -> int {
+        const int old = (int)(i % kLoopRing);
+        if (fused) {
+            int v = 0;
+            CHK(poll_flag(c, &c->h_flags[old], v));
+            finished = v != 0;
+        } else {
+            HIPCHK(hipEventSynchronize(c->loop_ev[old]));
+            finished = c->h_flags[old] != 0;
+        }
+        return FICP_OK;
+    };
+    static const bool half_env = !getenv("FICP_HALFSTEP") || atoi(getenv("FICP_HALFSTEP")) != 0;
+    if (fused && la == 1 && half_env) {
+        // half-step lookahead: iteration i's selection, then i+1's fit and NN, then wait
+        // for i's flag.  The device runs that fit + NN (>= 30 us) while the host wakes and
+        // enqueues the next selection, and a finished run leaves two no-op launches
+        // queued instead of a whole iteration's seven
+        if (!finished && cap > 0) CHK(enq_a(0));
+        for (; j < cap && !finished; ++j) {
+            CHK(enq_b(j));
+            if (j + 1 < cap) CHK(enq_a(j + 1));
+            CHK(wait_flag(j));
+        }
+    } else {
+        for (; j < cap && !finished; ++j) {
+            CHK(enq_a(j));
+            CHK(enq_b(j));
+            if (j >= la) CHK(wait_flag(j - la));
         }
     }
     // one host round trip for everything the run reports: the caller-order XY, the loop

@@ -466,11 +466,12 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     const bool fuse_fit = getenv("FICP_FUSE_FIT") && atoi(getenv("FICP_FUSE_FIT")) != 0;
     // Iterations are enqueued `la` ahead of the one whose done flag the host reads, so
     // the device never waits for the host; the iterations enqueued past the end are
-    // no-ops (every kernel tests the flags k_loop_update set).  One ahead suffices once an
-    // iteration outlasts the host's seven launches (~35 us; ~120 us at 1M rows) and
-    // leaves one no-op iteration at the end instead of two (C3: +0.8 %).
+    // no-ops (every kernel tests the flags k_loop_update set).  la = 1 with the fused
+    // selection runs the half-step form below; it needs the fit + NN of an iteration to
+    // outlast the host's wake-up and five launches (~20 us): from 64k rows (C2 100k:
+    // equal to la = 2; C3: +1.5 % over whole-iteration lookahead).
     static const int la_env = getenv("FICP_LOOKAHEAD") ? std::max(1, atoi(getenv("FICP_LOOKAHEAD"))) : 0;
-    const int la = std::min(kLoopRing - 1, la_env ? la_env : (n >= (1 << 18) ? 1 : 2));
+    const int la = std::min(kLoopRing - 1, la_env ? la_env : (n >= (1 << 16) ? 1 : 2));
     const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1);
     int64_t j = 0;
     bool finished = nstages <= 0;

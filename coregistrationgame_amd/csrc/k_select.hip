@@ -69,7 +69,8 @@ constexpr int NB_LOG = 13;
 constexpr int HT = 512;      // threads of the bounds / final kernels (at 1024 they spilled)
 constexpr int NWAVE = HT / 64;
 constexpr int HHT = 1024;    // threads of the histogram kernel (33 VGPRs)
-constexpr int CAP = 4096;    // candidates sorted in LDS
+constexpr int CAP = 4096;    // candidates sorted in LDS with their r (the common case)
+constexpr int CAP2 = 8192;   // candidates sorted in LDS with r left in global memory
 constexpr int NSB = 2048;    // bins of the LDS bucket sort
 constexpr int NSB_LOG = 11;
 constexpr int NS = 4096;     // sub-bins of one refinement level
@@ -1000,15 +1001,20 @@ __device__ __forceinline__ void publish(IterState *st, const FinalIn &in, double
     st->torig = (long long)torig;
 }
 
-// LDS layout of the final kernel (bytes)
-constexpr int L_K = 0;                          // u64[CAP]
-constexpr int L_R = L_K + CAP * 8;              // f64[CAP]
-constexpr int L_O = L_R + CAP * 8;              // u32[CAP]
-constexpr int L_POS = L_O + CAP * 4;            // u16[CAP]
-constexpr int L_MEM = L_POS + CAP * 2;          // u16[CAP]
-constexpr int L_BC = L_MEM + CAP * 2;           // u32[NSB] counts / fill
-constexpr int L_BO = L_BC + NSB * 4;            // u32[NSB] offsets
-constexpr int L_END = L_BO + NSB * 4;
+// LDS layout of the final kernel's sort (bytes) for CAPT candidates, r in LDS or not
+template <int CAPT, bool RL>
+struct LdsLay {
+    static constexpr int K = 0;                               // u64[CAPT]
+    static constexpr int R = K + CAPT * 8;                    // f64[CAPT] (RL)
+    static constexpr int O = R + (RL ? CAPT * 8 : 0);         // u32[CAPT]
+    static constexpr int POS = O + CAPT * 4;                  // u16[CAPT]
+    static constexpr int MEM = POS + CAPT * 2;                // u16[CAPT]
+    static constexpr int BC = MEM + CAPT * 2;                 // u32[NSB] counts / fill
+    static constexpr int BO = BC + NSB * 4;                   // u32[NSB] offsets
+    static constexpr int END = BO + NSB * 4;
+};
+constexpr int L_END = LdsLay<CAP, true>::END > LdsLay<CAP2, false>::END ? LdsLay<CAP, true>::END
+                                                                         : LdsLay<CAP2, false>::END;
 // refinement: u32[NS] counts + f64[NS] sums + u32 counter (aliases the above)
 constexpr int R_C = 0;
 constexpr int R_S = NS * 4;
@@ -1023,16 +1029,22 @@ constexpr int X_END = X_T + 256 * 4;
 constexpr int SMEM = L_END > R_END ? (L_END > X_END ? L_END : X_END) : (R_END > X_END ? R_END : X_END);
 static_assert(SMEM <= 150 * 1024, "final kernel LDS");
 
-// (a) c <= CAP candidates: bucket sort in LDS, exact prefix sums, first minimum
+// (a) c <= CAPT candidates: bucket sort in LDS, exact prefix sums, first minimum.  RL:
+// r is staged in LDS too (c <= CAP); otherwise (c <= CAP2) r is read from global memory
+// in sorted order and the prefix sums overwrite the keys.  Flat FRMSD curves (lambda
+// near 1) leave thousands of candidates that no bound separates: the in-workgroup radix
+// sort took ~220 us for 5.4k of them, this path ~2x the small one.
+template <int CAPT, bool RL>
 __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsigned char *sm,
                           Scr &scr, IterState *st) {
-    u64 *lk = (u64 *)(sm + L_K);
-    double *lr = (double *)(sm + L_R);
-    uint32_t *lo = (uint32_t *)(sm + L_O);
-    uint16_t *pos = (uint16_t *)(sm + L_POS);
-    uint16_t *mem = (uint16_t *)(sm + L_MEM);
-    unsigned *bc = (unsigned *)(sm + L_BC);
-    unsigned *bo = (unsigned *)(sm + L_BO);
+    using LY = LdsLay<CAPT, RL>;
+    u64 *lk = (u64 *)(sm + LY::K);
+    double *lr = (double *)(sm + LY::R);
+    uint32_t *lo = (uint32_t *)(sm + LY::O);
+    uint16_t *pos = (uint16_t *)(sm + LY::POS);
+    uint16_t *mem = (uint16_t *)(sm + LY::MEM);
+    unsigned *bc = (unsigned *)(sm + LY::BC);
+    unsigned *bo = (unsigned *)(sm + LY::BO);
     const int t = threadIdx.x;
     u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
     for (unsigned i = t; i < c; i += HT) {
@@ -1040,7 +1052,7 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
         const uint32_t o = src.o[i];
         lk[i] = k;
         lo[i] = o;
-        lr[i] = src.r[i];
+        if (RL) lr[i] = src.r[i];
         kmn = k < kmn ? k : kmn;
         kmx = k > kmx ? k : kmx;
         omn = o < omn ? o : omn;
@@ -1099,13 +1111,13 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
     __syncthreads();
     SELPROF(3);
     // exact prefix sums in sorted order, FRMSD of every candidate k
-    constexpr int PP = CAP / HT;  // 4 positions per thread
+    constexpr int PP = CAPT / HT;  // positions per thread
     double v[PP];
     double tsum = 0.0;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
         const unsigned p = (unsigned)(t * PP + q);
-        v[q] = p < c ? lr[pos[p]] : 0.0;
+        v[q] = p < c ? (RL ? lr[pos[p]] : src.r[pos[p]]) : 0.0;
         tsum = tsum + v[q];
     }
     double all;
@@ -1114,7 +1126,7 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
     // FRMSD of every position with the positions dealt over all lanes (a thread's own
     // PP positions would run PP dependent pow() chains back to back)
     __syncthreads();
-    double *ls = lr;
+    double *ls = RL ? lr : (double *)lk;  // (!RL: the keys are read from global below)
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
         const unsigned p = (unsigned)(t * PP + q);
@@ -1145,7 +1157,7 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
         uint32_t to = 0;
         if (bk != 0x7fffffffffffffffLL) {
             const unsigned e = pos[(unsigned)(bk - in.K0 - 1)];
-            tk = lk[e];
+            tk = RL ? lk[e] : src.k[e];
             to = lo[e];
         }
         publish(st, in, bf, bk, tk, to);
@@ -1494,7 +1506,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
         Cand src{w.ka, w.oa, w.ra, w.pa}, dst{w.kb, w.ob, w.rb, w.pb};
         int lev = 0;
         bool stalled = false;
-        while (c > (unsigned)CAP && lev < MAXLEV && !stalled) {
+        while (c > (unsigned)CAP2 && lev < MAXLEV && !stalled) {
             stalled = !refine(src, dst, c, in, sm, scr);
             if (!stalled) ++lev;
             __threadfence_block();
@@ -1502,7 +1514,9 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
         }
         if (t == 0) w.ctl->levels += lev;
         if (c <= (unsigned)CAP) {
-            final_lds(src, c, in, sm, scr, &s_st);
+            final_lds<CAP, true>(src, c, in, sm, scr, &s_st);
+        } else if (c <= (unsigned)CAP2) {
+            final_lds<CAP2, false>(src, c, in, sm, scr, &s_st);
         } else {
             if (t == 0) w.ctl->radix += 1;
             final_radix(src, dst, c, in, sm, scr, &s_st);

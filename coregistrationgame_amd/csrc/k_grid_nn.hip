@@ -1026,17 +1026,32 @@ __global__ __launch_bounds__(256) void k_minmax2_partial(const double *x, const 
                                                          double *oz) {
     __shared__ double s[4][256];
     double a0 = INFINITY, a1 = -INFINITY, b0 = INFINITY, b1 = -INFINITY;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (int64_t)gridDim.x * 256) {
-        const double vx = x[i], vy = y[i];
-        if (ox) {
-            ox[i] = vx;
-            oy[i] = vy;
-            if (z && oz) oz[i] = z[i];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    // 4 grid-stride rows in flight per thread (one at a time serialised 4 latencies)
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < m; i0 += 4 * stride) {
+        double xs[4], ys[4], zs[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + u * stride;
+            xs[u] = i < m ? x[i] : NAN;
+            ys[u] = i < m ? y[i] : NAN;
+            zs[u] = (i < m && ox && z && oz) ? z[i] : 0.0;
         }
-        a0 = fmin(a0, vx);
-        a1 = fmax(a1, vx);
-        b0 = fmin(b0, vy);
-        b1 = fmax(b1, vy);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i >= m) continue;
+            const double vx = xs[u], vy = ys[u];
+            if (ox) {
+                ox[i] = vx;
+                oy[i] = vy;
+                if (z && oz) oz[i] = zs[u];
+            }
+            a0 = fmin(a0, vx);
+            a1 = fmax(a1, vx);
+            b0 = fmin(b0, vy);
+            b1 = fmax(b1, vy);
+        }
     }
     s[0][threadIdx.x] = a0;
     s[1][threadIdx.x] = a1;

@@ -1047,9 +1047,20 @@ static_assert(SMEM <= 150 * 1024, "final kernel LDS");
 // in sorted order and the prefix sums overwrite the keys.  Flat FRMSD curves (lambda
 // near 1) leave thousands of candidates that no bound separates: the in-workgroup radix
 // sort took ~220 us for 5.4k of them, this path ~2x the small one.
+// result of one sorted scan: first minimum (bf, bk; every thread), its threshold pair
+// (tk, to; thread 0) and the sum of the scanned r (every thread)
+struct ScanOut {
+    double bf;
+    long long bk;
+    u64 tk;
+    uint32_t to;
+    double total;
+};
+
+// sort c <= CAPT candidates in LDS and scan them from (K0, S0): positions K0 + 1 .. K0 + c
 template <int CAPT, bool RL>
-__device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsigned char *sm,
-                          Scr &scr, IterState *st) {
+__device__ ScanOut lds_sort_scan(const Cand &src, unsigned c, long long K0, double S0,
+                                 const FinalIn &in, unsigned char *sm, Scr &scr) {
     using LY = LdsLay<CAPT, RL>;
     u64 *lk = (u64 *)(sm + LY::K);
     double *lr = (double *)(sm + LY::R);
@@ -1151,8 +1162,8 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
     double bf = INFINITY;
     long long bk = 0x7fffffffffffffffLL;
     for (unsigned p = t; p < c; p += HT) {
-        const long long k = in.K0 + (long long)p + 1;
-        const double f = frmsd_of(k, in.N, in.S0 + ls[p], in.lam);
+        const long long k = K0 + (long long)p + 1;
+        const double f = frmsd_of(k, in.N, S0 + ls[p], in.lam);
         if (f < bf) {
             bf = f;
             bk = k;
@@ -1160,21 +1171,149 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
     }
     SELPROF(4);
     blk_argmin(bf, bk, scr);
-    if (in.fs.on && bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
+    ScanOut r{bf, bk, 0, 0, all};
+    if (t == 0 && bk != 0x7fffffffffffffffLL) {
+        const unsigned e = pos[(unsigned)(bk - K0 - 1)];
+        r.tk = RL ? lk[e] : src.k[e];
+        r.to = lo[e];
+    }
+    return r;
+}
+
+// (a) c <= CAPT candidates: one sorted scan, the fused fit's selected candidates, publish
+template <int CAPT, bool RL>
+__device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsigned char *sm,
+                          Scr &scr, IterState *st) {
+    const ScanOut r = lds_sort_scan<CAPT, RL>(src, c, in.K0, in.S0, in, sm, scr);
+    if (in.fs.on && r.bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
+        const uint16_t *pos = (const uint16_t *)(sm + LdsLay<CAPT, RL>::POS);
         double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (unsigned q = t; q < (unsigned)(bk - in.K0); q += HT) fit_row(cf, in.fs, src.p[pos[q]]);
+        for (unsigned q = threadIdx.x; q < (unsigned)(r.bk - in.K0); q += HT)
+            fit_row(cf, in.fs, src.p[pos[q]]);
         blk_sum8_add(cf, in.fsum, scr);
     }
-    if (t == 0) {
-        u64 tk = 0;
-        uint32_t to = 0;
-        if (bk != 0x7fffffffffffffffLL) {
-            const unsigned e = pos[(unsigned)(bk - in.K0 - 1)];
-            tk = RL ? lk[e] : src.k[e];
-            to = lo[e];
-        }
-        publish(st, in, bf, bk, tk, to);
+    if (threadIdx.x == 0) publish(st, in, r.bf, r.bk, r.tk, r.to);
+}
+
+// (a') more than CAP2 candidates that refinement could not narrow (flat FRMSD curves at
+// millions of rows, ties): counted into NS sub-bins of the (key, orig) order, moved into
+// dst in sub-bin order, and scanned as consecutive groups of <= CAP2 (a group starts at
+// the sub-bin holding every multiple of CAP2 / 2 of the prefix count, so no sub-bin may
+// exceed CAP2 / 2),
+// carrying k and the exact sum from group to group.  Returns false (nothing published)
+// when a sub-bin is too large or there are too many groups: the radix path takes it.
+constexpr int MAXGRP = 512;
+__device__ bool final_chunked(const Cand &src, const Cand &dst, unsigned c, const FinalIn &in,
+                              unsigned char *sm, Scr &scr, IterState *st, unsigned *g_beg) {
+    constexpr unsigned H = CAP2 / 2;
+    unsigned *cnt = (unsigned *)sm;        // [NS] (the sort area is free until the groups)
+    unsigned *off = cnt + NS;              // [NS]
+    unsigned *fil = off + NS;              // [NS]
+    __shared__ unsigned s_ng, s_bad;
+    const int t = threadIdx.x;
+    u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
+    for (unsigned i = t; i < c; i += HT) {
+        const u64 k = src.k[i];
+        const uint32_t o = src.o[i];
+        kmn = k < kmn ? k : kmn;
+        kmx = k > kmx ? k : kmx;
+        omn = o < omn ? o : omn;
+        omx = o > omx ? o : omx;
     }
+    for (int b = t; b < NS; b += HT) {
+        cnt[b] = 0u;
+        fil[b] = 0u;
+    }
+    if (t == 0) {
+        s_ng = 0u;
+        s_bad = 0u;
+    }
+    blk_minmax2_u64(kmn, kmx, omn, omx, scr);
+    const Comp cmp = make_comp(kmn, kmx, (uint32_t)omn, (uint32_t)omx);
+    const int vb = bits_of(cmp(kmx, (uint32_t)omx));
+    const int sh = vb > NS_LOG ? vb - NS_LOG : 0;
+    for (unsigned i = t; i < c; i += HT) atomicAdd(&cnt[(int)(cmp(src.k[i], src.o[i]) >> sh)], 1u);
+    __syncthreads();
+    {
+        constexpr int PB = NS / HT;
+        unsigned v[PB];
+        long long tot = 0;
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            v[j] = cnt[t * PB + j];
+            tot += v[j];
+        }
+        long long all;
+        long long ex = blk_excl_scan_ll(tot, scr, all);
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const int b = t * PB + j;
+            off[b] = (unsigned)ex;
+            if (v[j] > H) atomicOr(&s_bad, 1u);
+            // groups begin at offset 0 and at every sub-bin that holds a multiple m H
+            // (m >= 1) of the prefix count: consecutive starts are < 2 H = CAP2 apart
+            // because a sub-bin holds at most H rows
+            const unsigned exu = (unsigned)ex, vv = v[j];
+            bool start = false;
+            if (vv) {
+                const unsigned m = (exu + H - 1) / H;
+                start = exu == 0 || m * H < exu + vv;
+            }
+            if (start) {
+                const unsigned gi = atomicAdd(&s_ng, 1u);
+                if (gi < (unsigned)MAXGRP) g_beg[gi] = exu;
+            }
+            ex += v[j];
+        }
+    }
+    __syncthreads();
+    const unsigned ng = s_ng;
+    if (s_bad || ng > (unsigned)MAXGRP) return false;
+    // group starts in ascending order (few: an insertion sort by thread 0)
+    if (t == 0) {
+        for (unsigned a = 1; a < ng; ++a) {
+            const unsigned x = g_beg[a];
+            unsigned b = a;
+            while (b > 0 && g_beg[b - 1] > x) {
+                g_beg[b] = g_beg[b - 1];
+                --b;
+            }
+            g_beg[b] = x;
+        }
+        g_beg[ng] = c;
+    }
+    for (unsigned i = t; i < c; i += HT) {
+        const u64 k = src.k[i];
+        const uint32_t o = src.o[i];
+        const int b = (int)(cmp(k, o) >> sh);
+        const unsigned q = off[b] + atomicAdd(&fil[b], 1u);
+        dst.k[q] = k;
+        dst.o[q] = o;
+        dst.r[q] = src.r[i];
+        dst.p[q] = src.p[i];
+    }
+    __threadfence_block();
+    __syncthreads();
+    double carry = 0.0, bf = INFINITY;
+    long long bk = 0x7fffffffffffffffLL;
+    u64 tk = 0;
+    uint32_t to = 0;
+    for (unsigned gi = 0; gi < ng; ++gi) {
+        const unsigned a = g_beg[gi], e = g_beg[gi + 1];
+        const Cand sub{dst.k + a, dst.o + a, dst.r + a, dst.p + a};
+        const ScanOut r = lds_sort_scan<CAP2, false>(sub, e - a, in.K0 + (long long)a,
+                                                    in.S0 + carry, in, sm, scr);
+        if (t == 0 && better(r.bf, r.bk, bf, bk)) {
+            bf = r.bf;
+            bk = r.bk;
+            tk = r.tk;
+            to = r.to;
+        }
+        carry = carry + r.total;
+        __syncthreads();
+    }
+    if (t == 0) publish(st, in, bf, bk, tk, to);
+    return true;
 }
 
 // (b) one refinement level over c > CAP candidates in global memory: returns false when
@@ -1485,6 +1624,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     __shared__ Scr scr;
     __shared__ IterState s_st;  // thread 0's working copy of the state (one load, one store)
     __shared__ double s_fit[8];  // fused fit sums (thread 0)
+    __shared__ unsigned s_gbeg[MAXGRP + 1];  // group starts of the chunked scan
     const int t = threadIdx.x;
     SELPROF(0);
     if (t == 0) s_st = *st;
@@ -1530,6 +1670,8 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
             final_lds<CAP, true>(src, c, in, sm, scr, &s_st);
         } else if (c <= (unsigned)CAP2) {
             final_lds<CAP2, false>(src, c, in, sm, scr, &s_st);
+        } else if (!fs.on && final_chunked(src, dst, c, in, sm, scr, &s_st, s_gbeg)) {
+            if (t == 0) w.ctl->levels += 1u << 16;  // statistics: chunked scans (high half)
         } else {
             if (t == 0) w.ctl->radix += 1;
             final_radix(src, dst, c, in, sm, scr, &s_st);

@@ -140,8 +140,8 @@ def test_grid_clustered_layers(ctx, oracle):
 def test_selection_selfcheck():
     """tools/selcheck: the bucketed FRMSD selection (k_select.hip) against a CPU sort on
     residual distributions that exercise its refinement and radix paths (zeros, all
-    equal, five distinct values, 20 decades) and the 4097-8192-candidate LDS path (flat
-    FRMSD curves at 1M rows, lambda 0.95 and 1.3)."""
+    equal, five distinct values, 20 decades), the 4097-8192-candidate LDS path (flat
+    FRMSD curves at 1M rows, lambda 0.95 and 1.3) and the chunked scan (8M rows)."""
     import subprocess
     from pathlib import Path
     exe = Path(__file__).resolve().parents[1] / "tools" / "selcheck"
@@ -149,7 +149,8 @@ def test_selection_selfcheck():
         pytest.skip("tools/selcheck not built (make -C coregistrationgame_amd/csrc selcheck)")
     for args in (["200000", "3", "0", "3.0"], ["200000", "3", "0", "0.95"], ["100000", "3", "1", "3.0"],
                  ["50000", "2", "2", "3.0"], ["100000", "2", "3", "0.95"], ["200000", "3", "5", "1.3"],
-                 ["3000", "3", "4", "3.0"], ["1000000", "2", "0", "0.95"], ["1000000", "2", "0", "1.3"]):
+                 ["3000", "3", "4", "3.0"], ["1000000", "2", "0", "0.95"], ["1000000", "2", "0", "1.3"],
+                 ["8000000", "2", "0", "3.0"]):
         r = subprocess.run([str(exe)] + args, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stdout + r.stderr
 

@@ -177,10 +177,10 @@ int main(int argc, char **argv) {
     SelCtl ctl;
     CK(hipMemcpy(&ctl, w.ctl, sizeof ctl, hipMemcpyDeviceToHost));
     const char *names[4] = {"hist+red", "bounds", "gather", "final"};
-    printf("n=%lld mode=%d lam=%g k=%lld cand=%u buckets=[%d,%d] levels=%u radix=%u err=%u "
-           "bad=%d/%d\n",
-           (long long)n, mode, lam, bk, ctl.ccount, ctl.b0, ctl.b1, stats[1], stats[2], stats[0],
-           bad, reps);
+    printf("n=%lld mode=%d lam=%g k=%lld cand=%u buckets=[%d,%d] levels=%u chunked=%u radix=%u "
+           "err=%u bad=%d/%d\n",
+           (long long)n, mode, lam, bk, ctl.ccount, ctl.b0, ctl.b1, stats[1] & 0xffffu,
+           stats[1] >> 16, stats[2], stats[0], bad, reps);
     float tot = 0.f;
     for (int q = 0; q < 4; ++q) {
         std::sort(tk[q].begin(), tk[q].end());

@@ -1627,7 +1627,11 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     __shared__ unsigned s_gbeg[MAXGRP + 1];  // group starts of the chunked scan
     const int t = threadIdx.x;
     SELPROF(0);
-    if (t == 0) s_st = *st;
+    // the state copied word by word by all threads (thread 0 alone issued ~35 dependent
+    // 16-B loads here and as many stores at the end: ~1 us each way)
+    static_assert(sizeof(IterState) % 4 == 0, "IterState words");
+    constexpr int SW = (int)(sizeof(IterState) / 4);
+    for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
     if (t < 8) s_fit[t] = 0.0;
     double a = 0.0;
     for (int p = t; p < nparts; p += HT) a = a + w.parts[p];  // fixed order per thread
@@ -1683,10 +1687,11 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
         // fused fit: T of the next loop body from this selection (k_fit_sums' work)
         if (fs.on && !s_st.no_fit && s_st.k > 0)
             fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
-        *st = s_st;
-        if (host_flag)
-            __hip_atomic_store(host_flag, s_st.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    __syncthreads();
+    for (int q = t; q < SW; q += HT) ((uint32_t *)st)[q] = ((const uint32_t *)&s_st)[q];
+    if (t == 0 && host_flag)
+        __hip_atomic_store(host_flag, s_st.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     SELPROF(6);
 }
 

@@ -380,6 +380,30 @@ def test_device_resident_path_matches_host_path(md):
         ctx.close()
 
 
+def test_run_many_stages_matches_split_runs():
+    """Six stages in one ficp_run (lambdas past the fourth come from the device array, the
+    first four from the kernel arguments) equal the same stages run as two calls."""
+    from coregistrationgame_amd import _lib, synth
+    p = synth.make_plot(80_000, 90_000, 0.7, seed=31, md=3)
+    lams = [3.0, 0.95, 1.3, 2.0, 0.95, 3.0]
+    one = p.source.copy()
+    c1 = _lib.Context(0)
+    c1.set_target(p.target, 3)
+    s1 = c1.run(one, lams, 1e-6, 1000, False)
+    c1.close()
+    two = p.source.copy()
+    c2 = _lib.Context(0)
+    c2.set_target(p.target, 3)
+    a = c2.run(two, lams[:2], 1e-6, 1000, False)
+    b = c2.run(two, lams[2:], 1e-6, 1000, False)
+    c2.close()
+    # the second call rebuilds the work order from moved positions, so the fit's sums
+    # run in another order: XY agree to the north-star bar, not bit for bit
+    assert s1["n_nn_calls"] == a["n_nn_calls"] + b["n_nn_calls"]
+    np.testing.assert_allclose(one[:, :2], two[:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(bits(one[:, 2]), bits(p.source[:, 2]))
+
+
 def test_run_1M_properties():
     """C3 (1M x 1M, f=0.6, to convergence): the run undoes the synthetic misregistration
     (size-independent property) and a second run from its output is a fixed point."""

@@ -83,6 +83,12 @@ def nn_bytes_per_launch(n, m, md):
     return n * (8 * md + 16 + 12) + m * 8 * md
 
 
+def iteration_bytes(n, m, md, k):
+    """SURVEY.md §8(d)'s algorithmic HBM bytes of one ICP loop body (reference algorithm:
+    apply, NN, sort, prefix scan, fit gather): N (32 + 8 md + 12 + 24 + 16 + 32 k/N) + 8 md M."""
+    return n * (32 + 8 * md + 12 + 24 + 16) + 32 * k + 8 * md * m
+
+
 def pmc_traffic(kernel_prefix):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC profile
     (profiles/*_pmc_*_nn.json, written from tools/pmc.sh output), or None."""
@@ -219,6 +225,14 @@ def bench_batch(args, rank, world, local, dist):
                          "launches": nn["count"], "algorithmic_bytes_per_launch": bytes_launch,
                          "note": "bytes count every tree of the rank as live"},
             "kernel_ms": prof,
+            # the whole loop body against SURVEY.md §8(d)'s per-iteration bytes (k = n: the
+            # upper bound of the fit term), for reference beside the dominant kernel's line
+            # (per plot-iteration here)
+            "iteration_roofline": {"bytes_per_iteration": iteration_bytes(n, m, md, n),
+                                   "achieved": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9,
+                                   "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                                   "frac": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9
+                                   / HBM_PEAK_GBS},
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -409,6 +423,13 @@ def main():
                          "timed_launches_incl_noop": nn["count"],
                          "algorithmic_bytes_per_launch": bytes_launch},
             "kernel_ms": prof,
+            # the whole loop body against SURVEY.md §8(d)'s per-iteration bytes (k = n: the
+            # upper bound of the fit term), for reference beside the dominant kernel's line
+            "iteration_roofline": {"bytes_per_iteration": iteration_bytes(n, m, md, n),
+                                   "achieved": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9,
+                                   "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                                   "frac": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9
+                                   / HBM_PEAK_GBS},
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -516,7 +516,6 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
                                                  const int *skip, HistPack hp) {
     if (skip && *skip) return;
     __shared__ u64 sp[NB];
-    __shared__ short se[NB];
     __shared__ u64 s_u[HHT / 64], s_v[HHT / 64];
     u64 kmin, kmax;
     if (nparts > 0) {
@@ -549,10 +548,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
         kmax = range[1];
     }
     const int s = sel_shift(kmin, kmax);
-    for (int b = threadIdx.x; b < NB; b += HHT) {
-        sp[b] = 0ULL;
-        se[b] = (short)bucket_exp(kmin, kmax, s, b);
-    }
+    for (int b = threadIdx.x; b < NB; b += HHT) sp[b] = 0ULL;
     const u64 one = 1ULL << hp.shift;
     __syncthreads();
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -574,7 +570,9 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
         for (int u = 0; u < U; ++u) {
             if (i + (int64_t)u * HHT < i1) {
                 const int b = (int)((kk[u] - kmin) >> s);
-                const int e = se[b];
+                // r < 2^e for every row of the bucket, from the bucket's upper key bits
+                // (a per-bucket LDS table cost its init and 16 KB: +1 % without it)
+                const int e = bucket_exp(kmin, kmax, s, b);
                 const u64 m = (e < 1024 && rv[u] < INFINITY) ? (u64)ldexp(rv[u], hp.fixb - e) : 0ULL;
                 atomicAdd(&sp[b], one + m);
             }

@@ -218,6 +218,24 @@ def test_fit_golden(ctx):
         np.testing.assert_array_equal(T[2], [0.0, 0.0, 1.0])
 
 
+def test_fit_arrival_many_grid_sizes(ctx, oracle):
+    """k_fit_sums' two-level arrival (8 group counters + a top counter, the last workgroup
+    solves) over 120 fits back to back whose sizes give 1 to ~100 workgroups (groups of
+    uneven size, fewer workgroups than groups) against the oracle's SVD fit."""
+    rng = np.random.default_rng(2024)
+    sizes = np.unique(np.r_[1, 2, 3, 4095, 4096, 4097, 8191, 8193, 3 * 4096 + 1,
+                            rng.integers(1, 400_000, 111)])
+    for k in sizes:
+        k = int(k)
+        src = rng.normal(0, 50, (k, 2)) + [6.4e5, 6.48e6]
+        th = rng.uniform(-0.1, 0.1)
+        R = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+        tgt = src @ R.T + rng.uniform(-3, 3, 2) + rng.normal(0, 0.3, (k, 2))
+        T = ctx.fit_rigid2d(src, tgt, False)
+        Tref = oracle.fit_rigid2d(src, tgt, False)
+        assert_T_close(T, Tref, src, msg=f"k={k}")
+
+
 def test_apply_golden_bit_exact():
     from coregistrationgame_amd import FractionalICP
     cases, _ = load_cases("apply")

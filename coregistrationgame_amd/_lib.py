@@ -79,6 +79,25 @@ def build(force: bool = False) -> Path:
 _lib = None
 
 
+def _bind_hip_runtime():
+    """Map PyTorch's HIP runtime before libficp.so, so that both use ONE runtime.
+
+    torch/lib ships its own libamdhip64 + libhsa-runtime64 and its libraries name them
+    as DT_NEEDED "libamdhip64.so", which the dynamic linker does not match with the
+    "libamdhip64.so.7" SONAME that libficp.so binds to in /opt/rocm.  Mapped in the
+    other order, a later `import torch` (partitioned.py, shard.py, the bench's
+    torch.distributed leg) maps a second HIP/HSA runtime into the process, and its
+    device initialisation fails ("No HIP GPUs are available").  With torch mapped
+    first, libficp.so's "libamdhip64.so.7" resolves to torch's already-loaded copy.
+    FICP_HIP_RUNTIME=system skips this (processes that never import torch)."""
+    if os.environ.get("FICP_HIP_RUNTIME", "") == "system":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib():
     """Load libficp.so (raises if it was not built)."""
     global _lib
@@ -87,6 +106,7 @@ def lib():
     if not LIB_PATH.exists():
         raise FicpError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                         " or `make -C coregistrationgame_amd/csrc` (no CPU fallback exists)")
+    _bind_hip_runtime()
     L = C.CDLL(str(LIB_PATH))
     sig = {
         "ficp_version": ([], C.c_int),
@@ -356,6 +376,9 @@ class Context:
 def _make_stats(n, trace, trace_idx, max_trace):
     st = Stats()
     keep = {}
+    if trace_idx and n > 0:
+        # the per-call idx trace is max_trace x n int32 on both sides: keep it <= ~1 GB
+        max_trace = max(64, min(max_trace, int(1e9) // (4 * n)))
     if trace:
         st.max_trace = max_trace
         keep["k"] = np.zeros(max_trace, np.int64)

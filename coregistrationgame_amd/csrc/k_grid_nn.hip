@@ -609,6 +609,30 @@ __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, con
     return true;
 }
 
+// cold start of a scan: the 3x3 cells around q, then rings until a stem is found
+template <int MD>
+__device__ __forceinline__ void cold_start(const GridView &g, const Stems &S, double qx, double qy,
+                                           double qz, int cx, int cy, Best2 &b) {
+    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, g.gy - 1); ++yy) {
+        const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
+        scan2<MD>(S, rw[max(cx - 1, 0)], rw[min(cx + 1, g.gx - 1) + 1], qx, qy, qz, b);
+    }
+    for (int r = 2; !(b.d2 < INFINITY); ++r) {
+        const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
+        if (xa < 0 && ya < 0 && xb >= g.gx && yb >= g.gy) break;  // empty layer
+        const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);
+        for (int yy = max(ya, 0); yy <= min(yb, g.gy - 1); ++yy) {
+            const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
+            if (yy == ya || yy == yb) {
+                scan2<MD>(S, rw[xlo], rw[xhi + 1], qx, qy, qz, b);
+            } else {
+                if (xa >= 0) scan2<MD>(S, rw[xa], rw[xa + 1], qx, qy, qz, b);
+                if (xb < g.gx) scan2<MD>(S, rw[xb], rw[xb + 1], qx, qy, qz, b);
+            }
+        }
+    }
+}
+
 // Step 2: the full scan of an uncertified query at its (already moved) position: warm
 // bound from the stored match (or the cold 3x3 start), every stem within d + pad
 // evaluated, the new bound G and the match slot stored, outputs written.
@@ -627,30 +651,21 @@ __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, co
     const int cx = cell_coord(qx, g.x0, g.inv_h, g.gx);
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
     const double mq = query_margin(g, qx, qy);
-    if (!(b.d2 < INFINITY)) {  // cold start: the 3x3 cells around q, then rings
-        for (int yy = max(cy - 1, 0); yy <= min(cy + 1, g.gy - 1); ++yy) {
-            const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
-            scan2<MD>(S, rw[max(cx - 1, 0)], rw[min(cx + 1, g.gx - 1) + 1], qx, qy, qz, b);
-        }
-        for (int r = 2; !(b.d2 < INFINITY); ++r) {
-            const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
-            if (xa < 0 && ya < 0 && xb >= g.gx && yb >= g.gy) break;  // empty layer
-            const int xlo = max(xa, 0), xhi = min(xb, g.gx - 1);
-            for (int yy = max(ya, 0); yy <= min(yb, g.gy - 1); ++yy) {
-                const int32_t *rw = g.cell_start + (int64_t)yy * g.gx;
-                if (yy == ya || yy == yb) {
-                    scan2<MD>(S, rw[xlo], rw[xhi + 1], qx, qy, qz, b);
-                } else {
-                    if (xa >= 0) scan2<MD>(S, rw[xa], rw[xa + 1], qx, qy, qz, b);
-                    if (xb < g.gx) scan2<MD>(S, rw[xb], rw[xb + 1], qx, qy, qz, b);
-                }
-            }
-        }
-    }
+    if (!(b.d2 < INFINITY)) cold_start<MD>(g, S, qx, qy, qz, cx, cy, b);
     double gnew = 0.0;
     if (b.d2 < INFINITY) {
-        const double rc = sqrt(b.d2) + pad;
+        double rc = sqrt(b.d2) + pad;
         cover_scan<MD>(g, S, qx, qy, qz, cy, mq, rc * rc, b);
+        if (b.slot < 0) {
+            // A warm bound whose stem the cover did not re-evaluate.  The cover contains
+            // the stored match (it lies at exactly sqrt(d2w) < rc), so this is not
+            // expected; should it happen, search again from scratch rather than write
+            // slot -1: the result is then the cold search's, still exact.
+            b = Best2{INFINITY, 0x7fffffff, -1, INFINITY};
+            cold_start<MD>(g, S, qx, qy, qz, cx, cy, b);
+            rc = sqrt(b.d2) + pad;
+            if (b.d2 < INFINITY) cover_scan<MD>(g, S, qx, qy, qz, cy, mq, rc * rc, b);
+        }
         gnew = fmin(sqrt(b.s2), rc - mq) - eps;
     }
     a.gap[i] = b.slot >= 0 ? gnew : 0.0;
@@ -720,8 +735,11 @@ __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView 
         b.slot = take ? oslot : b.slot;
     }
     if (lg != 0) return;
-    double gnew = 0.0;
-    if (b.slot >= 0) gnew = fmin(sqrt(b.s2), rc - mq) - eps;
+    if (b.slot < 0) {  // the stored match was not re-evaluated (not expected): cold search
+        cert_scan<MD>(a, g, S, i, false, pad, kmin_c, kmax);
+        return;
+    }
+    const double gnew = fmin(sqrt(b.s2), rc - mq) - eps;
     a.gap[i] = gnew;
     finish(a, S, i, qz, Best{b.d2, b.id, max(b.slot, 0)}, kmin_c, kmax);
 }

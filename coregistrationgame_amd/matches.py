@@ -30,7 +30,7 @@ def thresholds(plot_h, use_3d: bool, min_dist_percent=15) -> np.ndarray:
     """The per-tree distance limits of chm_plot.py:249 (3-D) and 273-282 (2-D)."""
     h = np.asarray(plot_h, dtype=np.float64)
     if not use_3d:
-        h = np.where(np.isfinite(h), h, 10.0)  # chm_plot.py:276-281: 10 m when missing
+        h = np.where(np.isnan(h), 10.0, h)  # chm_plot.py:276-281: 10 m when NaN (inf stays)
     return (min_dist_percent / 100.0) * h
 
 
@@ -41,7 +41,8 @@ def remove_matches_arrays(plot, chm, min_dist_percent=15, *, device=None) -> np.
         raise ValueError("plot and chm must be (N, 3) arrays of x, y, height.")
     if len(plot) == 0 or len(chm) == 0:
         return np.zeros(0, np.int64)
-    use_3d = bool(np.isfinite(plot[:, 2]).all() and np.isfinite(chm[:, 2]).all())
+    # chm_plot.py:236-244 tests np.isnan only: an infinite height keeps the 3-D search
+    use_3d = bool(not np.isnan(plot[:, 2]).any() and not np.isnan(chm[:, 2]).any())
     md = 3 if use_3d else 2
     ctx = _lib.Context(device, _lib.NN_GRID)
     try:

@@ -222,20 +222,42 @@ EXPORT int orc_kd_query(const void *tp, const double *src, int64_t n, int64_t ld
 }
 
 /* ---------------------------------------------------------------- ordering */
-static const double *g_sort_d;
-static int cmp_di(const void *a, const void *b) {
-    int64_t i = *(const int64_t *)a, j = *(const int64_t *)b;
-    double di = g_sort_d[i], dj = g_sort_d[j];
-    if (di < dj) return -1;
-    if (di > dj) return 1;
-    return (i > j) - (i < j);
+/* ficp.py:63,78 -- argsort(distances), ties by index (stable): the order of the
+   comparison (d_i < d_j) || (d_i == d_j && i < j).  Stable LSD radix sort (4 passes of 16
+   bits) over the order-preserving u64 image of each double, starting from index order,
+   so equal keys keep index order.  -0.0 maps to +0.0 (they compare equal). */
+static inline uint64_t ord_bits(double v) {
+    if (v == 0.0) v = 0.0;
+    uint64_t u;
+    memcpy(&u, &v, 8);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
-/* ficp.py:63,78 -- argsort(distances), ties by index (stable). Not thread safe. */
 EXPORT void orc_sort_order(const double *d, int64_t n, int64_t *order) {
-    for (int64_t i = 0; i < n; ++i) order[i] = i;
-    g_sort_d = d;
-    qsort(order, (size_t)n, sizeof(int64_t), cmp_di);
+    if (n <= 0) return;
+    uint64_t *key = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)n);
+    uint64_t *key2 = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)n);
+    int64_t *tmp = (int64_t *)malloc(sizeof(int64_t) * (size_t)n);
+    size_t *cnt = (size_t *)malloc(sizeof(size_t) * 65536);
+    for (int64_t i = 0; i < n; ++i) { order[i] = i; key[i] = ord_bits(d[i]); }
+    int64_t *src = order, *dst = tmp;
+    uint64_t *ks = key, *kd = key2;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int sh = 16 * pass;
+        memset(cnt, 0, sizeof(size_t) * 65536);
+        for (int64_t i = 0; i < n; ++i) cnt[(ks[i] >> sh) & 0xffff]++;
+        size_t run = 0;
+        for (int b = 0; b < 65536; ++b) { size_t c = cnt[b]; cnt[b] = run; run += c; }
+        for (int64_t i = 0; i < n; ++i) {
+            size_t at = cnt[(ks[i] >> sh) & 0xffff]++;
+            dst[at] = src[i];
+            kd[at] = ks[i];
+        }
+        int64_t *t = src; src = dst; dst = t;
+        uint64_t *tk = ks; ks = kd; kd = tk;
+    }
+    /* 4 passes: the result is back in `order` */
+    free(key); free(key2); free(tmp); free(cnt);
 }
 
 /* ---------------------------------------------------------------- fraction */
@@ -247,14 +269,16 @@ static inline double frmsd_val(double frac, double lam, double S, int64_t k) {
 /* ficp.py:73-86.  r_i = sum_md (src_i - corr_i)^2 (ficp.py:58-59).  N = len(self.source).
    literal != 0 recomputes every prefix sum from scratch (the O(N^2) cost model of
    ficp.py:80-85); the values are identical to the O(N) cumsum. */
-EXPORT int orc_optimal_fraction(const double *src, int64_t lds, const double *corr, int64_t ldc,
-                                const double *d, int64_t n, int64_t N, int md, double lam,
-                                int literal, double *frac_out, int64_t *k_out, double *frmsd_out) {
+static int optimal_fraction_ex(const double *src, int64_t lds, const double *corr, int64_t ldc,
+                               const double *d, int64_t n, int64_t N, int md, double lam, int literal,
+                               double *frac_out, int64_t *k_out, double *frmsd_out, double *gap_out,
+                               int64_t *order_out) {
     *frac_out = 0.0;
     *k_out = 0;
     if (frmsd_out) *frmsd_out = INFINITY;
+    if (gap_out) *gap_out = INFINITY;
     if (N == 0 || n == 0) return 0;
-    int64_t *order = (int64_t *)malloc(sizeof(int64_t) * (size_t)n);
+    int64_t *order = order_out ? order_out : (int64_t *)malloc(sizeof(int64_t) * (size_t)n);
     double *r = (double *)malloc(sizeof(double) * (size_t)n);
     orc_sort_order(d, n, order);
     for (int64_t j = 0; j < n; ++j) {
@@ -266,7 +290,7 @@ EXPORT int orc_optimal_fraction(const double *src, int64_t lds, const double *co
         }
         r[j] = acc;
     }
-    double best = INFINITY, bfrac = 0.0, S = 0.0;
+    double best = INFINITY, second = INFINITY, bfrac = 0.0, S = 0.0;
     int64_t bk = 0;
     for (int64_t k = 1; k <= N; ++k) {
         if (literal) {
@@ -278,14 +302,25 @@ EXPORT int orc_optimal_fraction(const double *src, int64_t lds, const double *co
         }
         double frac = (double)k / (double)N;
         double v = frmsd_val(frac, lam, S, k);
-        if (v < best) { best = v; bfrac = frac; bk = k; }
+        if (v < best) { second = best; best = v; bfrac = frac; bk = k; }
+        else if (v < second) second = v;
     }
-    free(order);
+    if (!order_out) free(order);
     free(r);
     *frac_out = bfrac;
     *k_out = bk;
     if (frmsd_out) *frmsd_out = best;
+    /* relative FRMSD gap between the best k and the runner-up: where it is at rounding
+       level the winning k is not pinned by any implementation (tests/conftest.py) */
+    if (gap_out) *gap_out = (best > 0.0 && isfinite(second)) ? (second - best) / best : INFINITY;
     return 0;
+}
+
+EXPORT int orc_optimal_fraction(const double *src, int64_t lds, const double *corr, int64_t ldc,
+                                const double *d, int64_t n, int64_t N, int md, double lam,
+                                int literal, double *frac_out, int64_t *k_out, double *frmsd_out) {
+    return optimal_fraction_ex(src, lds, corr, ldc, d, n, N, md, lam, literal, frac_out, k_out, frmsd_out,
+                               NULL, NULL);
 }
 
 /* ficp.py:54-60 */
@@ -382,6 +417,7 @@ typedef struct {
     double *lam;           /* [max_calls]                                        */
     double *T;             /* [max_calls * 9] fits (n_fits of them)              */
     int32_t *idx;          /* [max_calls * n] NN idx per call, nullable          */
+    double *gap;           /* [max_calls] FRMSD best vs runner-up (relative), nullable */
 } orc_trace;
 
 typedef struct {
@@ -404,26 +440,29 @@ static void run_nn(nnctx *c, const double *src, int64_t n, int64_t lds, int32_t 
 }
 
 static int64_t choose(nnctx *c, const double *src, int64_t n, int64_t lds, int32_t *idx, double *dist,
-                      double *d2, double *corr, int64_t *order, double lam, double *fr_out, double *frac_out) {
+                      double *d2, double *corr, int64_t *order, double lam, double *fr_out, double *frac_out,
+                      double *gap_out) {
     run_nn(c, src, n, lds, idx, dist, d2);
     for (int64_t i = 0; i < n; ++i)
         for (int t = 0; t < c->md; ++t) corr[i * 3 + t] = c->tgt[(int64_t)idx[i] * c->ldt + t];
     double frac, fr;
     int64_t k;
-    orc_optimal_fraction(src, lds, corr, 3, dist, n, n, c->md, lam, c->literal, &frac, &k, &fr);
-    orc_sort_order(dist, n, order);
+    /* the fraction's argsort is the selection's order too (ficp.py:63,78: same input) */
+    optimal_fraction_ex(src, lds, corr, 3, dist, n, n, c->md, lam, c->literal, &frac, &k, &fr, gap_out, order);
     *fr_out = fr;
     *frac_out = frac;
     return k;
 }
 
-static void trace_call(orc_trace *tr, int64_t k, double fr, double lam, const int32_t *idx, int64_t n) {
+static void trace_call(orc_trace *tr, int64_t k, double fr, double lam, const int32_t *idx, int64_t n,
+                       double gap) {
     if (!tr) return;
     int32_t c = tr->n_calls++;
     if (c >= tr->max_calls) return;
     if (tr->k) tr->k[c] = k;
     if (tr->frmsd) tr->frmsd[c] = fr;
     if (tr->lam) tr->lam[c] = lam;
+    if (tr->gap) tr->gap[c] = gap;
     if (tr->idx) memcpy(tr->idx + (int64_t)c * n, idx, sizeof(int32_t) * (size_t)n);
 }
 
@@ -438,9 +477,9 @@ static int iterate(nnctx *c, double *src, int64_t n, int64_t lds, double lam, do
     int64_t *order = (int64_t *)malloc(sizeof(int64_t) * (size_t)n);
     double *ss = (double *)malloc(sizeof(double) * (size_t)n * 2);
     double *cc = (double *)malloc(sizeof(double) * (size_t)n * 2);
-    double cur, frac;
-    int64_t k = choose(c, src, n, lds, idx, dist, d2, corr, order, lam, &cur, &frac);
-    trace_call(tr, k, cur, lam, idx, n);
+    double cur, frac, gap;
+    int64_t k = choose(c, src, n, lds, idx, dist, d2, corr, order, lam, &cur, &frac, &gap);
+    trace_call(tr, k, cur, lam, idx, n, gap);
     int it = 0;
     if (k > 0) {
         while (it < max_iter) {
@@ -458,8 +497,8 @@ static int iterate(nnctx *c, double *src, int64_t n, int64_t lds, double lam, do
             }
             orc_apply_xy(src, n, lds, T);
             double nw;
-            k = choose(c, src, n, lds, idx, dist, d2, corr, order, lam, &nw, &frac);
-            trace_call(tr, k, nw, lam, idx, n);
+            k = choose(c, src, n, lds, idx, dist, d2, corr, order, lam, &nw, &frac, &gap);
+            trace_call(tr, k, nw, lam, idx, n, gap);
             if (cur - nw <= thr) break;
             cur = nw;
             it++;

@@ -30,7 +30,7 @@ class OrcTrace(C.Structure):
     _fields_ = [
         ("max_calls", C.c_int32), ("n_calls", C.c_int32), ("n_fits", C.c_int32),
         ("iters", C.c_int32 * 2),
-        ("k", _ip64), ("frmsd", _dp), ("lam", _dp), ("T", _dp), ("idx", _ip32),
+        ("k", _ip64), ("frmsd", _dp), ("lam", _dp), ("T", _dp), ("idx", _ip32), ("gap", _dp),
     ]
 
 
@@ -182,15 +182,16 @@ def run(src, tgt, lam0=3.0, lam1=None, threshold=1e-6, max_iterations=1000, allo
     karr = np.zeros(max_calls, np.int64)
     farr = np.zeros(max_calls)
     larr = np.zeros(max_calls)
+    garr = np.zeros(max_calls)
     Tarr = np.zeros(max_calls * 9)
     iarr = np.zeros((max_calls, n), np.int32) if trace_idx else None
     tr.max_calls = max_calls
-    tr.k, tr.frmsd, tr.lam, tr.T = _p(karr, _ip64), _p(farr), _p(larr), _p(Tarr)
+    tr.k, tr.frmsd, tr.lam, tr.T, tr.gap = _p(karr, _ip64), _p(farr), _p(larr), _p(Tarr), _p(garr)
     tr.idx = _p(iarr, _ip32) if iarr is not None else None
     lib().orc_run(_p(src), n, src.shape[1], _p(tgt), len(tgt), tgt.shape[1], md, lam0, lam1, threshold,
                   max_iterations, int(allow_reflection), int(literal), nthreads, C.byref(tr))
     nc, nf = min(tr.n_calls, max_calls), min(tr.n_fits, max_calls)
-    out = dict(k=karr[:nc].copy(), frmsd=farr[:nc].copy(), lam=larr[:nc].copy(),
+    out = dict(k=karr[:nc].copy(), frmsd=farr[:nc].copy(), lam=larr[:nc].copy(), gap=garr[:nc].copy(),
                T=Tarr[:nf * 9].reshape(nf, 3, 3).copy(), iters=(tr.iters[0], tr.iters[1]),
                n_calls=tr.n_calls, n_fits=tr.n_fits)
     if iarr is not None:
@@ -255,7 +256,7 @@ def remove_matches(plot, chm, min_dist_percent=15.0):
     """
     plot = np.asarray(plot, dtype=np.float64)
     chm = np.asarray(chm, dtype=np.float64)
-    use3d = bool(np.isfinite(plot[:, 2]).all() and np.isfinite(chm[:, 2]).all())
+    use3d = bool(not np.isnan(plot[:, 2]).any() and not np.isnan(chm[:, 2]).any())  # np.isnan only
     remaining = list(range(len(chm)))
     removed = []
     for i in range(len(plot)):
@@ -272,7 +273,7 @@ def remove_matches(plot, chm, min_dist_percent=15.0):
         d = np.sqrt(d2)
         j = int(np.argmin(d))
         h = plot[i, 2]
-        if not use3d and not np.isfinite(h):
+        if not use3d and np.isnan(h):
             h = 10.0
         if d[j] < (min_dist_percent / 100.0) * h:
             removed.append(remaining.pop(j))

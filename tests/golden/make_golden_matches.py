@@ -110,6 +110,15 @@ def main():
         plots.append(c[pick] + np.column_stack([rng.normal(0, 0.6, 70), rng.normal(0, 0.6, 70),
                                                 rng.normal(0, 1.0, 70)]))
     cases["sequence"] = (plots, c)
+    # infinite heights: chm_plot.py:236-244 tests np.isnan only, so inf keeps the 3-D
+    # search (and an infinite distance limit); in 2-D an infinite plot height is kept
+    p, c = case_random(rng, 60, 200, 0.8)
+    p[[3, 17, 40], 2] = np.inf
+    c[[5, 50], 2] = np.inf
+    cases["inf3d"] = ([p], c)
+    p, c = case_random(rng, 80, 200, 0.8, nan_plot=True)
+    p[[1, 2, 30], 2] = np.inf
+    cases["inf2d"] = ([p], c)
     for name, (plots, chm) in cases.items():
         exp = run_reference(plots, chm, 15)
         out[f"{name}/chm"] = chm

@@ -1,26 +1,35 @@
 #!/usr/bin/env python3
-"""Benchmark: FICP iterations/s at 1M trees x 1M CHM stems (BASELINE.json metric).
+"""Benchmark: FICP iterations/s (BASELINE.json metric) on MI355X.
 
-One "step" = one complete FractionalICP.run() (ficp.py:149-154: two FRMSD stages to
-convergence) of one synthetic C3 plot whose layers are already resident in HBM:
-static-layer grid build + copy of the pristine source + the device-resident ICP.
-`value` = ICP loop bodies (fit -> apply -> NN -> sort -> FRMSD scan; ficp.py:132-145)
-completed per second over all ranks; the two initial NN+selection passes per run are
-inside the timed region but not counted as iterations.
+Workloads (`--workload`, default by GPU count):
+  c3     (default at N=1) one 1M-tree vs 1M-stem plot per GPU, f=0.6, md=3, run() to
+         convergence.  A step = one complete FractionalICP.run() (ficp.py:149-154) on
+         layers already resident in HBM: grid build, copy of the pristine source, the
+         device-resident two-stage loop.  value = loop bodies (ficp.py:132-145) per second
+         over all ranks ("scaling": "weak", one independent plot per GPU).
+  batch  (default at N>1) C4: 1024 plots of 10k x 10k dealt over the ranks
+         (shard.deal_plots), each rank runs its share in one ficp_run_batch_device per
+         step; value = plot loop bodies per second of the whole job ("scaling": "strong":
+         the 1024 plots are fixed as N grows).  The north star's 1/2/4/8-GPU line.
+  c2     100k x 100k, f=0.8, exactly 2 x 25 loop bodies.
+  c5     one 8M x 8M plot whose CHM layer is split over the GPUs (RCCL merge per NN call).
 
-Multi-GPU: one process per GPU (torch.distributed.run), each rank co-registers its own
-independent 1M x 1M plot (seed 1_000_000 + rank) -- plots shard with no data-path
-collective ("scaling": "weak"); torch.distributed only provides the barrier and the
-max-over-ranks time.
+Every line carries the other scale's figure as an extra key: at N=1 `batch` (the
+1-GPU point of the batch curve), at N>1 `c3_replicas` (the weak-scaling C3 figure).
 
-Other workloads (not the default bench line): --workload c2 (100k x 100k, f=0.8, exactly
-50 loop bodies), --workload batch (C4 plots of 10k x 10k, dealt over ranks).
+Launch: `python bench.py --gpus N` starts N rank processes itself (before anything in
+the parent touches a GPU) and exits with the first failing rank's code; under
+torch.distributed.run (RANK / WORLD_SIZE set) it is one rank.  Rank 0 prints ONE JSON
+line.  `--dry-run` exercises the launcher, the process group and the report with no
+GPU work (CPU tests, gloo).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -30,7 +39,7 @@ import numpy as np
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
-from coregistrationgame_amd import _lib, synth  # noqa: E402
+from coregistrationgame_amd import _lib, synth  # noqa: E402  (no GPU work at import)
 
 METRIC = "FICP iterations/sec (and correspondences/sec) at 1M×1M points, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -56,6 +65,48 @@ def dist_env():
     return rank, world, local
 
 
+# ----------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int, argv: list[str]) -> int:
+    """Start one rank process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), wait for
+    all of them; the first rank that fails stops the others.  The parent never touches
+    a GPU (no HIP call, no torch.cuda), so this is not an exec from a GPU process."""
+    env0 = dict(os.environ)
+    env0.setdefault("MASTER_ADDR", "127.0.0.1")
+    env0["MASTER_PORT"] = str(_free_port())
+    env0["WORLD_SIZE"] = str(n)
+    env0["LOCAL_WORLD_SIZE"] = str(n)
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        time.sleep(0.05)
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench: rank pid {p.pid} exited with {code}; stopping the others", file=sys.stderr)
+                for q in alive:
+                    q.terminate()
+    for p in procs:
+        p.wait()
+    return rc
+
+
+# ----------------------------------------------------------------------------- helpers
 class DevArray:
     """A device buffer owned through libficp (no torch types at the boundary)."""
 
@@ -77,7 +128,7 @@ class DevArray:
 
 
 def nn_bytes_per_launch(n, m, md):
-    """Algorithmic HBM bytes of one fused apply+NN launch: per tree read md
+    """Algorithmic HBM bytes of one fused apply+NN pass: per tree read md
     coordinates, write the moved XY (16 B), write idx (4) + dist (8); read the CHM layer
     once (8*md per stem) -- SURVEY.md §8(d)'s NN + apply terms."""
     return n * (8 * md + 16 + 12) + m * 8 * md
@@ -89,11 +140,11 @@ def iteration_bytes(n, m, md, k):
     return n * (32 + 8 * md + 12 + 24 + 16) + 32 * k + 8 * md * m
 
 
-def pmc_traffic(kernel_prefix):
+def pmc_traffic(kernel_prefix, tag):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC profile
-    (profiles/*_pmc_*_nn.json, written from tools/pmc.sh output), or None."""
+    (profiles/*_pmc_<tag>_nn.json, written from tools/pmc.sh output), or None."""
     best = None
-    for f in sorted((REPO / "profiles").glob("*_pmc_*_nn.json")):
+    for f in sorted((REPO / "profiles").glob(f"*_pmc_{tag}_nn.json")):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
@@ -103,45 +154,276 @@ def pmc_traffic(kernel_prefix):
     return best
 
 
-def cpu_baseline(plot, threads):
-    """The pinned C oracle (oracle/ficp_oracle.c, kind "port") on the same C3 plot: static
-    kd-tree + O(N) fraction scan, 2 stages x 2 loop bodies (threshold -inf), timed on
-    this host's cores.  Bounded sample; the reference ficp.py itself would need ~5.5 h per
-    iteration at 1M (O(N^2) scan)."""
+def roofline(achieved_gbs, traffic, extra):
+    out = {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
+           "traffic_source": traffic[1] if traffic else None}
+    out.update(extra)
+    return out
+
+
+class Dist:
+    """torch.distributed for the barrier, the max-over-ranks time and the sums (RCCL
+    "nccl" on GPUs, gloo for --dry-run)."""
+
+    def __init__(self, world, local, backend):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.gpu = backend == "nccl"
+        if self.gpu:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            self.dev = torch.device("cuda", local)
+        else:
+            dist.init_process_group("gloo")
+            self.dev = torch.device("cpu")
+        self.world = dist.get_world_size()
+
+    def barrier(self):
+        self.dist.barrier()
+        if self.gpu:
+            self.torch.cuda.synchronize()
+
+    def reduce(self, vals, op):
+        t = self.torch.tensor([float(v) for v in vals], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=op)
+        return [float(x) for x in t.cpu().numpy()]
+
+    def max(self, vals):
+        return self.reduce(vals, self.dist.ReduceOp.MAX)
+
+    def sum(self, vals):
+        return self.reduce(vals, self.dist.ReduceOp.SUM)
+
+    def close(self):
+        self.dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, affinity
+
+
+def _oracle():
     sys.path.insert(0, str(REPO / "oracle"))
     import ficp_oracle
     ficp_oracle.build()
+    return ficp_oracle
+
+
+def cpu_baseline(plot, threads):
+    """The pinned C oracle (oracle/ficp_oracle.c, kind "port") on the same C3 plot, timed
+    on this host: bounded samples, not the target.
+    * value: fair mode (kd-tree built once, O(N) FRMSD scan), 2 stages x 2 loop bodies,
+      `threads` OpenMP threads (the job's CPU share);
+    * value_1thread: the same, 1 thread, 2 stages x 1 loop body;
+    * literal mode (ficp.py:69-85's cost model: the index rebuilt every NN call and the
+      O(N^2) prefix scan) measured at N = 2k..16k on plots of C3's density, fitted with
+      a*N + b*N^2 per loop body and extrapolated to 1M (labelled "extrapolated")."""
+    orc = _oracle()
+    model, logical, affinity = cpu_info()
     t0 = time.perf_counter()
-    _, tr = ficp_oracle.run(plot.source, plot.target, threshold=float("-inf"), max_iterations=2,
-                            nthreads=threads, trace=True)
+    _, tr = orc.run(plot.source, plot.target, threshold=float("-inf"), max_iterations=2, nthreads=threads)
     dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    _, tr1 = orc.run(plot.source, plot.target, threshold=float("-inf"), max_iterations=1, nthreads=1)
+    dt1 = time.perf_counter() - t0
+    ns, per = [], []
+    for n in (2000, 4000, 8000, 16000):
+        p = synth.make_plot(n, n, 0.6, 1_000_000 + n, md=3)
+        t0 = time.perf_counter()
+        _, trl = orc.run(p.source, p.target, threshold=float("-inf"), max_iterations=1, literal=True, nthreads=1)
+        ns.append(n)
+        per.append((time.perf_counter() - t0) / trl["n_fits"])
+    A = np.column_stack([np.array(ns, float), np.array(ns, float) ** 2])
+    (a, b), *_ = np.linalg.lstsq(A, np.array(per), rcond=None)
+    n_full = len(plot.source)
     return {"value": tr["n_fits"] / dt, "unit": "iterations/s", "cores": threads, "kind": "port",
             "sample": f"C3 plot (1M x 1M, md=3): 2 stages x 2 loop bodies ({tr['n_calls']} NN calls, "
                       f"{tr['n_fits']} fits) in {dt:.2f} s; kd-tree built once, O(N) FRMSD scan, "
-                      f"{threads} OpenMP threads"}
+                      f"{threads} OpenMP threads",
+            "cpu_model": model, "host_logical_cpus": logical, "affinity_cpus": affinity,
+            "threads_all": threads,
+            "value_1thread": tr1["n_fits"] / dt1,
+            "sample_1thread": f"same plot, 2 stages x 1 loop body ({tr1['n_calls']} NN calls) in {dt1:.2f} s, 1 thread",
+            "literal_samples": {"n": ns, "s_per_iteration": per},
+            "literal_fit": {"a_s_per_row": float(a), "b_s_per_row2": float(b)},
+            "literal_extrapolated_s_per_iter": float(a * n_full + b * n_full ** 2),
+            "literal_note": "extrapolated: kd-tree rebuilt per NN call + O(N^2) FRMSD prefix scan "
+                            "(ficp.py:69-85 cost model) measured at N=2k-16k, 1 thread, fitted a*N+b*N^2"}
 
 
-def cpu_baseline_batch(plots, threads, budget_s=15.0):
+def cpu_baseline_batch(plots, threads, budget_s=10.0):
     """The C oracle on the first plots of this rank's share, one run() each, until the
     time budget is spent (bounded sample); iterations/s = its loop bodies / time."""
-    sys.path.insert(0, str(REPO / "oracle"))
-    import ficp_oracle
-    ficp_oracle.build()
+    orc = _oracle()
+    model, logical, affinity = cpu_info()
     fits = done = 0
     t0 = time.perf_counter()
     for pl in plots:
-        _, tr = ficp_oracle.run(pl.source, pl.target, nthreads=threads, trace=True)
+        _, tr = orc.run(pl.source, pl.target, nthreads=threads, trace=True)
         fits += tr["n_fits"]
         done += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     return {"value": fits / dt, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_logical_cpus": logical,
             "sample": f"{done} C4 plots (10k x 10k, md=3), full run() each: {fits} loop bodies in "
                       f"{dt:.2f} s; kd-tree built once per plot, O(N) FRMSD scan, {threads} OpenMP threads"}
 
 
-def bench_batch(args, rank, world, local, dist):
+def host_path_cost(plot, device, reps=3):
+    """The drop-in call shape of app.py:658-660: FractionalICP(src, tgt).run() from numpy
+    arrays, a new instance (and library context) per call, result back in numpy.  Also
+    the same sequence through the context with its phases timed: constructor copies,
+    context creation, set_target (H2D of the CHM layer + grid build), run (H2D of the
+    source, work order, device loop, caller-order scatter, D2H), and the device loop's
+    own time (ficp_stats.gpu_ms)."""
+    from coregistrationgame_amd import FractionalICP
+    md = 3
+    tot = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        icp = FractionalICP(plot.source, plot.target, device=device)
+        icp.run()
+        tot.append(1e3 * (time.perf_counter() - t0))
+        icp.close()
+    ph = {"copy_ms": [], "context_ms": [], "set_target_ms": [], "run_ms": [], "gpu_loop_ms": []}
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        src = np.array(plot.source, dtype=np.float64, order="C", copy=True)
+        tgt = np.ascontiguousarray(plot.target[:, :md])
+        t1 = time.perf_counter()
+        ctx = _lib.Context(device)
+        t2 = time.perf_counter()
+        ctx.set_target(tgt, md)
+        ctx.synchronize()
+        t3 = time.perf_counter()
+        st = ctx.run(src, [3.0, 0.95], 1e-6, 1000, False)
+        t4 = time.perf_counter()
+        ctx.close()
+        for k, v in (("copy_ms", t1 - t0), ("context_ms", t2 - t1), ("set_target_ms", t3 - t2),
+                     ("run_ms", t4 - t3)):
+            ph[k].append(1e3 * v)
+        ph["gpu_loop_ms"].append(st["gpu_ms"])
+    out = {"ms_per_run": float(np.median(tot)), "ms_first_run": tot[0],
+           "iterations_per_s": None, "breakdown_median_ms": {k: float(np.median(v)) for k, v in ph.items()}}
+    b = out["breakdown_median_ms"]
+    b["run_minus_gpu_loop_ms"] = b["run_ms"] - b["gpu_loop_ms"]
+    out["note"] = ("numpy in/out per call (app.py:658-660); run_minus_gpu_loop = source H2D + work order + "
+                   "result D2H + host overhead")
+    return out
+
+
+# ----------------------------------------------------------------------------- workloads
+def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
+    """C3 / C2: one plot per rank (seed + rank), device-resident layers."""
+    n, m, f, seed0, md, thr, max_it, desc = WORKLOADS[wl]
+    plot = synth.make_plot(n, m, f, seed0 + rank, md=md)
+    ctx = _lib.Context(local, {"auto": 0, "brute": 1, "grid": 2}[args.nn_mode])
+    cols = [plot.source[:, j] for j in range(md)]
+    src0 = [DevArray(ctx, c) for c in cols]          # pristine source, resident
+    src = [DevArray(ctx, c) for c in cols]           # working copy (x, y move)
+    tgt = [DevArray(ctx, plot.target[:, j]) for j in range(md)]
+    lam = [3.0, 0.95 if md == 3 else 1.3]
+
+    def step():
+        src[0].copy_from(src0[0])
+        src[1].copy_from(src0[1])
+        ctx.set_target_device(tgt[0].ptr, tgt[1].ptr, tgt[2].ptr if md == 3 else 0, m, md)
+        return ctx.run_device(src[0].ptr, src[1].ptr, src[2].ptr if md == 3 else 0, n, lam, thr, max_it)
+
+    def barrier():
+        ctx.synchronize()
+        if D is not None:
+            D.barrier()
+
+    for _ in range(warmup):
+        step()
+    ctx.profile_report()  # drop warmup records
+    # NN launch timing: HIP events carried by the NN dispatches themselves on the library
+    # stream, inside the timed region.  Each timed dispatch leaves ~5 us of idle queue
+    # around it, so by default only the first timed step carries them.
+    ctx.profile_enable(_lib.PROF_NN if args.nn_timing != "none" else 0)
+    barrier()
+    t0 = time.perf_counter()
+    fits = calls = timed_calls = 0
+    for s_i in range(steps):
+        st = step()
+        fits += st["n_fits"]
+        calls += st["n_nn_calls"]
+        if args.nn_timing == "all" or (args.nn_timing == "first" and s_i == 0):
+            timed_calls += st["n_nn_calls"]
+        if s_i == 0 and args.nn_timing == "first":
+            ctx.profile_enable(0)
+    barrier()
+    dt = time.perf_counter() - t0
+    ctx.profile_enable(0)
+    prof = json.loads(ctx.profile_report())
+    dt_max, fits_all, calls_all = dt, fits, calls
+    if D is not None:
+        dt_max = D.max([dt])[0]
+        fits_all, calls_all = D.sum([fits, calls])
+    out = None
+    if rank == 0:
+        nn = prof.get("nn_grid") or prof.get("nn_brute") or {"count": 0, "ms": 0.0}
+        # per real NN call: the device loop also enqueues a few no-op iterations past the
+        # end of each run (their early-exit launches are in nn["ms"]: conservative)
+        avg_ms = nn["ms"] / max(timed_calls, 1)
+        bytes_launch = nn_bytes_per_launch(n, m, md)
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic = pmc_traffic("k_nn_grid<3" if md == 3 else "k_nn_grid<2", "c3") if wl == "c3" else None
+        ib = iteration_bytes(n, m, md, n)
+        out = {
+            "metric": METRIC, "value": fits_all / dt_max, "unit": "iterations/s", "n_gpus": world,
+            "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * dt_max / steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic (SURVEY.md §8(d) generator, seed {seed0}+rank, geo-referenced)",
+            "config": {"workload": desc, "n_trees": n, "n_chm": m, "inlier_fraction": f, "match_dims": md,
+                       "plots_per_rank": 1, "parallelism": f"{world} independent plots (1 per GPU)",
+                       "nn": args.nn_mode},
+            "iterations_per_step": fits_all / steps / world,
+            "nn_calls_per_step": calls_all / steps / world,
+            "correspondences_per_s": calls_all * n / dt_max,
+            "roofline": roofline(achieved, traffic, {
+                "kernel": "k_nn_grid (fused apply + exact 1-NN)", "avg_launch_us": avg_ms * 1e3,
+                "launches": timed_calls, "timed_launches_incl_noop": nn["count"],
+                "algorithmic_bytes_per_launch": bytes_launch}),
+            "kernel_ms": prof,
+            # the whole loop body against SURVEY.md §8(d)'s per-iteration bytes (k = n: the
+            # upper bound of the fit term), beside the dominant kernel's line
+            "iteration_roofline": {"bytes_per_iteration": ib, "achieved": ib * fits_all / dt_max / 1e9,
+                                   "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                                   "frac": ib * fits_all / dt_max / 1e9 / HBM_PEAK_GBS},
+        }
+    for a in src0 + src + tgt:
+        a.free()
+    ctx.close()
+    if rank == 0 and world == 1 and with_cpu:
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(plot, threads)
+        if wl == "c3":
+            out["host_path"] = host_path_cost(plot, local)
+    elif out is not None:
+        out["cpu_baseline"] = None
+    return out
+
+
+def bench_batch(args, rank, world, local, D, steps, warmup, with_cpu):
     """C4: the batch is dealt over ranks (shard.deal_plots); each rank runs its plots in
     one ficp_run_batch_device per step; no collective on the data path."""
     from coregistrationgame_amd import shard
@@ -170,12 +452,10 @@ def bench_batch(args, rank, world, local, dist):
 
     def barrier():
         ctx.synchronize()
-        if dist is not None:
-            import torch
-            dist.barrier()
-            torch.cuda.synchronize()
+        if D is not None:
+            D.barrier()
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     ctx.profile_report()
     ctx.profile_enable(_lib.PROF_NN | _lib.PROF_SORT | _lib.PROF_FRAC | _lib.PROF_FIT)
@@ -183,7 +463,7 @@ def bench_batch(args, rank, world, local, dist):
     t0 = time.perf_counter()
     fits = calls = 0
     last = None
-    for _ in range(args.steps):
+    for _ in range(steps):
         last = step()
         fits += int(last["n_fits"].sum())
         calls += int(last["n_nn_calls"].sum())
@@ -191,61 +471,55 @@ def bench_batch(args, rank, world, local, dist):
     dt = time.perf_counter() - t0
     ctx.profile_enable(0)
     prof = json.loads(ctx.profile_report())
-    tot = np.array([dt, fits, calls], dtype=np.float64)
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        c = torch.tensor([float(fits), float(calls)], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        tot = np.array([t.item(), c[0].item(), c[1].item()])
+    dt_max, fits_all, calls_all = dt, fits, calls
+    if D is not None:
+        dt_max = D.max([dt])[0]
+        fits_all, calls_all = D.sum([fits, calls])
         # one all-gather of the per-plot records, outside the timed region
-        shard.gather_plot_stats(deal, last, rank, device=f"cuda:{local}")
-    dt_max, fits_all, calls_all = tot
+        shard.gather_plot_stats(deal, last, rank, device=D.dev)
+    out = None
     if rank == 0:
         nn = prof.get("nn_grid_batch") or {"count": 0, "ms": 0.0}
-        avg_ms = nn["ms"] / max(nn["count"], 1)
-        n_loc = int(so[-1])
-        bytes_launch = nn_bytes_per_launch(n_loc, int(to[-1]), md)
-        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        # algorithmic bytes of every plot-NN call this rank made in the timed steps over
+        # the NN kernel's total time: converged plots drop out of later launches
+        nn_bytes = calls * nn_bytes_per_launch(n, m, md)
+        achieved = nn_bytes / (nn["ms"] * 1e-3) / 1e9 if nn["ms"] > 0 else 0.0
+        ib = iteration_bytes(n, m, md, n)
         out = {
             "metric": METRIC, "value": fits_all / dt_max, "unit": "iterations/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * dt_max / args.steps,
+            "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * dt_max / steps,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": f"synthetic (SURVEY.md §8(d) generator, seeds {seed0}+plot, geo-referenced)",
             "config": {"workload": desc, "plots": nplots, "plots_per_rank": len(mine), "n_trees": n,
                        "n_chm": m, "inlier_fraction": f, "match_dims": md,
                        "parallelism": f"plots dealt over {world} GPU(s), no data-path collective"},
-            "iterations_per_step": fits_all / args.steps,
-            "nn_calls_per_step": calls_all / args.steps,
+            "iterations_per_step": fits_all / steps,
+            "nn_calls_per_step": calls_all / steps,
             "correspondences_per_s": calls_all * n / dt_max,
-            "roofline": {"bound": "hbm", "kernel": "nn_grid_batch (fused apply + exact 1-NN, all plots)",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_us": avg_ms * 1e3,
-                         "launches": nn["count"], "algorithmic_bytes_per_launch": bytes_launch,
-                         "note": "bytes count every tree of the rank as live"},
+            "roofline": roofline(achieved, pmc_traffic("k_nn_grid_batch", "batch"), {
+                "kernel": "k_nn_grid_batch (fused apply + exact 1-NN, all live plots)",
+                "avg_launch_us": 1e3 * nn["ms"] / max(nn["count"], 1), "launches": nn["count"],
+                "algorithmic_bytes_per_plot_call": nn_bytes_per_launch(n, m, md),
+                "note": "rank 0: algorithmic bytes of its plot-NN calls / total NN kernel time"}),
             "kernel_ms": prof,
-            # the whole loop body against SURVEY.md §8(d)'s per-iteration bytes (k = n: the
-            # upper bound of the fit term), for reference beside the dominant kernel's line
-            # (per plot-iteration here)
-            "iteration_roofline": {"bytes_per_iteration": iteration_bytes(n, m, md, n),
-                                   "achieved": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9,
+            "iteration_roofline": {"bytes_per_iteration": ib, "achieved": ib * fits_all / dt_max / 1e9,
                                    "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                                   "frac": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9
-                                   / HBM_PEAK_GBS},
+                                   "frac": ib * fits_all / dt_max / 1e9 / HBM_PEAK_GBS,
+                                   "note": "per plot-iteration, SURVEY.md §8(d) bytes at 10k x 10k"},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline_batch(plots, threads)
-        else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
     for a in src0 + src + tgt:
         a.free()
     ctx.close()
+    if out is not None:
+        if world == 1 and with_cpu:
+            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline_batch(plots, threads)
+        else:
+            out["cpu_baseline"] = None
+    return out
 
 
-def bench_c5(args, rank, world, local, dist):
+def bench_c5(args, rank, world, local, D, steps, warmup):
     """C5: the CHM layer is split in contiguous row shards over the ranks (SURVEY.md §8(e));
     every NN call merges the shards with two all-reduces over RCCL.  One plot for the whole
     job: value = its loop bodies per second ("scaling": "strong")."""
@@ -256,54 +530,86 @@ def bench_c5(args, rank, world, local, dist):
     plot = synth.make_plot(n, m, f, seed0, md=md)  # same plot on every rank (replicated source)
     part = PartitionedFICP(plot.source, plot.target, threshold=thr, max_iterations=max_it,
                            device=local, local_shards=args.local_shards)
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         part.run_resident(lambda0=3.0)
 
     def barrier():
         import torch
         torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-            torch.cuda.synchronize()
+        if D is not None:
+            D.barrier()
 
     barrier()
     t0 = time.perf_counter()
     fits = calls = 0
-    for _ in range(args.steps):
+    for _ in range(steps):
         st = part.run_resident(lambda0=3.0)
         fits += st["n_fits"]
         calls += st["n_nn_calls"]
     barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": fits / dt, "unit": "iterations/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": f"synthetic (SURVEY.md §8(d) generator, seed {seed0}, geo-referenced)",
-            "config": {"workload": desc, "n_trees": n, "n_chm": m, "inlier_fraction": f, "match_dims": md,
-                       "shards": world * args.local_shards,
-                       "parallelism": f"CHM layer in {world * args.local_shards} row shards over {world} GPU(s); "
-                                      "2 all-reduces (d2 MIN, idx MIN) per NN call"},
-            "iterations_per_step": fits / args.steps, "nn_calls_per_step": calls / args.steps,
-            "correspondences_per_s": calls * n / dt, "roofline": None, "cpu_baseline": None,
-        }
-        print(json.dumps(out), flush=True)
+    if D is not None:
+        dt = D.max([dt])[0]
     part.close()
+    if rank != 0:
+        return None
+    return {
+        "metric": METRIC, "value": fits / dt, "unit": "iterations/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * dt / steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": f"synthetic (SURVEY.md §8(d) generator, seed {seed0}, geo-referenced)",
+        "config": {"workload": desc, "n_trees": n, "n_chm": m, "inlier_fraction": f, "match_dims": md,
+                   "shards": world * args.local_shards,
+                   "parallelism": f"CHM layer in {world * args.local_shards} row shards over {world} GPU(s); "
+                                  "2 all-reduces (d2 MIN, idx MIN) per NN call"},
+        "iterations_per_step": fits / steps, "nn_calls_per_step": calls / steps,
+        "correspondences_per_s": calls * n / dt, "roofline": None, "cpu_baseline": None,
+    }
 
 
+def bench_dry(args, wl, rank, world, D, steps, warmup):
+    """No GPU work: the launcher, the process group, the plot deal, the timed-region
+    bracket with max-over-ranks, the end-of-run all-gather and the report."""
+    from coregistrationgame_amd import shard
+    nplots = args.plots or BATCH_PLOTS
+    deal = shard.deal_plots(np.full(nplots, 1.0), world)
+    mine = deal[rank]
+    if D is not None:
+        D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pass
+    if D is not None:
+        D.barrier()
+    dt = max(time.perf_counter() - t0, 1e-9)
+    dt_max = D.max([dt])[0] if D is not None else dt
+    counts = D.sum([len(mine)]) if D is not None else [len(mine)]
+    if D is not None:
+        rec = np.zeros(len(mine), _lib.PLOT_STATS_DTYPE)
+        rec["k_last"] = mine
+        allrec = shard.gather_plot_stats(deal, rec, rank, device=D.dev)
+        assert np.array_equal(allrec["k_last"], np.arange(nplots))
+    if rank != 0:
+        return None
+    return {"metric": METRIC, "value": 0.0, "unit": "iterations/s", "n_gpus": world, "steps": steps,
+            "warmup": warmup, "ms_per_step": 1e3 * dt_max / max(steps, 1), "higher_is_better": True,
+            "scaling": "strong" if wl == "batch" else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "none (dry run)", "dry_run": True,
+            "config": {"workload": wl, "plots": nplots, "plots_dealt": int(counts[0])},
+            "roofline": None, "cpu_baseline": None}
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: c3 at 1 GPU, batch at more")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the other scale's figure (batch at N=1, c3_replicas at N>1)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = $OMP_NUM_THREADS or min(16, host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nn-timing", default="first", choices=["first", "all", "none"],
                     help="timed steps whose NN dispatches carry HIP events")
@@ -311,138 +617,46 @@ def main():
     ap.add_argument("--plots", type=int, default=0, help="batch workload: number of plots (default 1024)")
     ap.add_argument("--c5-size", type=int, default=0, help="c5 workload: trees = stems (default 8M)")
     ap.add_argument("--local-shards", type=int, default=1, help="c5 workload: shards per GPU")
+    ap.add_argument("--dry-run", action="store_true", help="no GPU work (launcher/process-group check)")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"])
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     rank, world, local = dist_env()
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    wl = args.workload or ("c3" if world == 1 else "batch")
+    backend = args.backend if args.backend != "auto" else ("gloo" if args.dry_run else "nccl")
+    D = Dist(world, local, backend) if world > 1 else None
+    ranks_seen = D.world if D is not None else 1
 
-    if args.workload in ("batch", "c5"):
-        (bench_batch if args.workload == "batch" else bench_c5)(args, rank, world, local, dist)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-
-    n, m, f, seed0, md, thr, max_it, desc = WORKLOADS[args.workload]
-    plot = synth.make_plot(n, m, f, seed0 + rank, md=md)
-    ctx = _lib.Context(local, {"auto": 0, "brute": 1, "grid": 2}[args.nn_mode])
-    cols = [plot.source[:, j] for j in range(md)]
-    tcols = [plot.target[:, j] for j in range(md)]
-    src0 = [DevArray(ctx, c) for c in cols]          # pristine source, resident
-    src = [DevArray(ctx, c) for c in cols]           # working copy (x, y move)
-    tgt = [DevArray(ctx, c) for c in tcols]
-    lam = [3.0, 0.95 if md == 3 else 1.3]
-
-    def step():
-        src[0].copy_from(src0[0])
-        src[1].copy_from(src0[1])
-        ctx.set_target_device(tgt[0].ptr, tgt[1].ptr, tgt[2].ptr if md == 3 else 0, m, md)
-        return ctx.run_device(src[0].ptr, src[1].ptr, src[2].ptr if md == 3 else 0, n, lam, thr, max_it)
-
-    def barrier():
-        ctx.synchronize()
-        if dist is not None:
-            dist.barrier()
-            import torch
-            torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    ctx.profile_report()  # drop warmup records
-    # NN launch timing: events carried by the NN dispatches themselves, inside the timed
-    # region.  Each timed dispatch still leaves ~5 us of idle queue around it, so by
-    # default only the first timed step carries them (--nn-timing all: every step).
-    ctx.profile_enable(_lib.PROF_NN if args.nn_timing != "none" else 0)
-    barrier()
-    t0 = time.perf_counter()
-    fits = calls = 0
-    timed_calls = 0
-    for s_i in range(args.steps):
-        st = step()
-        fits += st["n_fits"]
-        calls += st["n_nn_calls"]
-        if args.nn_timing == "all" or (args.nn_timing == "first" and s_i == 0):
-            timed_calls += st["n_nn_calls"]
-        if s_i == 0 and args.nn_timing == "first":
-            ctx.profile_enable(0)
-    barrier()
-    dt = time.perf_counter() - t0
-    ctx.profile_enable(0)
-    prof = json.loads(ctx.profile_report())
-
-    tot = np.array([dt, fits, calls], dtype=np.float64)
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        c = torch.tensor([float(fits), float(calls)], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        tot = np.array([t.item(), c[0].item(), c[1].item()])
-    dt_max, fits_all, calls_all = tot
-
-    if rank == 0:
-        nn = prof.get("nn_grid") or prof.get("nn_brute") or {"count": 0, "ms": 0.0}
-        # per real NN call: the device loop also enqueues a few no-op iterations past the
-        # end of each run (their early-exit launches are in nn["ms"]: conservative)
-        launches = timed_calls
-        avg_ms = nn["ms"] / max(launches, 1)
-        bytes_launch = nn_bytes_per_launch(n, m, md)
-        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic = pmc_traffic("k_nn_grid<3" if md == 3 else "k_nn_grid<2") if args.workload == "c3" else None
-        out = {
-            "metric": METRIC,
-            "value": fits_all / dt_max,
-            "unit": "iterations/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": 1e3 * dt_max / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": f"synthetic (SURVEY.md §8(d) generator, seed {seed0}+rank, geo-referenced)",
-            "config": {"workload": desc, "n_trees": n, "n_chm": m, "inlier_fraction": f, "match_dims": md,
-                       "plots_per_rank": 1, "parallelism": f"{world} independent plots (1 per GPU)",
-                       "nn": args.nn_mode},
-            "iterations_per_step": fits_all / args.steps / world,
-            "nn_calls_per_step": calls_all / args.steps / world,
-            "correspondences_per_s": calls_all * n / dt_max,
-            "roofline": {"bound": "hbm", "kernel": "nn_grid (fused apply + exact 1-NN)",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic[0] if traffic else None,
-                         "traffic_source": traffic[1] if traffic else None,
-                         "avg_launch_us": avg_ms * 1e3, "launches": launches,
-                         "timed_launches_incl_noop": nn["count"],
-                         "algorithmic_bytes_per_launch": bytes_launch},
-            "kernel_ms": prof,
-            # the whole loop body against SURVEY.md §8(d)'s per-iteration bytes (k = n: the
-            # upper bound of the fit term), for reference beside the dominant kernel's line
-            "iteration_roofline": {"bytes_per_iteration": iteration_bytes(n, m, md, n),
-                                   "achieved": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9,
-                                   "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                                   "frac": iteration_bytes(n, m, md, n) * fits_all / dt_max / 1e9
-                                   / HBM_PEAK_GBS},
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(plot, threads)
-        else:
-            out["cpu_baseline"] = None
+    if args.dry_run:
+        out = bench_dry(args, wl, rank, world, D, args.steps, args.warmup)
+    elif wl == "batch":
+        out = bench_batch(args, rank, world, local, D, args.steps, args.warmup, not args.no_cpu_baseline)
+        if not args.no_extra and world > 1:
+            rep = bench_single(args, "c3", rank, world, local, D, args.steps, args.warmup, False)
+            if out is not None:
+                out["c3_replicas"] = {k: rep[k] for k in ("value", "unit", "ms_per_step", "scaling", "config",
+                                                          "iterations_per_step", "roofline", "iteration_roofline")}
+    elif wl == "c5":
+        out = bench_c5(args, rank, world, local, D, args.steps, args.warmup)
+    else:
+        out = bench_single(args, wl, rank, world, local, D, args.steps, args.warmup, not args.no_cpu_baseline)
+        if not args.no_extra and wl == "c3":
+            b = bench_batch(args, rank, world, local, D, max(3, args.steps // 2), 1, False)
+            if out is not None:
+                out["batch"] = {k: b[k] for k in ("value", "unit", "n_gpus", "ms_per_step", "scaling", "config",
+                                                  "iterations_per_step", "nn_calls_per_step",
+                                                  "correspondences_per_s", "roofline", "iteration_roofline",
+                                                  "kernel_ms")}
+    if out is not None:
+        out["ranks_seen"] = ranks_seen
         print(json.dumps(out), flush=True)
-
-    for a in src0 + src + tgt:
-        a.free()
-    ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if D is not None:
+        D.close()
 
 
 if __name__ == "__main__":

@@ -6,10 +6,9 @@
 // arrays (per-plot geometry, global cell ids), and one batch iteration advances every
 // live plot by one step of ficp.py:122-147:
 //
-//   batch_fit (LOOP plots: fit on the plot's selection, T kept in the plot's state)
+//   batch_fit    (LOOP plots: fit on the plot's selection, T kept in the plot's state)
 //   -> nn_grid_batch (applies T, exact 1-NN against the plot's own grid, keys + r)
-//   -> sort_seg      (distance order, then stable partition by plot)
-//   -> batch_fraction(one workgroup per plot: FRMSD argmin over its segment)
+//   -> batch_select  (one workgroup per plot: FRMSD-optimal k + selection threshold)
 //   -> batch_update  (per-plot convergence test ficp.py:142, stage switch ficp.py:152)
 //
 // The host reads one counter (live plots) per batch iteration.
@@ -18,13 +17,14 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
 struct BatchBufs {
     DevBuf so, to, plot_of, tplot, grids, st, active, bb, lams;
     DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp;
-    DevBuf key, idx, r, ccx, ccy, order, rs, sort_tmp, range, bp;
+    DevBuf key, gap, r, ccx, ccy, bp, dz2, wkey, skey, wrow, srow, wr, sr;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
     unsigned int *h_active = nullptr;      // pinned
 };
@@ -33,10 +33,11 @@ void batch_release(BatchBufs *b) {
     if (!b) return;
     DevBuf *bufs[] = {&b->so,       &b->to,      &b->plot_of,  &b->tplot, &b->grids, &b->st,
                       &b->active,   &b->bb,      &b->lams,     &b->cell_of, &b->counts,
-                      &b->fill,     &b->cell_start, &b->pts,   &b->scan_tmp, &b->key, &b->idx,
-                      &b->r,        &b->ccx,     &b->ccy,      &b->order, &b->rs,
-                      &b->sort_tmp, &b->range,   &b->sx,       &b->sy,    &b->sz,    &b->tx,
-                      &b->ty,       &b->tz,      &b->stage,    &b->bp};
+                      &b->fill,     &b->cell_start, &b->pts,   &b->scan_tmp, &b->key, &b->gap,
+                      &b->r,        &b->ccx,     &b->ccy,      &b->wkey,  &b->skey,  &b->wrow,
+                      &b->srow,     &b->wr,      &b->sr,       &b->sx,    &b->sy,    &b->sz,
+                      &b->tx,       &b->ty,      &b->tz,       &b->stage, &b->bp,
+                      &b->dz2};
     for (DevBuf *d : bufs) d->release();
     if (b->h_active) (void)hipHostFree(b->h_active);
     delete b;
@@ -155,35 +156,44 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         }
         CHK(b.plot_of.ensure(n * 4));
         CHK(b.key.ensure(n * 8));
-        CHK(b.idx.ensure(n * 4));
+        CHK(b.gap.ensure(n * 8));
+        CHK(b.dz2.ensure(n * 8));
         CHK(b.r.ensure(n * 8));
         CHK(b.ccx.ensure(n * 8));
         CHK(b.ccy.ensure(n * 8));
-        CHK(b.order.ensure(n * 4));
-        CHK(b.rs.ensure(n * 8));
-        CHK(b.sort_tmp.ensure(sort_seg_tmp_bytes(n)));
-        CHK(b.range.ensure(range_words(n) * 8));
         CHK(b.bp.ensure(n * 4));
-        // keys of plots that never run (no CHM stems) must be defined for the sort
-        HIPCHK(hipMemsetAsync(b.key.p, 0, n * 8, c->stream));
+        CHK(b.wkey.ensure(n * 8));
+        CHK(b.skey.ensure(n * 8));
+        CHK(b.wrow.ensure(n * 4));
+        CHK(b.srow.ensure(n * 4));
+        CHK(b.wr.ensure(n * 8));
+        CHK(b.sr.ensure(n * 8));
+        const BatchSelScratch ws{b.wkey.as<unsigned long long>(), b.skey.as<unsigned long long>(),
+                                 b.wrow.as<uint32_t>(), b.srow.as<uint32_t>(), b.wr.as<double>(),
+                                 b.sr.as<double>()};
+        int64_t max_rows = 0;
+        for (int32_t p = 0; p < nplots; ++p) max_rows = std::max(max_rows, so_h[p + 1] - so_h[p]);
         HIPCHK(launch_fill_plot_ids(b.so.as<int64_t>(), nplots, b.plot_of.as<int32_t>(),
                                     c->stream));
-        uint32_t *tflag = sort_timeout_flag(b.sort_tmp.p, n);
-        HIPCHK(launch_atomic_zero32(tflag, 1, c->stream));
         NNArgs a{};
         a.sx = sx;
         a.sy = sy;
         a.sz = md == 3 ? sz : nullptr;
         a.n = n;
-        a.idx = b.idx.as<int32_t>();
+        a.idx = nullptr;  // the batch returns XY and per-plot records, not the NN index
         a.r = b.r.as<double>();
         a.key = b.key.as<unsigned long long>();
         a.cx = b.ccx.as<double>();
         a.cy = b.ccy.as<double>();
         a.tx = tx;
         a.ty = ty;
-        a.range = b.range.as<unsigned long long>();
+        a.range = nullptr;
         a.out_bp = b.bp.as<int32_t>();
+        // certified reuse of each query's match (k_grid_nn.hip cert_try): the first call
+        // of the batch is cold (every plot starts there), the rest are warm
+        a.gap = b.gap.as<double>();
+        a.dz2 = md == 3 ? b.dz2.as<double>() : nullptr;
+        a.cert_block = 8;
         PlotState *st = b.st.as<PlotState>();
         // every plot makes at most nstages * (max_iter + 1) NN calls
         const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1) + 1;
@@ -191,11 +201,11 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             {
                 ProfScope ps(c, P_FIT, "batch_fit");
                 HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
-                                        b.key.as<unsigned long long>(), b.order.as<uint32_t>(),
-                                        b.so.as<int64_t>(), b.grids.as<PlotGrid>(), nplots,
-                                        allow_refl, st, c->stream));
+                                        b.key.as<unsigned long long>(), b.so.as<int64_t>(),
+                                        b.grids.as<PlotGrid>(), nplots, allow_refl, st,
+                                        c->stream));
             }
-            a.prev_bp = bit > 0 ? b.bp.as<int32_t>() : nullptr;  // warm start after the first call
+            a.warm_c = bit > 0 ? 1 : 0;
             {
                 ProfScope ps(c, P_NN, "nn_grid_batch");
                 HIPCHK(launch_nn_grid_batch(a, b.plot_of.as<int32_t>(), b.grids.as<PlotGrid>(),
@@ -203,16 +213,10 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                                             md, c->stream));
             }
             {
-                ProfScope ps(c, P_SORT, "sort_seg");
-                HIPCHK(launch_sort_seg(b.key.as<unsigned long long>(), b.plot_of.as<int32_t>(), n,
-                                       b.range.as<unsigned long long>(), b.order.as<uint32_t>(),
-                                       b.r.as<double>(), b.rs.as<double>(), b.sort_tmp.p,
-                                       c->stream));
-            }
-            {
-                ProfScope ps(c, P_FRAC, "batch_fraction");
-                HIPCHK(launch_batch_fraction(b.rs.as<double>(), b.so.as<int64_t>(), nplots,
-                                             b.lams.as<double>(), st, c->stream));
+                ProfScope ps(c, P_FRAC, "batch_select");
+                HIPCHK(launch_batch_select(b.key.as<unsigned long long>(), b.r.as<double>(),
+                                           b.so.as<int64_t>(), nplots, max_rows,
+                                           b.lams.as<double>(), st, ws, c->stream));
             }
             HIPCHK(launch_batch_update(nplots, nstages, threshold, max_iter, st,
                                        (unsigned int *)b.active.p, c->stream));
@@ -220,10 +224,6 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             CHK(sync(c));
             if (*b.h_active == 0) break;
         }
-        uint32_t tf = 0;
-        HIPCHK(hipMemcpyAsync(&tf, tflag, 4, hipMemcpyDeviceToHost, c->stream));
-        CHK(sync(c));
-        if (tf) return fail(FICP_EHIP, "residual sort look-back timed out (results invalid)");
         if (*b.h_active != 0) return fail(FICP_EHIP, "batch did not converge within its bound");
     }
     HIPCHK(hipEventRecord(c->ev1, c->stream));

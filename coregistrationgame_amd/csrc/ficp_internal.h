@@ -547,6 +547,8 @@ struct alignas(16) PlotState {
     int it;            // loop bodies completed in this stage
     int apply;
     int n_nn, n_fit, iters0, iters1;
+    unsigned long long tkey;  // selection threshold: rows with (key, row) <= (tkey, trow)
+    long long trow;           // (global row index) are the k selected ones
 };
 
 // per-plot bbox of the CHM layer: bb[4p..4p+3] = xmin, xmax, ymin, ymax
@@ -570,11 +572,21 @@ int64_t sort_seg_tmp_bytes(int64_t n);
 hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
                              PlotState *st, hipStream_t s);
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
-                            const double *cy, const unsigned long long *key,
-                            const uint32_t *order, const int64_t *so, const PlotGrid *grids,
-                            int nplots, int allow_refl, PlotState *st, hipStream_t s);
-hipError_t launch_batch_fraction(const double *rs, const int64_t *so, int nplots,
-                                 const double *lambdas, PlotState *st, hipStream_t s);
+                            const double *cy, const unsigned long long *key, const int64_t *so,
+                            const PlotGrid *grids, int nplots, int allow_refl, PlotState *st,
+                            hipStream_t s);
+// Per-plot FRMSD-optimal fraction (ficp.py:73-86), one workgroup per live plot: bucket
+// histogram of the plot's keys, bounds, exact sort of the candidate window only; sets
+// k, frac, frmsd and the threshold pair (tkey, trow).  Scratch: 3 x n words of 8 B and
+// 2 x n of 4 B (indexed by global row).  max_rows: the largest plot.
+struct BatchSelScratch {
+    unsigned long long *wkey, *skey;
+    uint32_t *wrow, *srow;
+    double *wr, *sr;
+};
+hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,
+                               int nplots, int64_t max_rows, const double *lambdas,
+                               PlotState *st, BatchSelScratch ws, hipStream_t s);
 hipError_t launch_batch_update(int nplots, int nstages, double threshold, int max_iter,
                                PlotState *st, unsigned int *active, hipStream_t s);
 

@@ -1,18 +1,19 @@
 // k_batch.hip -- many plots per launch (BASELINE config C4: 1024 plots x 10k trees vs 10k
 // CHM stems).  Every plot runs the reference's two-stage _iterate (ficp.py:122-154); the
 // plots advance together, one batch iteration = {fit of looping plots -> NN with the fit
-// applied -> segmented sort -> per-plot FRMSD scan -> per-plot state machine}, and a plot
-// leaves the batch when its own convergence test fires (per-plot masks, no host work).
+// applied -> per-plot FRMSD selection -> per-plot state machine}, and a plot leaves the
+// batch when its own convergence test fires (per-plot masks, no host work).
 //
 //  * k_batch_bbox / k_fill_plot_ids / k_batch_grid_count: per-plot CHM grids in one set of
 //    arrays (cell ids offset by each plot's cell_base).
-//  * k_batch_fraction: one workgroup per plot scans r in the plot's (distance, index)
-//    order -> first-minimum FRMSD argmin (same formula and tie rule as k_frac_eval).
+//  * k_batch_select: one workgroup per live plot: bucketed FRMSD bounds, exact order of
+//    the candidate window only -> first-minimum FRMSD argmin and the selection threshold.
 //  * k_batch_fit: one workgroup per looping plot streams the plot's trees, selects
 //    (key, index) <= (key_t, t), reduces the 8 pivot-shifted sums and solves the 2x2
 //    Kabsch problem in closed form (same as k_fit_final).
 //  * k_batch_update: one thread per plot advances HEAD -> LOOP -> (stage 2) -> DONE.
 #include "ficp_internal.h"
+#include "frmsd_bounds.h"
 
 #include <math.h>
 
@@ -22,8 +23,7 @@ namespace ficp {
 
 namespace {
 
-constexpr int BB = 256;  // threads per per-plot workgroup
-constexpr int BI = 4;    // items per thread per chunk
+constexpr int BB = 256;  // threads per per-plot workgroup (bbox, fit)
 
 __device__ __forceinline__ double bsum(double v, double *s) {
     s[threadIdx.x] = v;
@@ -35,26 +35,6 @@ __device__ __forceinline__ double bsum(double v, double *s) {
     const double r = s[0];
     __syncthreads();
     return r;
-}
-
-// exclusive scan over the workgroup + total (Hillis-Steele, deterministic)
-__device__ __forceinline__ double bscan(double v, double *s /*[2*BB]*/, double &total) {
-    double *a = s, *b = s + BB;
-    a[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 1; o < BB; o <<= 1) {
-        const double x =
-            ((int)threadIdx.x >= o) ? a[threadIdx.x - o] + a[threadIdx.x] : a[threadIdx.x];
-        b[threadIdx.x] = x;
-        __syncthreads();
-        double *t = a;
-        a = b;
-        b = t;
-    }
-    const double ex = threadIdx.x ? a[threadIdx.x - 1] : 0.0;
-    total = a[BB - 1];
-    __syncthreads();
-    return ex;
 }
 
 __device__ __forceinline__ bool better(double f, long long k, double bf, long long bk) {
@@ -133,37 +113,399 @@ __global__ void k_batch_init(const int64_t *so, const int64_t *to, int nplots, i
     st[p] = z;
 }
 
-// one workgroup per plot: FRMSD argmin over the plot's r in (distance, index) order
-__global__ __launch_bounds__(BB) void k_batch_fraction(const double *rs, const int64_t *so,
-                                                       const double *lams, PlotState *st) {
-    __shared__ double s[2 * BB];
-    __shared__ double s_f[BB];
-    __shared__ long long s_k[BB];
+// ---------------------------------------------------------------- per-plot selection
+// ficp.py:73-86 for one plot per workgroup, without sorting the plot: the FRMSD-optimal
+// k needs the exact order only where the FRMSD curve can hold its minimum.
+//  1. key range of the plot's finite rows (r = inf / NaN rows sort last and never win:
+//     every FRMSD from them on is inf or NaN, never < the running minimum);
+//  2. LDS histogram of the keys into SB buckets (count + fp64 sum of r);
+//  3. prefix counts/sums over the buckets; U = the smallest upper bound of h (the log2
+//     form of FRMSD, frmsd_bounds.h) at a bucket end; the candidate window = the buckets
+//     from the first to the last whose lower bound is <= U (the minimum lies inside);
+//  4. S_base = the sum of r below the window (each thread's rows in a fixed order, then a
+//     fixed reduction tree: deterministic), window rows appended to a scratch region;
+//  5. exact (key, row) order of the window: rank of each row inside its bucket;
+//  6. prefix sums over the window in that order, FRMSD of every window position, first
+//     minimum (strict <, ascending k).
+// The bucket sums only feed the bounds (kMarg covers their rounding); every FRMSD value
+// compared comes from the deterministic S_base + window prefix sums.
+constexpr int ST = 512;          // threads
+constexpr int SWV = ST / 64;
+constexpr int SB = 2048;         // buckets
+constexpr int SB_LOG = 11;
+constexpr int SPER = SB / ST;    // buckets per thread in the scans
+constexpr int RPT = 32;          // rows per thread kept in registers (plots <= 16384 rows)
+constexpr int SRP = 4;           // window rows per thread per scan chunk
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ double wave_sum_d(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = x + __shfl_xor(x, o, 64);  // same bits on every lane
+    return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T y = __shfl_up(x, o, 64);
+        if (lane >= o) x = x + y;
+    }
+    return x;
+}
+
+struct SelRed {
+    double d[SWV];
+    u64 a[SWV], b[SWV];
+    unsigned c[SWV];
+    long long l[SWV];
+};
+
+// block sum of a double in a fixed order (deterministic, same value on every thread)
+__device__ __forceinline__ double blk_sum_d(double x, SelRed &r) {
+    x = wave_sum_d(x);
+    if ((threadIdx.x & 63) == 0) r.d[threadIdx.x >> 6] = x;
+    __syncthreads();
+    double t = r.d[0];
+#pragma unroll
+    for (int w = 1; w < SWV; ++w) t = t + r.d[w];
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ double blk_min_d(double x, SelRed &r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, 64));
+    if ((threadIdx.x & 63) == 0) r.d[threadIdx.x >> 6] = x;
+    __syncthreads();
+    double t = r.d[0];
+#pragma unroll
+    for (int w = 1; w < SWV; ++w) t = fmin(t, r.d[w]);
+    __syncthreads();
+    return t;
+}
+
+// {max a, max b, sum c} over the block
+__device__ __forceinline__ void blk_max2_sum(u64 &a, u64 &b, unsigned &c, SelRed &r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const u64 xa = __shfl_xor(a, o, 64), xb = __shfl_xor(b, o, 64);
+        a = xa > a ? xa : a;
+        b = xb > b ? xb : b;
+        c += __shfl_xor(c, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        r.a[threadIdx.x >> 6] = a;
+        r.b[threadIdx.x >> 6] = b;
+        r.c[threadIdx.x >> 6] = c;
+    }
+    __syncthreads();
+    a = r.a[0];
+    b = r.b[0];
+    c = r.c[0];
+#pragma unroll
+    for (int w = 1; w < SWV; ++w) {
+        a = r.a[w] > a ? r.a[w] : a;
+        b = r.b[w] > b ? r.b[w] : b;
+        c += r.c[w];
+    }
+    __syncthreads();
+}
+
+// {min lo, max hi} over the block
+__device__ __forceinline__ void blk_minmax_ll(long long &lo, long long &hi, SelRed &r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (long long)__shfl_xor(lo, o, 64));
+        hi = max(hi, (long long)__shfl_xor(hi, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        r.l[threadIdx.x >> 6] = lo;
+        r.a[threadIdx.x >> 6] = (u64)hi;
+    }
+    __syncthreads();
+    lo = r.l[0];
+    hi = (long long)r.a[0];
+#pragma unroll
+    for (int w = 1; w < SWV; ++w) {
+        lo = min(lo, r.l[w]);
+        hi = max(hi, (long long)r.a[w]);
+    }
+    __syncthreads();
+}
+
+// exclusive scan over the block (thread order) of a count and a sum; fixed schedule
+__device__ __forceinline__ void blk_excl_scan2(unsigned &c, double &x, SelRed &r) {
+    const unsigned ci = wave_incl_scan(c);
+    const double xi = wave_incl_scan(x);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned ce = __shfl_up(ci, 1, 64);
+    double xe = __shfl_up(xi, 1, 64);
+    if (lane == 0) {
+        ce = 0;
+        xe = 0.0;
+    }
+    if (lane == 63) {
+        r.c[w] = ci;
+        r.d[w] = xi;
+    }
+    __syncthreads();
+    unsigned cp = 0;
+    double xp = 0.0;
+    for (int v = 0; v < w; ++v) {
+        cp += r.c[v];
+        xp = xp + r.d[v];
+    }
+    __syncthreads();
+    c = cp + ce;
+    x = xp + xe;
+}
+
+// exclusive scan of a double over the block + the block total; fixed schedule
+__device__ __forceinline__ double blk_excl_scan_d(double x, double &total, SelRed &r) {
+    const double xi = wave_incl_scan(x);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double xe = __shfl_up(xi, 1, 64);
+    if (lane == 0) xe = 0.0;
+    if (lane == 63) r.d[w] = xi;
+    __syncthreads();
+    double xp = 0.0, tot = 0.0;
+#pragma unroll
+    for (int v = 0; v < SWV; ++v) {
+        if (v < w) xp = xp + r.d[v];
+        tot = tot + r.d[v];
+    }
+    __syncthreads();
+    total = tot;
+    return xp + xe;
+}
+
+__device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed &r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double of = __shfl_xor(f, o, 64);
+        const long long ok = __shfl_xor(k, o, 64);
+        if (better(of, ok, f, k)) {
+            f = of;
+            k = ok;
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        r.d[threadIdx.x >> 6] = f;
+        r.l[threadIdx.x >> 6] = k;
+    }
+    __syncthreads();
+    f = r.d[0];
+    k = r.l[0];
+#pragma unroll
+    for (int w = 1; w < SWV; ++w)
+        if (better(r.d[w], r.l[w], f, k)) {
+            f = r.d[w];
+            k = r.l[w];
+        }
+    __syncthreads();
+}
+
+// every row of the plot with its key and r: CACHED keeps them in registers (RPT per
+// thread, rows past the plot hold r = inf), otherwise they are re-read per pass
+#define SEL_ROWS(BODY)                                                              \
+    if (CACHED) {                                                                   \
+        _Pragma("unroll") for (int q = 0; q < RPT; ++q) {                           \
+            const int64_t i = b + t + (int64_t)q * ST;                              \
+            const u64 kk = kc[q];                                                   \
+            const double rv = rc[q];                                                \
+            (void)i;                                                                \
+            BODY                                                                    \
+        }                                                                           \
+    } else {                                                                        \
+        for (int64_t i = b + t; i < e; i += ST) {                                   \
+            const u64 kk = key[i];                                                  \
+            const double rv = r[i];                                                 \
+            (void)i;                                                                \
+            BODY                                                                    \
+        }                                                                           \
+    }
+
+template <bool CACHED>
+__global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key,
+                                                     const double *__restrict__ r,
+                                                     const int64_t *__restrict__ so,
+                                                     const double *__restrict__ lams,
+                                                     PlotState *__restrict__ st,
+                                                     BatchSelScratch ws) {
+    __shared__ unsigned s_cnt[SB];  // counts, then exclusive bucket starts
+    __shared__ double s_sum[SB];    // sums, then per-bucket fill counters (as unsigned)
+    __shared__ SelRed red;
+    __shared__ long long s_k[2];
     const int p = blockIdx.x;
+    const int t = threadIdx.x;
     if (st[p].phase == PH_DONE) return;  // uniform per workgroup
     const double lam = lams[st[p].stage];
+    const double pe = 2.0 * lam + 1.0;
     const int64_t b = so[p], e = so[p + 1];
     const long long N = e - b;
-    double run = 0.0, bf = INFINITY;
+    u64 kc[CACHED ? RPT : 1];
+    double rc[CACHED ? RPT : 1];
+    if (CACHED) {
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int64_t i = b + t + (int64_t)q * ST;
+            kc[q] = i < e ? key[i] : ~0ULL;
+            rc[q] = i < e ? r[i] : INFINITY;
+        }
+    }
+    // 1. key range of the finite rows
+    u64 amin = 0, kmax = 0;
+    unsigned nfin = 0;
+    SEL_ROWS(if (rv < INFINITY) {
+        amin = max(amin, ~kk);
+        kmax = max(kmax, kk);
+        ++nfin;
+    })
+    blk_max2_sum(amin, kmax, nfin, red);
+    if (nfin == 0) {  // every distance inf / NaN: the reference keeps (0.0, 0)
+        if (t == 0) {
+            st[p].k = 0;
+            st[p].frac = 0.0;
+            st[p].frmsd = INFINITY;
+        }
+        return;
+    }
+    const u64 kmin = ~amin;
+    const int nb = fb::bits_of(kmax - kmin);
+    const int sh = nb > SB_LOG ? nb - SB_LOG : 0;
+    // 2. histogram
+#pragma unroll
+    for (int j = 0; j < SPER; ++j) {
+        s_cnt[t * SPER + j] = 0u;
+        s_sum[t * SPER + j] = 0.0;
+    }
+    __syncthreads();
+    SEL_ROWS(if (rv < INFINITY) {
+        const int bk = (int)((kk - kmin) >> sh);
+        atomicAdd(&s_cnt[bk], 1u);
+        atomicAdd(&s_sum[bk], rv);
+    })
+    __syncthreads();
+    // 3. bounds over the buckets (thread t owns buckets t*SPER .. t*SPER + SPER - 1)
+    unsigned c[SPER];
+    double sm[SPER];
+    unsigned tc = 0;
+    double ts = 0.0;
+#pragma unroll
+    for (int j = 0; j < SPER; ++j) {
+        c[j] = s_cnt[t * SPER + j];
+        sm[j] = s_sum[t * SPER + j];
+        tc += c[j];
+        ts = ts + sm[j];
+    }
+    unsigned Cex = tc;
+    double Pex = ts;
+    blk_excl_scan2(Cex, Pex, red);
+    double U = INFINITY;
+    {
+        long long C = Cex;
+        double P = Pex;
+#pragma unroll
+        for (int j = 0; j < SPER; ++j) {
+            if (c[j]) {
+                C += c[j];
+                P = P + sm[j];
+                U = fmin(U, fb::h_of(C, P, pe) + fb::kMarg);
+            }
+        }
+    }
+    U = blk_min_d(U, red);
+    long long bmin = SB, bmax = -1;
+    {
+        long long C = Cex;
+        double P = Pex;
+#pragma unroll
+        for (int j = 0; j < SPER; ++j) {
+            const int bk = t * SPER + j;
+            if (c[j]) {
+                const double lb = fb::block_lb(C, c[j], P, fb::lo_r(kmin + ((u64)bk << sh)), pe);
+                if (!(lb > U) || !(pe >= 1.0)) {
+                    bmin = min(bmin, (long long)bk);
+                    bmax = max(bmax, (long long)bk);
+                }
+            }
+            C += c[j];
+            P = P + sm[j];
+        }
+    }
+    blk_minmax_ll(bmin, bmax, red);
+    // bucket starts (rows before each bucket) replace the counts; fill counters zeroed
+    unsigned *fill = reinterpret_cast<unsigned *>(s_sum);
+    {
+        unsigned C = Cex;
+#pragma unroll
+        for (int j = 0; j < SPER; ++j) {
+            const int bk = t * SPER + j;
+            s_cnt[bk] = C;
+            fill[bk] = 0u;
+            if (bk == bmin) s_k[0] = C;
+            if (bk == bmax) s_k[1] = C + c[j];
+            C += c[j];
+        }
+    }
+    __syncthreads();
+    const long long K0 = s_k[0];
+    const long long W = s_k[1] - K0;
+    // 4. sum of r below the window (deterministic), window rows to scratch
+    double sb = 0.0;
+    SEL_ROWS(if (rv < INFINITY) {
+        const int bk = (int)((kk - kmin) >> sh);
+        if (bk < bmin) {
+            sb = sb + rv;
+        } else if (bk <= bmax) {
+            const int64_t slot = b + (int64_t)s_cnt[bk] - K0 + atomicAdd(&fill[bk], 1u);
+            ws.wkey[slot] = kk;
+            ws.wrow[slot] = (uint32_t)i;
+            ws.wr[slot] = rv;
+        }
+    })
+    const double S_base = blk_sum_d(sb, red);  // its barriers also publish the scratch
+    // 5. exact (key, row) order of the window: rank inside the row's bucket
+    for (long long q = t; q < W; q += ST) {
+        const u64 kq = ws.wkey[b + q];
+        const uint32_t rq = ws.wrow[b + q];
+        const int bk = (int)((kq - kmin) >> sh);
+        const long long s0 = (long long)s_cnt[bk] - K0;
+        const long long s1 = (long long)(bk + 1 < SB ? s_cnt[bk + 1] : nfin) - K0;
+        long long rank = 0;
+        for (long long j = s0; j < s1; ++j) {
+            const u64 kj = ws.wkey[b + j];
+            rank += (kj < kq) || (kj == kq && ws.wrow[b + j] < rq);
+        }
+        const int64_t pos = b + s0 + rank;
+        ws.skey[pos] = kq;
+        ws.srow[pos] = rq;
+        ws.sr[pos] = ws.wr[b + q];
+    }
+    __syncthreads();
+    // 6. prefix sums in window order, FRMSD of every window position, first minimum
+    double run = S_base, bf = INFINITY;
     long long bk = 0x7fffffffffffffffLL;
-    for (int64_t c = b; c < e; c += BB * BI) {
-        const int64_t j0 = c + (int64_t)threadIdx.x * BI;
-        double v[BI];
+    for (long long c0 = 0; c0 < W; c0 += (long long)ST * SRP) {
+        const long long j0 = c0 + (long long)t * SRP;
+        double v[SRP];
         double acc = 0.0;
 #pragma unroll
-        for (int q = 0; q < BI; ++q) {
-            v[q] = (j0 + q < e) ? rs[j0 + q] : 0.0;
+        for (int q = 0; q < SRP; ++q) {
+            v[q] = (j0 + q < W) ? ws.sr[b + j0 + q] : 0.0;
             acc = acc + v[q];
         }
         double tot;
-        double S = run + bscan(acc, s, tot);
+        double S = run + blk_excl_scan_d(acc, tot, red);
 #pragma unroll
-        for (int q = 0; q < BI; ++q) {
-            if (j0 + q < e) {
+        for (int q = 0; q < SRP; ++q) {
+            if (j0 + q < W) {
                 S = S + v[q];
-                const long long k = j0 + q - b + 1;
-                const double frac = (double)k / (double)N;
-                const double f = (1.0 / pow(frac, lam)) * sqrt(S / (double)k);
+                const long long k = K0 + j0 + q + 1;
+                const double f = (1.0 / pow((double)k / (double)N, lam)) * sqrt(S / (double)k);
                 if (f < bf) {  // ascending k: strict < keeps the first minimum (ficp.py:84)
                     bf = f;
                     bk = k;
@@ -172,37 +514,29 @@ __global__ __launch_bounds__(BB) void k_batch_fraction(const double *rs, const i
         }
         run = run + tot;
     }
-    s_f[threadIdx.x] = bf;
-    s_k[threadIdx.x] = bk;
-    __syncthreads();
-    for (int w = BB / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w &&
-            better(s_f[threadIdx.x + w], s_k[threadIdx.x + w], s_f[threadIdx.x], s_k[threadIdx.x])) {
-            s_f[threadIdx.x] = s_f[threadIdx.x + w];
-            s_k[threadIdx.x] = s_k[threadIdx.x + w];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        if (s_k[0] == 0x7fffffffffffffffLL) {  // every FRMSD NaN: the reference keeps (0.0, 0)
+    blk_argmin(bf, bk, red);
+    if (t == 0) {
+        if (bk == 0x7fffffffffffffffLL) {  // every FRMSD NaN: the reference keeps (0.0, 0)
             st[p].k = 0;
             st[p].frac = 0.0;
             st[p].frmsd = INFINITY;
         } else {
-            st[p].k = s_k[0];
-            st[p].frac = (double)s_k[0] / (double)N;
-            st[p].frmsd = s_f[0];
+            st[p].k = bk;
+            st[p].frac = (double)bk / (double)N;
+            st[p].frmsd = bf;
+            st[p].tkey = ws.skey[b + (bk - K0 - 1)];
+            st[p].trow = (long long)ws.srow[b + (bk - K0 - 1)];
         }
     }
 }
+#undef SEL_ROWS
 
 // one workgroup per looping plot: rigid fit on the plot's first k trees of the order
 __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double *sy,
                                                   const double *cx, const double *cy,
                                                   const unsigned long long *key,
-                                                  const uint32_t *order, const int64_t *so,
-                                                  const PlotGrid *grids, int allow_refl,
-                                                  PlotState *st) {
+                                                  const int64_t *so, const PlotGrid *grids,
+                                                  int allow_refl, PlotState *st) {
     __shared__ double s[BB];
     const int p = blockIdx.x;
     if (st[p].phase != PH_LOOP) {
@@ -210,9 +544,9 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
         return;
     }
     const int64_t b = so[p], e = so[p + 1];
-    const long long k = st[p].k;
-    const int64_t t = (int64_t)order[b + k - 1];  // k >= 1 in the loop phase
-    const unsigned long long tk = key[t];
+    const long long k = st[p].k;  // k >= 1 in the loop phase
+    const int64_t t = st[p].trow;  // the k-th row of the (key, row) order (k_batch_select)
+    const unsigned long long tk = st[p].tkey;
     const double px = grids[p].px, py = grids[p].py;
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t i = b + threadIdx.x; i < e; i += BB) {
@@ -357,19 +691,25 @@ hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, i
 }
 
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
-                            const double *cy, const unsigned long long *key,
-                            const uint32_t *order, const int64_t *so, const PlotGrid *grids,
-                            int nplots, int allow_refl, PlotState *st, hipStream_t s) {
+                            const double *cy, const unsigned long long *key, const int64_t *so,
+                            const PlotGrid *grids, int nplots, int allow_refl, PlotState *st,
+                            hipStream_t s) {
     if (nplots <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_batch_fit, dim3(nplots), dim3(BB), 0, s, sx, sy, cx, cy, key, order, so,
-                       grids, allow_refl, st);
+    hipLaunchKernelGGL(k_batch_fit, dim3(nplots), dim3(BB), 0, s, sx, sy, cx, cy, key, so, grids,
+                       allow_refl, st);
     return hipGetLastError();
 }
 
-hipError_t launch_batch_fraction(const double *rs, const int64_t *so, int nplots,
-                                 const double *lambdas, PlotState *st, hipStream_t s) {
+hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,
+                               int nplots, int64_t max_rows, const double *lambdas,
+                               PlotState *st, BatchSelScratch ws, hipStream_t s) {
     if (nplots <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_batch_fraction, dim3(nplots), dim3(BB), 0, s, rs, so, lambdas, st);
+    if (max_rows <= (int64_t)ST * RPT)
+        hipLaunchKernelGGL(k_batch_select<true>, dim3(nplots), dim3(ST), 0, s, key, r, so, lambdas, st,
+                           ws);
+    else
+        hipLaunchKernelGGL(k_batch_select<false>, dim3(nplots), dim3(ST), 0, s, key, r, so, lambdas,
+                           st, ws);
     return hipGetLastError();
 }
 

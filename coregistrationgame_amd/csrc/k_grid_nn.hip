@@ -893,6 +893,27 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
 
 // Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against
 // plot p's own CHM grid (cells cell_base_p.., stems indexed in the concatenated layer).
+__device__ __forceinline__ GridView plot_view(const PlotGrid &pg, const TPt *pts,
+                                              const int32_t *cell_start, int64_t m) {
+    GridView g;
+    g.pts = pts;
+    g.cell_start = cell_start + pg.cell_base;
+    g.x0 = pg.x0;
+    g.y0 = pg.y0;
+    g.h = pg.h;
+    g.inv_h = pg.inv_h;
+    g.margin = pg.margin;
+    g.gx = pg.gx;
+    g.gy = pg.gy;
+    g.m = m;
+    return g;
+}
+
+// The single-plot kernel's certified reuse per plot: warm calls (a.warm_c) try every
+// live query's certificate (cert_try) against its own plot's grid; the workgroup's
+// uncertified queries are then packed onto its first lanes, GS lanes per query when
+// few remain, each scanning with its own plot's grid (a workgroup may straddle plots).
+// The cold call runs the plain scan and stores G = 0.  Converged plots are skipped.
 template <int MD>
 __global__ __launch_bounds__(256) void k_nn_grid_batch(NNArgs a, const int32_t *__restrict__ plot_of,
                                                        const PlotGrid *__restrict__ grids,
@@ -900,29 +921,60 @@ __global__ __launch_bounds__(256) void k_nn_grid_batch(NNArgs a, const int32_t *
                                                        const int32_t *__restrict__ cell_start,
                                                        const PlotState *__restrict__ st) {
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    unsigned long long kmin_c = 0, kmax = 0;
+    unsigned long long kmin_c = 0, kmax = 0;  // (no key range: the batch selection is per plot)
+    const Stems S = stems_of(pts, m);
+    int p = 0;
+    bool live = false;
     if (i < a.n) {
-        const int p = plot_of[i];
-        if (st[p].phase != PH_DONE) {
-            const PlotGrid pg = grids[p];
-            GridView g;
-            g.pts = pts;
-            g.cell_start = cell_start + pg.cell_base;
-            g.x0 = pg.x0;
-            g.y0 = pg.y0;
-            g.h = pg.h;
-            g.inv_h = pg.inv_h;
-            g.margin = pg.margin;
-            g.gx = pg.gx;
-            g.gy = pg.gy;
-            g.m = m;
-            nn_query<MD>(a, g, stems_of(pts, m), i, st[p].apply ? st[p].T : nullptr, kmin_c, kmax);
-        } else {  // converged plot: its last outputs stay, its keys stay inside the range
-            kmin_c = ~a.key[i];
-            kmax = a.key[i];
-        }
+        p = plot_of[i];
+        live = st[p].phase != PH_DONE;
     }
-    if (a.range) block_range_store(a.range, true, kmin_c, kmax);
+    const double *T = (live && st[p].apply) ? st[p].T : nullptr;
+    if (a.gap && a.warm_c) {
+        __shared__ int s_list[256];
+        __shared__ double s_mv[256];
+        __shared__ int s_n;
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        double mv = 0.0;
+        bool pend = false;
+        if (live) {
+            const GridView g = plot_view(grids[p], pts, cell_start, m);
+            pend = !cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv);
+        }
+        const unsigned long long msk = __ballot(pend);
+        const int lane = threadIdx.x & 63;
+        int base = 0;
+        if (lane == 0 && msk) base = atomicAdd(&s_n, __popcll(msk));
+        base = __shfl(base, 0);
+        if (pend) {
+            const int q = base + __popcll(msk & ((1ULL << lane) - 1));
+            s_list[q] = (int)(i & 255);
+            s_mv[q] = mv;
+        }
+        __syncthreads();
+        const int tot = s_n;
+        const int64_t i0 = i - threadIdx.x;
+        const int t = threadIdx.x;
+        int gs = 1;
+        if (a.cert_block >= 8 && tot <= 32) gs = 8;
+        else if (a.cert_block >= 4 && tot <= 64) gs = 4;
+        else if (a.cert_block >= 2 && tot <= 128) gs = 2;
+        if (t < tot * gs) {
+            const int q = t / gs;
+            const int64_t iq = i0 + s_list[q];
+            const GridView gq = plot_view(grids[plot_of[iq]], pts, cell_start, m);
+            const double pad = cert_pad(gq, s_mv[q]);
+            if (gs == 8) cert_scan_group<MD, 8>(a, gq, S, iq, t & 7, pad, kmin_c, kmax);
+            else if (gs == 4) cert_scan_group<MD, 4>(a, gq, S, iq, t & 3, pad, kmin_c, kmax);
+            else if (gs == 2) cert_scan_group<MD, 2>(a, gq, S, iq, t & 1, pad, kmin_c, kmax);
+            else cert_scan<MD>(a, gq, S, iq, true, pad, kmin_c, kmax);
+        }
+    } else if (live) {
+        const GridView g = plot_view(grids[p], pts, cell_start, m);
+        nn_query<MD>(a, g, S, i, T, kmin_c, kmax);
+        if (a.gap) a.gap[i] = 0.0;  // the cold call stores no certificate (k_nn_grid)
+    }
 }
 
 constexpr int kTile = 256;

@@ -34,6 +34,7 @@
 // k and threshold pair depend only on the exact, deterministic prefix sums.
 // At C3 (1M x 1M) the candidate set holds 15-5000 rows, so step (a) is the normal case.
 #include "ficp_internal.h"
+#include "frmsd_bounds.h"
 
 #include <math.h>
 
@@ -189,18 +190,16 @@ SelWS carve(void *tmp, int64_t n) {
     return w;
 }
 
-__device__ __forceinline__ int bits_of(u64 v) { return v ? 64 - __clzll((long long)v) : 0; }
+using fb::bits_of;
+using fb::block_lb;
+using fb::h_of;
+using fb::kMarg;
+using fb::lg2;
+using fb::lo_r;
 
 __device__ __forceinline__ int sel_shift(u64 kmin, u64 kmax) {
     const int b = bits_of(kmax > kmin ? kmax - kmin : 0ULL);
     return b > NB_LOG ? b - NB_LOG : 0;
-}
-
-// smallest r = d^2 of any row whose key is >= klo (d = sqrt(d2) correctly rounded)
-__device__ __forceinline__ double lo_r(u64 klo) {
-    if (!(klo >> 63)) return 0.0;
-    const double d = __longlong_as_double((long long)(klo & 0x7fffffffffffffffULL));
-    return d * d * (1.0 - 1e-15);
 }
 
 // exponent e_b with r < 2^e_b for every row of bucket b (1024: the bucket holds inf/NaN)
@@ -214,32 +213,7 @@ __device__ __forceinline__ int bucket_exp(u64 kmin, u64 kmax, int s, int b) {
     return min(2 * ex - 2044, 1024);  // 1024: the bucket may hold inf / NaN or overflow
 }
 
-// Bounds work on h(k, S) = log2(S) - p log2(k), p = 2 lambda + 1, a monotone function of
-// FRMSD(k) = N^lambda k^-lambda sqrt(S / k) (no pow per bucket).  lg2 is exact in the
-// exponent and ~1e-7 in the mantissa (v_log_f32); kMarg (log2 units) covers that, the
-// double rounding of the prefix sums and the refinement levels' LDS float sums.
-constexpr double kMarg = 1e-5;
-
-__device__ __forceinline__ double lg2(double x) {
-    if (!(x > 0.0)) return x == 0.0 ? -INFINITY : NAN;
-    if (!(x < INFINITY)) return INFINITY;
-    int e;
-    const double m = frexp(x, &e);  // [0.5, 1)
-    return (double)e + (double)__builtin_amdgcn_logf((float)m);
-}
-
-__device__ __forceinline__ double h_of(long long k, double S, double p) {
-    return lg2(S) - p * lg2((double)k);
-}
-
-// lower bound of h over k in (C0, C0 + c] when the c rows there are all >= lo: the
-// smaller end value (quasi-concave in k for p >= 1, see the header), minus the margin
-__device__ __forceinline__ double block_lb(long long C0, long long c, double P0, double lo,
-                                           double p) {
-    const double a = h_of(C0 + 1, P0 + lo, p);
-    const double b = h_of(C0 + c, P0 + (double)c * lo, p);
-    return fmin(a, b) - kMarg;
-}
+// Bounds work on h(k, S) (frmsd_bounds.h): no pow per bucket.
 
 __device__ __forceinline__ bool better(double f, long long k, double bf, long long bk) {
     return f < bf || (f == bf && k < bk);

@@ -23,6 +23,26 @@ using namespace ficp_capi;
 
 namespace ficp_capi {
 thread_local std::string g_err;
+
+// Wait for a done flag that a kernel stores into coherent pinned memory (-1 = not yet
+// written).  The stream is queried now and then so that a device error or a drained
+// stream without the store ends the wait instead of spinning forever.
+int poll_flag(ficp_ctx *c, int *flag, int &v) {
+    for (uint64_t spin = 1;; ++spin) {
+        v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
+        if (v != -1) return FICP_OK;
+        if ((spin & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) {
+                v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
+                if (v != -1) return FICP_OK;
+                return fail(FICP_EHIP, "device loop flag was not written");
+            }
+            if (e != hipErrorNotReady) return fail(FICP_EHIP, "device loop: %s", hipGetErrorString(e));
+        }
+        __builtin_ia32_pause();
+    }
+}
 }  // namespace ficp_capi
 
 namespace {
@@ -30,7 +50,6 @@ namespace {
 // bounding box of the CHM layer (grid geometry and the fit's pivot), once per target
 // Run the report kernel (device segments -> coherent pinned host memory) and poll its
 // flag: one short host wait instead of hipMemcpyAsync + hipStreamSynchronize.
-int poll_flag(ficp_ctx *c, int *flag, int &v);
 int report_wait(ficp_ctx *c, const ReportSeg &a, const ReportSeg &b, const ReportSeg &d,
                 unsigned long long *t_end = nullptr) {
     __atomic_store_n(&c->h_rep->flag, -1, __ATOMIC_RELAXED);
@@ -366,26 +385,6 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
                               c->wy.as<double>(), sz ? c->wz.as<double>() : nullptr,
                               c->worig.as<uint32_t>(), c->stream));
     return FICP_OK;
-}
-
-// Wait for a done flag that a kernel stores into coherent pinned memory (-1 = not yet
-// written).  The stream is queried now and then so that a device error or a drained
-// stream without the store ends the wait instead of spinning forever.
-int poll_flag(ficp_ctx *c, int *flag, int &v) {
-    for (uint64_t spin = 1;; ++spin) {
-        v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
-        if (v != -1) return FICP_OK;
-        if ((spin & 1023) == 0) {
-            const hipError_t e = hipStreamQuery(c->stream);
-            if (e == hipSuccess) {
-                v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
-                if (v != -1) return FICP_OK;
-                return fail(FICP_EHIP, "device loop flag was not written");
-            }
-            if (e != hipErrorNotReady) return fail(FICP_EHIP, "device loop: %s", hipGetErrorString(e));
-        }
-        __builtin_ia32_pause();
-    }
 }
 
 // the device-resident ICP: stages of ficp.py:122-147

@@ -11,7 +11,10 @@
 //   -> batch_select  (one workgroup per plot: FRMSD-optimal k + selection threshold)
 //   -> batch_update  (per-plot convergence test ficp.py:142, stage switch ficp.py:152)
 //
-// The host reads one counter (live plots) per batch iteration.
+// The update kernel stores the number of plots still running into a ring of coherent
+// pinned words; the host enqueues batch iteration i + 1 before it polls iteration i's
+// word, so the device never idles on the host.  A finished batch leaves one iteration
+// of no-op launches queued (every kernel skips converged plots).
 #include "capi_internal.h"
 
 #include <math.h>
@@ -22,24 +25,25 @@
 #include <vector>
 
 struct BatchBufs {
-    DevBuf so, to, plot_of, tplot, grids, st, active, bb, lams;
+    DevBuf so, to, plot_of, tplot, grids, st, bb, lams;
     DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp;
     DevBuf key, gap, r, ccx, ccy, bp, dz2, wkey, skey, wrow, srow, wr, sr;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
-    unsigned int *h_active = nullptr;      // pinned
+    int *h_flag = nullptr;                 // coherent pinned ring: plots still running
 };
+constexpr int kBatchRing = 4;
 
 void batch_release(BatchBufs *b) {
     if (!b) return;
     DevBuf *bufs[] = {&b->so,       &b->to,      &b->plot_of,  &b->tplot, &b->grids, &b->st,
-                      &b->active,   &b->bb,      &b->lams,     &b->cell_of, &b->counts,
+                      &b->bb,      &b->lams,     &b->cell_of, &b->counts,
                       &b->fill,     &b->cell_start, &b->pts,   &b->scan_tmp, &b->key, &b->gap,
                       &b->r,        &b->ccx,     &b->ccy,      &b->wkey,  &b->skey,  &b->wrow,
                       &b->srow,     &b->wr,      &b->sr,       &b->sx,    &b->sy,    &b->sz,
                       &b->tx,       &b->ty,      &b->tz,       &b->stage, &b->bp,
                       &b->dz2};
     for (DevBuf *d : bufs) d->release();
-    if (b->h_active) (void)hipHostFree(b->h_active);
+    if (b->h_flag) (void)hipHostFree(b->h_flag);
     delete b;
 }
 
@@ -131,12 +135,11 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                ficp_plot_stats *per_plot) {
     const int64_t n = so_h[nplots], m = to_h[nplots];
     BatchBufs &b = *batch_of(c);
-    if (!b.h_active)
-        HIPCHK(hipHostMalloc((void **)&b.h_active, sizeof(unsigned int), hipHostMallocDefault));
+    if (!b.h_flag)
+        HIPCHK(hipHostMalloc((void **)&b.h_flag, kBatchRing * sizeof(int), hipHostMallocCoherent));
     CHK(b.so.ensure((size_t)(nplots + 1) * 8));
     CHK(b.to.ensure((size_t)(nplots + 1) * 8));
     CHK(b.st.ensure((size_t)nplots * sizeof(PlotState)));
-    CHK(b.active.ensure(64));
     CHK(b.lams.ensure((size_t)std::max(nstages, 1) * 8));
     HIPCHK(hipMemcpyAsync(b.so.p, so_h, (size_t)(nplots + 1) * 8, hipMemcpyHostToDevice,
                           c->stream));
@@ -197,7 +200,9 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         PlotState *st = b.st.as<PlotState>();
         // every plot makes at most nstages * (max_iter + 1) NN calls
         const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1) + 1;
-        for (int64_t bit = 0; bit < cap; ++bit) {
+        auto enqueue = [&](int64_t bit) -> int {
+            int *flag = &b.h_flag[bit % kBatchRing];
+            __atomic_store_n(flag, -1, __ATOMIC_RELEASE);
             {
                 ProfScope ps(c, P_FIT, "batch_fit");
                 HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
@@ -218,13 +223,19 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                                            b.so.as<int64_t>(), nplots, max_rows,
                                            b.lams.as<double>(), st, ws, c->stream));
             }
-            HIPCHK(launch_batch_update(nplots, nstages, threshold, max_iter, st,
-                                       (unsigned int *)b.active.p, c->stream));
-            HIPCHK(hipMemcpyAsync(b.h_active, b.active.p, 4, hipMemcpyDeviceToHost, c->stream));
-            CHK(sync(c));
-            if (*b.h_active == 0) break;
+            HIPCHK(launch_batch_update(nplots, nstages, threshold, max_iter, st, flag, c->stream));
+            return FICP_OK;
+        };
+        bool finished = false;
+        CHK(enqueue(0));
+        for (int64_t w = 0; w < cap && !finished; ++w) {
+            if (w + 1 < cap) CHK(enqueue(w + 1));  // one batch iteration ahead
+            int live = 0;
+            CHK(poll_flag(c, &b.h_flag[w % kBatchRing], live));
+            finished = live == 0;
         }
-        if (*b.h_active != 0) return fail(FICP_EHIP, "batch did not converge within its bound");
+        if (!finished) return fail(FICP_EHIP, "batch did not converge within its bound");
+
     }
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     if (per_plot) {

@@ -243,4 +243,8 @@ inline int upload_rows(ficp_ctx *c, const double *rows, int64_t n, int64_t ld, i
                                c1.as<double>(), c2 ? c2->as<double>() : nullptr, c->stream));
     return FICP_OK;
 }
+// Wait for a flag that a kernel stores (system scope) into coherent pinned memory; -1 =
+// not yet written.  Ends with an error when the stream fails or drains without it.
+int poll_flag(ficp_ctx *c, int *flag, int &v);
+
 }  // namespace ficp_capi

@@ -587,7 +587,8 @@ struct BatchSelScratch {
 hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,
                                int nplots, int64_t max_rows, const double *lambdas,
                                PlotState *st, BatchSelScratch ws, hipStream_t s);
+// *flag (coherent pinned host memory) <- number of plots still running
 hipError_t launch_batch_update(int nplots, int nstages, double threshold, int max_iter,
-                               PlotState *st, unsigned int *active, hipStream_t s);
+                               PlotState *st, int *flag, hipStream_t s);
 
 }  // namespace ficp

@@ -616,11 +616,13 @@ __device__ __forceinline__ void end_stage(PlotState &s, int nstages) {
     }
 }
 
-// one thread per plot: the convergence logic of ficp.py:125-145 per plot
-__global__ void k_batch_update(int nplots, int nstages, double threshold, int max_iter,
-                               PlotState *st, unsigned int *active) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= nplots) return;
+// one workgroup, one thread per plot (strided): the convergence logic of ficp.py:125-145
+// per plot; the number of plots still running is stored (system scope, release) into
+// *flag in coherent pinned host memory, which the host polls while the next batch
+// iteration already runs
+constexpr int UT = 1024;
+__device__ __forceinline__ bool update_plot(PlotState *st, int p, int nstages, double threshold,
+                                            int max_iter) {
     PlotState s = st[p];
     if (s.phase != PH_DONE) {
         s.n_nn += 1;
@@ -653,7 +655,25 @@ __global__ void k_batch_update(int nplots, int nstages, double threshold, int ma
         s.apply = 0;
         st[p] = s;
     }
-    if (s.phase != PH_DONE) atomicAdd(active, 1u);
+    return s.phase != PH_DONE;
+}
+
+__global__ __launch_bounds__(UT) void k_batch_update(int nplots, int nstages, double threshold,
+                                                     int max_iter, PlotState *st, int *flag) {
+    __shared__ int s_live[UT / 64];
+    int live = 0;
+    for (int p = threadIdx.x; p < nplots; p += UT)
+        live += update_plot(st, p, nstages, threshold, max_iter) ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o, 64);
+    if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = live;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < UT / 64; ++w) tot += s_live[w];
+        __threadfence_system();
+        __hip_atomic_store(flag, tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
@@ -714,11 +734,9 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
 }
 
 hipError_t launch_batch_update(int nplots, int nstages, double threshold, int max_iter,
-                               PlotState *st, unsigned int *active, hipStream_t s) {
-    hipError_t e = launch_atomic_zero32(active, 1, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_batch_update, dim3(nblk(std::max(nplots, 1))), dim3(256), 0, s, nplots,
-                       nstages, threshold, max_iter, st, active);
+                               PlotState *st, int *flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_batch_update, dim3(1), dim3(UT), 0, s, nplots, nstages, threshold,
+                       max_iter, st, flag);
     return hipGetLastError();
 }
 

@@ -190,20 +190,7 @@ int ensure_work(ficp_ctx *c, int64_t n) {
     return FICP_OK;
 }
 
-// FICP_SELECT=0: the run loop uses the full residual sort + prefix scan instead of the
-// bucketed selection (A/B checks; both give the same k and threshold)
-bool use_select() {
-    static const bool on = !getenv("FICP_SELECT") || atoi(getenv("FICP_SELECT")) != 0;
-    return on;
-}
-
 unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long long>(); }
-
-// FICP_NN_CERT=0: no certified match reuse (every warm query scans)
-static bool nn_cert_on() {
-    static const bool on = !getenv("FICP_NN_CERT") || atoi(getenv("FICP_NN_CERT")) != 0;
-    return on;
-}
 
 // NN of the device source (sx, sy, sz) against the target; optional pending transform.
 // With want_keys the sort inputs (key, range, r, matched XY) are produced too (and dist
@@ -237,15 +224,13 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             CHK(c->dz2.ensure(n * 8));
             a.dz2 = c->dz2.as<double>();
             a.warm_c = warm == 2 ? 1 : 0;
-            // certified reuse of the match (nn_query_cert): the bound G and the match slot
-            if (nn_cert_on()) {
-                CHK(c->gap.ensure(n * 8));
-                CHK(c->bp.ensure(n * 4));
-                a.gap = c->gap.as<double>();
-                a.out_bp = c->bp.as<int32_t>();
-            }
-            static const int cblk = getenv("FICP_CERT_BLOCK") ? atoi(getenv("FICP_CERT_BLOCK")) : 8;
-            a.cert_block = cblk;
+            // certified reuse of the match (nn_query_cert): the bound G and the match slot;
+            // a workgroup's uncertified queries packed, up to 8 lanes per query
+            CHK(c->gap.ensure(n * 8));
+            CHK(c->bp.ensure(n * 4));
+            a.gap = c->gap.as<double>();
+            a.out_bp = c->bp.as<int32_t>();
+            a.cert_block = 8;
         }
         {
             KernelEvents ke(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
@@ -271,57 +256,6 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     return FICP_OK;
 }
 
-// FICP_CHECK=1: synchronise after every sort and fail at the first one that raised the
-// sort's error flag; FICP_CHECK=2 also verifies on the host that the order is a
-// permutation sorted by (key64, orig).  Debug only.
-int check_level() {
-    static const int lvl = getenv("FICP_CHECK") ? atoi(getenv("FICP_CHECK")) : 0;
-    return lvl;
-}
-
-int check_sort(ficp_ctx *c, int64_t n, const uint32_t *orig, const char *what) {
-    if (!check_level() || n == 0) return FICP_OK;
-    static int64_t ncall = 0;
-    ++ncall;
-    uint32_t tf = 0;
-    HIPCHK(hipMemcpyAsync(&tf, sort_timeout_flag(c->sort_tmp.p, n), 4, hipMemcpyDeviceToHost,
-                          c->stream));
-    CHK(sync(c));
-    if (tf) return fail(FICP_EHIP, "FICP_CHECK: sort flag %u after %s (sort call %lld, n=%lld)", tf,
-                        what, (long long)ncall, (long long)n);
-    if (check_level() < 2) return FICP_OK;
-    std::vector<uint32_t> ord(n), org(orig ? n : 0);
-    std::vector<unsigned long long> key(n);
-    HIPCHK(hipMemcpy(ord.data(), c->order.p, n * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(key.data(), c->key.p, n * 8, hipMemcpyDeviceToHost));
-    if (orig) HIPCHK(hipMemcpy(org.data(), orig, n * 4, hipMemcpyDeviceToHost));
-    std::vector<char> seen(n, 0);
-    for (int64_t j = 0; j < n; ++j) {
-        if (ord[j] >= (uint64_t)n || seen[ord[j]])
-            return fail(FICP_EHIP, "FICP_CHECK: %s order not a permutation at %lld (v=%u, call %lld)",
-                        what, (long long)j, ord[j], (long long)ncall);
-        seen[ord[j]] = 1;
-    }
-    if (orig) {
-        std::fill(seen.begin(), seen.end(), 0);
-        for (int64_t j = 0; j < n; ++j) {
-            if (org[j] >= (uint64_t)n || seen[org[j]])
-                return fail(FICP_EHIP, "FICP_CHECK: %s orig not a permutation at %lld (call %lld)",
-                            what, (long long)j, (long long)ncall);
-            seen[org[j]] = 1;
-        }
-    }
-    for (int64_t j = 1; j < n; ++j) {
-        const uint32_t a = ord[j - 1], b = ord[j];
-        const unsigned long long ka = key[a], kb = key[b];
-        const uint32_t oa = orig ? org[a] : a, ob = orig ? org[b] : b;
-        if (ka > kb || (ka == kb && oa > ob))
-            return fail(FICP_EHIP, "FICP_CHECK: %s order unsorted at %lld (call %lld)", what,
-                        (long long)j, (long long)ncall);
-    }
-    return FICP_OK;
-}
-
 // sort (key, orig) of the last NN call, then the FRMSD fraction scan
 int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam, const uint32_t *orig,
                     const int *skip = nullptr, const double *lam_dev = nullptr) {
@@ -331,7 +265,6 @@ int sort_and_select(ficp_ctx *c, int64_t n, int64_t N, double lam, const uint32_
                            c->order.as<uint32_t>(), c->r.as<double>(), c->rs.as<double>(),
                            c->sort_tmp.p, skip, c->stream));
     }
-    CHK(check_sort(c, n, orig, "residual sort"));
     {
         ProfScope ps(c, P_FRAC, "fraction");
         HIPCHK(launch_fraction(c->rs.as<double>(), n, N, lam, lam_dev, c->frac_tmp.p,
@@ -380,7 +313,6 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
     HIPCHK(launch_sort(c->key.as<unsigned long long>(), nullptr, n, range_ptr(c),
                        c->order.as<uint32_t>(), nullptr, nullptr, c->sort_tmp.p, nullptr,
                        c->stream));
-    CHK(check_sort(c, n, nullptr, "work-order sort"));
     HIPCHK(launch_gather_work(c->order.as<uint32_t>(), sx, sy, sz, n, c->wx.as<double>(),
                               c->wy.as<double>(), sz ? c->wz.as<double>() : nullptr,
                               c->worig.as<uint32_t>(), c->stream));
@@ -422,9 +354,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         worig = c->worig.as<uint32_t>();
     }
     IterState *dst = c->state_dev.as<IterState>();
-    const bool sel = use_select();
     FitIn fa{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
-             sel ? nullptr : c->order.as<uint32_t>(), worig, n, c->pivot_x, c->pivot_y, dst};
+             nullptr, worig, n, c->pivot_x, c->pivot_y, dst};
     // loop parameters and traces live on the device (k_loop.hip)
     LoopCtl lc{};
     lc.nstages = nstages;
@@ -469,8 +400,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // selection runs the half-step form below; it needs the fit + NN of an iteration to
     // outlast the host's wake-up and five launches (~20 us): from 64k rows (C2 100k:
     // equal to la = 2; C3: +1.5 % over whole-iteration lookahead).
-    static const int la_env = getenv("FICP_LOOKAHEAD") ? std::max(1, atoi(getenv("FICP_LOOKAHEAD"))) : 0;
-    const int la = std::min(kLoopRing - 1, la_env ? la_env : (n >= (1 << 16) ? 1 : 2));
+    const int la = n >= (1 << 16) ? 1 : 2;
     const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1);
     int64_t j = 0;
     bool finished = nstages <= 0;
@@ -478,7 +408,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // and stores the done flag straight into the pinned ring.  FICP_FUSE_FIT=1 also moves
     // the rigid fit into gather + final (no k_fit_sums pass): measured slower at C3
     // (gather +7 us, final +8.5 us vs the 12 us pass), so off by default.
-    const bool fused = sel && !tidx;
+    const bool fused = !tidx;
     // part A of iteration i: the fit and the NN call; part B: the selection (and, not
     // fused, the loop step and the flag copy)
     auto enq_a = [&](int64_t i) -> int {
@@ -487,21 +417,19 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, &dst->no_fit, c->stream));
         }
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
-                    !sel, tidx != nullptr || !sel));
+                    false, tidx != nullptr));
         return FICP_OK;
     };
     auto enq_b = [&](int64_t i) -> int {
         const int slot = (int)(i % kLoopRing);
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
-        if (sel) {
+        {
             ProfScope ps(c, P_SORT, "select");
             HIPCHK(launch_select(c->key.as<unsigned long long>(), worig, c->r.as<double>(), n, 0.0,
                                  &dst->lam_cur, range_ptr(c), nn_range_parts(n, c->m, use_grid(c, n)),
                                  c->sel_tmp.p, dst, &dst->done, fused ? &lc : nullptr,
                                  fused ? &c->h_flags[slot] : nullptr, c->stream,
                                  (fused && fuse_fit) ? &fsrc : nullptr));
-        } else {
-            CHK(sort_and_select(c, n, n, 0.0, worig, &dst->done, &dst->lam_cur));
         }
         if (!fused) {
             if (tidx)
@@ -527,8 +455,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         }
         return FICP_OK;
     };
-    static const bool half_env = !getenv("FICP_HALFSTEP") || atoi(getenv("FICP_HALFSTEP")) != 0;
-    if (fused && la == 1 && half_env) {
+    if (fused && la == 1) {
         // half-step lookahead: iteration i's selection, then i+1's fit and NN, then wait
         // for i's flag.  The device runs that fit + NN (>= 30 us) while the host wakes and
         // enqueues the next selection, and a finished run leaves two no-op launches
@@ -550,11 +477,11 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // state, the sort's timeout flag and the selection's statistics (each separate sync
     // cost ~40 us of idle device at C3)
     if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
-    if (sel) HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
+    HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
     c->h_rep->misc[1] = c->h_rep->misc[2] = c->h_rep->misc[3] = 0u;
     CHK(report_wait(c, ReportSeg{c->state_dev.p, &c->h_rep->st, (int)(sizeof(IterState) / 4)},
                     ReportSeg{tflag, &c->h_rep->misc[0], 1},
-                    sel ? ReportSeg{c->sel_stats.p, &c->h_rep->misc[1], 3} : ReportSeg{},
+                    ReportSeg{c->sel_stats.p, &c->h_rep->misc[1], 3},
                     &c->h_rep->t[1]));
     memcpy(c->h_state, &c->h_rep->st, sizeof(IterState));
     memcpy(c->h_misc, c->h_rep->misc, sizeof c->h_rep->misc);
@@ -591,11 +518,9 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     }
     if (c->h_misc[0])
         return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", c->h_misc[0]);
-    if (sel) {
-        c->sel_levels = c->h_misc[2];
-        c->sel_radix = c->h_misc[3];
-        if (c->h_misc[1]) return fail(FICP_EHIP, "fraction selection raised error flag %u", c->h_misc[1]);
-    }
+    c->sel_levels = c->h_misc[2];
+    c->sel_radix = c->h_misc[3];
+    if (c->h_misc[1]) return fail(FICP_EHIP, "fraction selection raised error flag %u", c->h_misc[1]);
     return FICP_OK;
 }
 
@@ -1090,7 +1015,7 @@ int ficp_select_fit_device(ficp_ctx *c, const double *x, const double *y, int64_
     HIPCHK(launch_corr_from_merge(d2, idx, tx, ty, n, c->key.as<unsigned long long>(),
                                   c->r.as<double>(), c->ccx.as<double>(), c->ccy.as<double>(),
                                   range_ptr(c), c->stream));
-    const bool sel = use_select() && n == n_source;
+    const bool sel = n == n_source;
     if (sel) {
         HIPCHK(launch_select(c->key.as<unsigned long long>(), nullptr, c->r.as<double>(), n,
                              lambda_val, nullptr, range_ptr(c), 0, c->sel_tmp.p,

@@ -563,12 +563,6 @@ hipError_t launch_batch_grid_count(const double *tx, const double *ty, int64_t m
 hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
                                 const TPt *pts, int64_t m, const int32_t *cell_start,
                                 const PlotState *st, int md, hipStream_t s);
-// stable argsort by (segment, key64, position): the distance sort of launch_sort followed
-// by a stable partition by seg[position] (two 8-bit passes, < 65536 segments).
-hipError_t launch_sort_seg(const unsigned long long *key64, const int32_t *seg, int64_t n,
-                           unsigned long long *range, uint32_t *order, const double *r,
-                           double *rs, void *tmp, hipStream_t s);
-int64_t sort_seg_tmp_bytes(int64_t n);
 hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
                              PlotState *st, hipStream_t s);
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,

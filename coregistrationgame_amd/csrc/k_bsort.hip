@@ -325,8 +325,9 @@ BSortPlan bsort_plan(int64_t n, int64_t nkeys) {
     int kb = 0;
     while (kb < 40 && (((int64_t)1) << kb) < nkeys) ++kb;
     // FICP_BS_BPTS / FICP_BS_SLICE: bucket and slice sizes (A/B runs)
-    static const int64_t bpts = getenv("FICP_BS_BPTS") ? atoll(getenv("FICP_BS_BPTS")) : 256;
-    static const int64_t slice = getenv("FICP_BS_SLICE") ? atoll(getenv("FICP_BS_SLICE")) : 4096;
+    // ~256 points per coarse bucket, slices of 4096 points (512-1024 and 8K-16K within 1 %)
+    constexpr int64_t bpts = 256;
+    constexpr int64_t slice = 4096;
     int want = 0;
     while (want < BMAXB_LOG && (bpts << want) < n) ++want;
     p.fs = std::max(0, kb - want);

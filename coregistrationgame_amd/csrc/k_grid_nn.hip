@@ -205,9 +205,6 @@ __device__ __forceinline__ void disk_scan_batched(const GridView &g, const Stems
             eval_slot<MD>(S, slot, qx, qy, qz, b);
         }
     }
-#ifdef FICP_NN_NOFAR  // timing experiment only: drop the rows at offset >= 2 (inexact)
-    return;
-#endif
     for (int k = 2;; ++k) {
         bool any = false;
 #pragma unroll
@@ -538,11 +535,6 @@ __device__ __forceinline__ void cover_scan(const GridView &g, const Stems &S, do
 #define FICP_CERT_PAD 0.25  // scans cover d_match + 0.25 cell sizes (0.1-0.4 within 1 % at C3)
 #endif
 
-#ifdef FICP_CERT_STATS
-__device__ unsigned long long g_cstat[4];
-__device__ unsigned g_cdone;
-#endif
-
 // rounding allowance of the certificate's distances (coordinates up to ~1e7 m: ulp ~2e-9 m)
 __device__ __forceinline__ double cert_eps(const GridView &g, double qx, double qy) {
     return 2.0 * g.margin + 1e-12 * (fabs(qx) + fabs(qy)) + 1e-9;
@@ -592,10 +584,7 @@ __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, con
     const double mx = qx - ox, my = qy - oy;
     mv = sqrt(mx * mx + my * my);
     const double G = a.gap[i] - mv - eps;
-#ifndef FICP_CERT_MUTANT
-#define FICP_CERT_MUTANT 0.0  // > 0 only in the mutation check of the tests (unsound)
-#endif
-    if (!(d2w < INFINITY && sqrt(d2w) + eps < G + FICP_CERT_MUTANT)) return false;
+    if (!(d2w < INFINITY && sqrt(d2w) + eps < G)) return false;
     a.gap[i] = G;
     if (a.idx) a.idx[i] = (int)load_zid(S.r, a.out_bp[i]).z;
     const double d = sqrt(d2w);
@@ -775,10 +764,6 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
     }
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
     Best b{INFINITY, 0x7fffffff, 0};
-#ifdef FICP_NN_IOONLY  // timing experiments only (inexact)
-    b.d2 = qx * 1e-9;
-    b.id = (int)i;
-#else
     if (a.warm_c) {
         // the previous match as a finite bound: its exact d2 to the moved query (the
         // operations of eval_slot), index unknown -- the scan meets it again and an
@@ -794,12 +779,7 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
         const int pb = a.prev_bp[i];
         if (pb >= 0) eval_slot<MD>(S, pb, qx, qy, qz, b);
     }
-#ifndef FICP_NN_WARMONLY
     grid_nn<MD>(g, S, qx, qy, qz, b);
-#else
-    if (!a.prev_bp) grid_nn<MD>(g, S, qx, qy, qz, b);
-#endif
-#endif
     finish(a, S, i, qz, b, kmin_c, kmax);
 }
 
@@ -809,35 +789,6 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     unsigned long long kmin_c = 0, kmax = 0;
     const double *T = (APPLY && (!a.apply_flag || *a.apply_flag)) ? a.T : nullptr;
-#ifdef FICP_CERT_STATS  // diagnostics only (tools/build_variant.sh certstats -DFICP_CERT_STATS)
-    bool certified = false;
-    if (i < a.n) {
-        if (a.gap) certified = nn_query_cert<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
-        else nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
-    }
-    {
-        const unsigned long long m = __ballot(certified), v = __ballot(i < a.n);
-        if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&g_cstat[0], (unsigned long long)__popcll(m));
-            atomicAdd(&g_cstat[1], (unsigned long long)__popcll(v));
-            atomicAdd(&g_cstat[2], (m == v && v) ? 1ULL : 0ULL);
-            atomicAdd(&g_cstat[3], 1ULL);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            const unsigned prev = atomicAdd(&g_cdone, 1u);
-            if (prev == gridDim.x - 1) {
-                __threadfence();
-                printf("CERT certified %llu / %llu lanes, %llu / %llu waves all certified\n",
-                       atomicAdd(&g_cstat[0], 0ULL), atomicAdd(&g_cstat[1], 0ULL),
-                       atomicAdd(&g_cstat[2], 0ULL), atomicAdd(&g_cstat[3], 0ULL));
-                for (int q = 0; q < 4; ++q) atomicExch(&g_cstat[q], 0ULL);
-                atomicExch(&g_cdone, 0u);
-            }
-        }
-    }
-#else
     if (a.cert_block && a.gap && a.warm_c) {
         // block-compacted: certificates first, then the workgroup's uncertified queries
         // packed densely onto its lanes (GS lanes per query when there are few of them)
@@ -887,7 +838,6 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
             nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
         }
     }
-#endif
     if (a.range) block_range_store(a.range, true, kmin_c, kmax);
 }
 

@@ -10,13 +10,11 @@
 //     reduced from per-workgroup parts of the NN kernel or of k_key_range), scatters
 //     (key32, position) into ORIG order -- so LSD stability alone orders exact ties by orig -- and builds the
 //     four digit histograms at once (they do not depend on the order).
-//  1-4. k_os_pass<P>: single-pass stable scatter per digit ("onesweep"): tiles take ids
-//     in dispatch order from an atomic ticket, rank their items with 64-lane ballot
-//     matching and per-wave LDS counters (no block barrier inside the ranking loop),
-//     publish their digit counts and find their global offsets by decoupled look-back
-//     over predecessor tiles (agent-scope relaxed atomics on 4-byte {flag|count} words:
-//     the data is the flag, MI355X_MICROARCH.md Valid forms / R2), then write digit runs
-//     coalesced from an LDS staging copy.  The last pass also emits r in selection order.
+//  1-3. per 8-bit digit, reduce-then-scan: k_rs_count (per-tile digit counts),
+//     k_rs_rowscan (exclusive offsets per digit over the tiles), k_os_pass (stable scatter:
+//     items ranked with 64-lane ballot matching and per-wave LDS counters, digit runs
+//     written coalesced from an LDS staging copy).  No communication between the
+//     workgroups of a launch.  The last pass also emits r in selection order.
 //  5. k_os_fixup: runs of equal key32 (distinct distances closer than 2^s ulps: rare)
 //     are re-ordered by key64 with a stable insertion sort.
 #include "ficp_internal.h"
@@ -33,10 +31,6 @@ namespace {
 constexpr int OB = 256;              // threads per pass block (4 waves)
 constexpr int OIPT = 8;              // items per thread
 constexpr int OTILE = OB * OIPT;     // 2048 items per tile
-constexpr uint32_t F_AGG = 1u << 30;
-constexpr uint32_t F_PRE = 2u << 30;
-constexpr uint32_t F_MASK = 3u << 30;
-constexpr uint32_t C_MASK = F_AGG - 1;
 constexpr int SCAN_I = 16;
 constexpr int SCAN_TILE = 256 * SCAN_I;
 
@@ -183,10 +177,8 @@ __global__ __launch_bounds__(256) void k_os_hist(const unsigned long long *key64
     }
 }
 
-// LB = true: onesweep (tile ids from tickets, offsets by decoupled look-back).
-// LB = false: reduce-then-scan (tile = blockIdx.x, offsets from excl_tab[digit][tile]
-// built by k_rs_count + k_rs_rowscan; no communication between workgroups of a launch).
-template <int PASS, bool LB, bool PIN = false>
+// tile = blockIdx.x; global offsets from excl_tab[digit][tile] (k_rs_count + k_rs_rowscan)
+template <int PASS, bool PIN = false>
 __global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint32_t *vin,
                                                 uint32_t *kout, uint32_t *vout, int64_t n,
                                                 SortWS ws, const uint32_t *excl_tab,
@@ -201,7 +193,7 @@ __global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint3
     __shared__ uint32_t s_w[4];
     __shared__ int s_tile;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_tile = LB ? (int)atomicAdd(&ws.tickets[PASS], 1u) : (int)blockIdx.x;
+    if (tid == 0) s_tile = (int)blockIdx.x;
 #pragma unroll
     for (int w = 0; w < 4; ++w) s_cnt[w][tid] = 0;
     // digit base = exclusive scan of this pass's global histogram (built by atomics:
@@ -255,40 +247,7 @@ __global__ __launch_bounds__(OB) void k_os_pass(const uint32_t *kin, const uint3
     // ---- per digit (thread = digit): wave offsets, tile count, look-back
     const uint32_t c0 = s_cnt[0][tid], c1 = s_cnt[1][tid], c2 = s_cnt[2][tid], c3 = s_cnt[3][tid];
     const uint32_t mine = c0 + c1 + c2 + c3;
-    uint32_t excl = 0;
-    if (!LB) {
-        excl = excl_tab[(int64_t)tid * ws.ntiles + t];
-    } else {
-    uint32_t *st = ws.status + ((int64_t)PASS * ws.ntiles + t) * 256 + tid;
-    // Status words are published and polled with device-scope atomic RMWs: atomics are
-    // performed at the memory side, so a poll can never be served by a stale copy of the
-    // line in this XCD's L2 (plain/sc1 loads can: the per-XCD L2s are not coherent).
-    if (t == 0) {
-        __hip_atomic_exchange(st, F_PRE | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        __hip_atomic_exchange(st, F_AGG | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t *prev = st - 256;
-        unsigned spins = 0;
-        for (int j = t - 1; j >= 0; --j, prev -= 256) {
-            uint32_t w;
-            for (;;) {
-                w = __hip_atomic_fetch_or(prev, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (w & F_MASK) break;
-                if (++spins > (1u << 20)) {  // bounded: never hang the device
-                    __hip_atomic_exchange(&ws.tickets[4], 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-                    w = F_PRE;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            excl += w & C_MASK;
-            if (w & F_PRE) break;
-        }
-        __hip_atomic_exchange(st, F_PRE | (excl + mine), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-    }
-    }  // LB
+    const uint32_t excl = excl_tab[(int64_t)tid * ws.ntiles + t];
     s_gb[tid] = dbase + excl;
     s_cnt[0][tid] = 0;
     s_cnt[1][tid] = c0;
@@ -367,34 +326,6 @@ __global__ __launch_bounds__(256) void k_rs_rowscan(uint32_t *counts, int ntiles
     }
 }
 
-// segmented sort: key32[j] = seg[order[j]] for the stable partition passes
-__global__ __launch_bounds__(256) void k_seg_keys(const int32_t *seg, const uint32_t *order,
-                                                  int64_t n, uint32_t *k32) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    k32[j] = (uint32_t)seg[order[j]];
-}
-
-// histograms of digits 0 and 1 of key32 -> hist[0..255], hist[256..511] (atomics)
-__global__ __launch_bounds__(256) void k_hist2(const uint32_t *k32, int64_t n, uint32_t *hist) {
-    __shared__ uint32_t s_h[2][256];
-    s_h[0][threadIdx.x] = 0;
-    s_h[1][threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t nround = (n + 255) / 256;
-    for (int64_t q = blockIdx.x; q < nround; q += gridDim.x) {
-        const int64_t j = q * 256 + threadIdx.x;
-        const bool valid = j < n;
-        const uint32_t k = valid ? k32[j] : 0u;
-        wave_hist_add(s_h[0], k & 255u, valid);
-        wave_hist_add(s_h[1], (k >> 8) & 255u, valid);
-    }
-    __syncthreads();
-    for (int e = 0; e < 2; ++e) {
-        const uint32_t c = s_h[e][threadIdx.x];
-        if (c) atomicAdd(&hist[e * 256 + threadIdx.x], c);
-    }
-}
 
 // Runs of equal key32 hold distinct distances closer than 2^s ulps: order them by the
 // full key (stable: equal key64 keep their orig order).
@@ -594,40 +525,23 @@ hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, in
                        unsigned long long *range, uint32_t *order, const double *r, double *rs,
                        void *tmp, const int *skip, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    static const int dbg = getenv("FICP_SORT_SYNC") ? atoi(getenv("FICP_SORT_SYNC")) : 0;
-    // FICP_SORT=onesweep selects the single-launch-per-digit look-back passes (DESIGN.md
-    // §4.2); the default reduce-then-scan passes need no inter-workgroup communication
-    static const bool onesweep = getenv("FICP_SORT") && !strcmp(getenv("FICP_SORT"), "onesweep");
-    auto step = [&]() {
-        if (dbg) (void)hipStreamSynchronize(s);
-    };
     SortWS w = carve(tmp, n);
     hipLaunchKernelGGL(k_atomic_zero32, dim3(NPASS), dim3(256), 0, s, w.hist,
                        (int64_t)(NPASS * 256));
-    step();
-    const int64_t status_words = onesweep ? (int64_t)NPASS * w.ntiles * 256 : 0;
+    const int64_t status_words = 0;
     const int hb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 2047) / 2048));
     hipLaunchKernelGGL(k_os_hist, dim3(hb), dim3(256), 0, s, key64, orig, n,
                        (const unsigned long long *)range, w, status_words, skip);
-    step();
     // pairs -> (kA, order) -> (kB, vB) -> (kA, order); the last pass also gathers rs
     static_assert(NPASS == 3, "pass chain below is written for three 8-bit digits");
     const dim3 g(w.ntiles), b(OB);
     const uint32_t *nul = nullptr;
-#define FICP_PASS(P, PIN, KIN, VIN, KOUT, VOUT, R, RS)                                          \
-    if (onesweep) {                                                                           \
-        hipLaunchKernelGGL((k_os_pass<P, true, PIN>), g, b, 0, s, KIN, VIN, KOUT, VOUT, n, w,   \
-                           nul, R, RS, skip);                                                 \
-    } else {                                                                                  \
-        hipLaunchKernelGGL((k_rs_count<P, PIN>), g, b, 0, s, KIN, (const uint2 *)w.pairs, n,   \
-                           w.counts, w.ntiles, skip);                                         \
-        step();                                                                               \
-        hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles, skip); \
-        step();                                                                               \
-        hipLaunchKernelGGL((k_os_pass<P, false, PIN>), g, b, 0, s, KIN, VIN, KOUT, VOUT, n, w,  \
-                           (const uint32_t *)w.counts, R, RS, skip);                          \
-    }                                                                                         \
-    step();
+#define FICP_PASS(P, PIN, KIN, VIN, KOUT, VOUT, R, RS)                                        \
+    hipLaunchKernelGGL((k_rs_count<P, PIN>), g, b, 0, s, KIN, (const uint2 *)w.pairs, n,       \
+                       w.counts, w.ntiles, skip);                                             \
+    hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles, skip);     \
+    hipLaunchKernelGGL((k_os_pass<P, PIN>), g, b, 0, s, KIN, VIN, KOUT, VOUT, n, w,             \
+                       (const uint32_t *)w.counts, R, RS, skip);
     const double *rnul = nullptr;
     double *rsnul = nullptr;
     FICP_PASS(0, true, nul, nul, w.kA, order, rnul, rsnul)
@@ -636,7 +550,6 @@ hipError_t launch_sort(const unsigned long long *key64, const uint32_t *orig, in
 #undef FICP_PASS
     hipLaunchKernelGGL(k_os_fixup, dim3(nblk(n)), dim3(256), 0, s, w.kA, order, key64, r, rs, n,
                        skip);
-    step();
     return hipGetLastError();
 }
 
@@ -644,42 +557,6 @@ hipError_t launch_keys_from_doubles(const double *d, int64_t n, unsigned long lo
                                     uint32_t *val, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_keys_from_doubles, dim3(nblk(n)), dim3(256), 0, s, d, n, key, val);
-    return hipGetLastError();
-}
-
-}  // namespace ficp
-
-namespace ficp {
-
-int64_t sort_seg_tmp_bytes(int64_t n) { return sort_tmp_bytes(n); }
-
-hipError_t launch_sort_seg(const unsigned long long *key64, const int32_t *seg, int64_t n,
-                           unsigned long long *range, uint32_t *order, const double *r,
-                           double *rs, void *tmp, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    // 1. distance order, exact ties by position (caller order)
-    hipError_t e = launch_sort(key64, nullptr, n, range, order, nullptr, nullptr, tmp, nullptr, s);
-    if (e != hipSuccess) return e;
-    // 2. stable partition by segment: LSD passes on the 16-bit segment id
-    SortWS w = carve(tmp, n);
-    hipLaunchKernelGGL(k_seg_keys, dim3(nblk(n)), dim3(256), 0, s, seg, order, n, w.kA);
-    hipLaunchKernelGGL(k_atomic_zero32, dim3(2), dim3(256), 0, s, w.hist, (int64_t)512);
-    const int hb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n + 2047) / 2048));
-    hipLaunchKernelGGL(k_hist2, dim3(hb), dim3(256), 0, s, w.kA, n, w.hist);
-    const dim3 g(w.ntiles), b(OB);
-    hipLaunchKernelGGL(k_rs_count<0>, g, b, 0, s, w.kA, (const uint2 *)nullptr, n, w.counts,
-                       w.ntiles, (const int *)nullptr);
-    hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles,
-                       (const int *)nullptr);
-    hipLaunchKernelGGL((k_os_pass<0, false>), g, b, 0, s, w.kA, order, w.kB, w.vB, n, w,
-                       (const uint32_t *)w.counts, (const double *)nullptr, (double *)nullptr,
-                       (const int *)nullptr);
-    hipLaunchKernelGGL(k_rs_count<1>, g, b, 0, s, w.kB, (const uint2 *)nullptr, n, w.counts,
-                       w.ntiles, (const int *)nullptr);
-    hipLaunchKernelGGL(k_rs_rowscan, dim3(256), dim3(256), 0, s, w.counts, w.ntiles,
-                       (const int *)nullptr);
-    hipLaunchKernelGGL((k_os_pass<1, false>), g, b, 0, s, w.kB, w.vB, w.kA, order, n, w,
-                       (const uint32_t *)w.counts, r, rs, (const int *)nullptr);
     return hipGetLastError();
 }
 

@@ -299,13 +299,23 @@ def test_run_vs_oracle_100k(oracle):
     np.testing.assert_array_equal(bits(final[:, 2]), bits(p.source[:, 2]))
 
 
-@pytest.mark.parametrize("fuse_fit,md", [("0", 3), ("1", 3), ("0", 2)])
-def test_run_untraced_vs_oracle_100k(oracle, fuse_fit, md, monkeypatch):
+# every environment switch of libficp.so that changes which kernels run (the only ones
+# left): the fused fit, and the two fallback paths the bucket sort takes for
+# layers it cannot plan (global-atomic grid build, 64-bit radix work order), forced here
+KNOBS = [{}, {"FICP_FUSE_FIT": "1"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
+         {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "1"}]
+
+
+@pytest.mark.parametrize("knobs,md", [(k, 3) for k in KNOBS] + [({}, 2), ({"FICP_GRID_ATOMIC": "1"}, 2)],
+                         ids=lambda v: ",".join(f"{a}={b}" for a, b in v.items()) or "default"
+                         if isinstance(v, dict) else f"md{v}")
+def test_run_untraced_vs_oracle_100k(oracle, knobs, md, monkeypatch):
     """The production loop (no traces: the selection's last kernel runs the loop step; with
     FICP_FUSE_FIT=1 it also runs the rigid fit; half-step lookahead, certified NN reuse)
-    against the pinned oracle at 100k, 3-D and 2-D matching."""
+    against the pinned oracle at 100k, 3-D and 2-D matching, under every kernel switch."""
     from coregistrationgame_amd import FractionalICP, synth
-    monkeypatch.setenv("FICP_FUSE_FIT", fuse_fit)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
     p = synth.make_plot(100_000, 100_000, 0.8, seed=100_000, md=md)
     icp = FractionalICP(p.source, p.target)
     final = icp.run()

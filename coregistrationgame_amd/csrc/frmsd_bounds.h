@@ -24,16 +24,17 @@ __device__ __forceinline__ double lo_r(unsigned long long klo) {
     return d * d * (1.0 - 1e-15);
 }
 
-// lg2 is exact in the exponent and ~1e-7 in the mantissa (v_log_f32); kMarg (log2
-// units) covers that and the rounding of the bucket sums the bounds are built from.
-constexpr double kMarg = 1e-5;
+// lg2 is the fp64 log2 (ocml, ~1 ulp).  kMarg (log2 units) covers its rounding, the
+// rounding of p log2 k and that of the fp64 prefix sums of the bucket sums the bounds are
+// built from (relative ~1e-12 at 2^13 buckets or 16k rows): 1e-9 leaves a factor ~100.
+// (The float log of round 1 forced 1e-5, which kept every position within ~3.5e-6 of the
+// minimum FRMSD a candidate: 700-2200 rows at C3 whatever the bucket width.)
+constexpr double kMarg = 1e-9;
 
 __device__ __forceinline__ double lg2(double x) {
     if (!(x > 0.0)) return x == 0.0 ? -INFINITY : NAN;
     if (!(x < INFINITY)) return INFINITY;
-    int e;
-    const double m = frexp(x, &e);  // [0.5, 1)
-    return (double)e + (double)__builtin_amdgcn_logf((float)m);
+    return log2(x);
 }
 
 __device__ __forceinline__ double h_of(long long k, double S, double p) {

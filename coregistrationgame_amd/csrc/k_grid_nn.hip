@@ -1307,7 +1307,16 @@ hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_
                           bool reduce_range, hipEvent_t e0, hipEvent_t e1) {
     if (a.n == 0) return hipSuccess;
     dim3 grid(nblk(a.n)), blk(256);
-    if (md == 3) {
+    if (!e0) {
+        // plain dispatch without events
+        if (md == 3) {
+            if (a.T) hipLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, a, g);
+            else hipLaunchKernelGGL((k_nn_grid<3, false>), grid, blk, 0, s, a, g);
+        } else {
+            if (a.T) hipLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, a, g);
+            else hipLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, a, g);
+        }
+    } else if (md == 3) {
         if (a.T) hipExtLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, e0, e1, 0, a, g);
         else hipExtLaunchKernelGGL((k_nn_grid<3, false>), grid, blk, 0, s, e0, e1, 0, a, g);
     } else {

@@ -30,7 +30,7 @@
 //                     rows that drop below, so still deterministic); (c) if that stalls
 //                     (clustered or equal keys), an in-workgroup LSD radix sort.
 // Level-0 bucket sums are bracketed exactly (truncated fixed point: [fx, fx + c) units);
-// the bounds are compared in the log2 domain with a 1e-5 margin (see h_of).  The decided
+// the bounds are compared in the log2 domain with a 1e-9 margin (see kMarg).  The decided
 // k and threshold pair depend only on the exact, deterministic prefix sums.
 // At C3 (1M x 1M) the candidate set holds 15-5000 rows, so step (a) is the normal case.
 #include "ficp_internal.h"

@@ -151,6 +151,10 @@ struct alignas(16) IterState {
     // stable (key, orig) order; the fit selects {i : (key_i, orig_i) <= (tkey, torig)}
     unsigned long long tkey;
     long long torig;
+    // |tkey - previous tkey| when both came from loop-body calls of one stage (else 0):
+    // sizes the next call's fine bucket window (k_select.hip make_bmap)
+    unsigned long long tmove;
+    unsigned long long pad2;
 };
 
 // FRMSD(k) = (1 / (k/N)**lambda) * sqrt(S_k / k), in the reference's operation order

@@ -90,9 +90,18 @@ constexpr int GI = FICP_GI;  // gather: rows per thread (~1 block per CU at 1M r
 // error bits of SelCtl::err (sticky; the host checks them after a run)
 constexpr unsigned ERR_EMPTY = 1u;  // candidate set empty (cannot happen with finite r)
 
+constexpr int NL = 2048, NF = 4096, NF_LOG = 12, NC_LOG = 11;
+static_assert(NL + NF + NL == NB, "bucket map regions");
+struct BMap {
+    u64 kmin, kmax, wlo, whi;  // fine window [wlo, whi) (win)
+    int s;                     // uniform shift (!win)
+    int sl, sf, sh;            // shifts of the low / fine / high regions (win)
+    int win, pad;
+};
+
 struct SelCtl {
-    u64 kmin;
-    int s, b0, b1, pad0;
+    BMap map;              // level-0 bucket map of this call (k_sel_hist, block 0)
+    int b0, b1;
     long long kbase;       // rows in buckets < b0
     double U;              // upper bound of h (log2 domain) at the minimum
     unsigned ccount;       // candidates appended (agent-scope atomics only)
@@ -202,10 +211,91 @@ __device__ __forceinline__ int sel_shift(u64 kmin, u64 kmax) {
     return b > NB_LOG ? b - NB_LOG : 0;
 }
 
+// Bucket map of the level-0 histogram.  Uniform (a stage's first call): NB buckets of
+// 2^s keys from kmin.  Windowed (the stage's later calls): the previous call's threshold
+// key c gets NF fine buckets of 2^sf keys around it (half-width >= 64 uniform buckets and
+// >= 4x the threshold's last move), the keys below and above the window NL coarse buckets
+// each.  The threshold moves little from call to call (C3: < 1 uniform bucket after the
+// third call), so the new candidate buckets fall in the fine part and hold ~1/32 of the
+// rows.  Any monotone map keeps the bounds rigorous: each bucket's key range gives the
+// lower r (lo_r of bucket_lo) and the fixed-point exponent (bucket_hi) of its rows.
+
+// what the map needs from the previous call (loaded early by k_sel_hist)
+struct BPrev {
+    u64 tkey, tmove;
+    int ok;
+};
+__device__ __forceinline__ BPrev bprev_of(const IterState *st) {
+    BPrev v{0ULL, 0ULL, 0};
+    if (st) {
+        v.ok = st->phase == PH_LOOP && st->k > 0;
+        v.tkey = st->tkey;
+        v.tmove = st->tmove;
+    }
+    return v;
+}
+
+__device__ __forceinline__ BMap make_bmap(u64 kmin, u64 kmax, const BPrev &pv) {
+    BMap m{};
+    m.kmin = kmin;
+    m.kmax = kmax;
+    m.s = sel_shift(kmin, kmax);
+    if (!pv.ok || m.s < 8) return m;
+    const u64 c = pv.tkey;
+    if (c < kmin || c > kmax) return m;
+    const u64 mv = pv.tmove;
+    u64 H = (u64)64 << m.s;
+    if (mv < ((u64)1 << 60) && 4 * mv > H) H = 4 * mv;
+    const int sf = max(0, bits_of(2 * H - 1) - NF_LOG);  // NF << sf >= 2 H
+    if (sf > m.s - 3) return m;                          // not >= 8x finer: uniform
+    const u64 W = (u64)NF << sf;
+    u64 wlo = c - min(c - kmin, W / 2);
+    if (kmax - wlo < W - 1) {
+        if (kmax - kmin < W - 1) return m;
+        wlo = kmax - (W - 1);
+    }
+    m.wlo = wlo;
+    m.whi = wlo + W;
+    m.sf = sf;
+    m.sl = wlo > kmin ? max(0, bits_of(wlo - 1 - kmin) - NC_LOG) : 0;
+    m.sh = m.whi <= kmax ? max(0, bits_of(kmax - m.whi) - NC_LOG) : 0;
+    m.win = 1;
+    return m;
+}
+
+__device__ __forceinline__ int bucket_of(const BMap &m, u64 k) {
+    if (!m.win) return (int)((k - m.kmin) >> m.s);
+    if (k < m.wlo) return (int)((k - m.kmin) >> m.sl);
+    if (k < m.whi) return NL + (int)((k - m.wlo) >> m.sf);
+    return NL + NF + (int)((k - m.whi) >> m.sh);
+}
+
+// lowest key of bucket b
+__device__ __forceinline__ u64 bucket_lo(const BMap &m, int b) {
+    if (!m.win) return m.kmin + ((u64)b << m.s);
+    if (b < NL) return m.kmin + ((u64)b << m.sl);
+    if (b < NL + NF) return m.wlo + ((u64)(b - NL) << m.sf);
+    return m.whi + ((u64)(b - NL - NF) << m.sh);
+}
+
+// highest key of sub-bucket j (width 2^sh) from base, clipped to lim; (j + 1) << sh wraps
+// to 0 only at 2^64 (j < 8192, sh <= 51), and then the clip applies
+__device__ __forceinline__ u64 span_hi(u64 base, u64 lim, int j, int sh) {
+    const u64 wdt = ((u64)(j + 1) << sh) - 1ULL;
+    return wdt > lim - base ? lim : base + wdt;
+}
+
+// highest key any row of bucket b can have
+__device__ __forceinline__ u64 bucket_hi(const BMap &m, int b) {
+    if (!m.win) return span_hi(m.kmin, m.kmax, b, m.s);
+    if (b < NL) return span_hi(m.kmin, m.wlo - 1, b, m.sl);
+    if (b < NL + NF) return span_hi(m.wlo, min(m.whi - 1, m.kmax), b - NL, m.sf);
+    return span_hi(m.whi, m.kmax, b - NL - NF, m.sh);
+}
+
 // exponent e_b with r < 2^e_b for every row of bucket b (1024: the bucket holds inf/NaN)
-__device__ __forceinline__ int bucket_exp(u64 kmin, u64 kmax, int s, int b) {
-    const u64 wdt = ((u64)(b + 1) << s) - 1ULL;  // wraps to ~0 for the top bucket at s = 51
-    const u64 khi = wdt > kmax - kmin ? kmax : kmin + wdt;
+__device__ __forceinline__ int bucket_exp(const BMap &m, int b) {
+    const u64 khi = bucket_hi(m, b);
     if (!(khi >> 63)) return 0;
     // from the bits of d_hi alone (no fp64 work): d < 2^(ex - 1022) for biased exponent ex,
     // so r = d^2 < 2^(2 ex - 2044); at most one bit looser than the exponent of d_hi^2
@@ -487,10 +577,30 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, Scr &s) {
 // block_range_store) and block 0 stores range[0..1] for the kernels that follow.
 __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *r, int64_t n,
                                                  u64 *range, int64_t nparts, SelWS w,
-                                                 const int *skip, HistPack hp) {
+                                                 const int *skip, HistPack hp,
+                                                 const IterState *st) {
     if (skip && *skip) return;
     __shared__ u64 sp[NB];
     __shared__ u64 s_u[HHT / 64], s_v[HHT / 64];
+#ifndef FICP_HIST_U
+#define FICP_HIST_U 4
+#endif
+    constexpr int U = FICP_HIST_U;  // rows in flight per thread (8 measured -1 %)
+    // this thread's first U rows and the previous call's threshold are loaded before the
+    // range reduction, so their latency overlaps it
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * per, i1 = min(n, i0 + per);
+    const int64_t ib = i0 + threadIdx.x;
+    u64 kk[U];
+    double rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t q = ib + (int64_t)u * HHT;
+        kk[u] = q < i1 ? key[q] : 0ULL;
+        rv[u] = q < i1 ? r[q] : 0.0;
+    }
+    const BPrev pv = bprev_of(st);
+    for (int b = threadIdx.x; b < NB; b += HHT) sp[b] = 0ULL;
     u64 kmin, kmax;
     if (nparts > 0) {
         u64 a = 0, b = 0;
@@ -510,7 +620,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
             }
         }
         a = ~a;
-        blk_minmax_u64<HHT / 64>(a, b, s_u, s_v);
+        blk_minmax_u64<HHT / 64>(a, b, s_u, s_v);  // (its barriers also cover the LDS zeroing)
         kmin = a;
         kmax = b;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -520,33 +630,28 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
     } else {
         kmin = ~range[0];
         kmax = range[1];
+        __syncthreads();
     }
-    const int s = sel_shift(kmin, kmax);
-    for (int b = threadIdx.x; b < NB; b += HHT) sp[b] = 0ULL;
+    // every block derives the same map; block 0 publishes it for the later kernels
+    const BMap bm = make_bmap(kmin, kmax, pv);
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.ctl->map = bm;
     const u64 one = 1ULL << hp.shift;
-    __syncthreads();
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t i0 = (int64_t)blockIdx.x * per, i1 = min(n, i0 + per);
-#ifndef FICP_HIST_U
-#define FICP_HIST_U 4
-#endif
-    constexpr int U = FICP_HIST_U;  // rows in flight per thread (8 measured -1 %)
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * HHT) {
-        u64 kk[U];
-        double rv[U];
+    for (int64_t i = ib; i < i1; i += (int64_t)U * HHT) {
+        if (i != ib) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t q = i + (int64_t)u * HHT;
-            kk[u] = q < i1 ? key[q] : 0ULL;
-            rv[u] = q < i1 ? r[q] : 0.0;
+            for (int u = 0; u < U; ++u) {
+                const int64_t q = i + (int64_t)u * HHT;
+                kk[u] = q < i1 ? key[q] : 0ULL;
+                rv[u] = q < i1 ? r[q] : 0.0;
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (i + (int64_t)u * HHT < i1) {
-                const int b = (int)((kk[u] - kmin) >> s);
+                const int b = bucket_of(bm, kk[u]);
                 // r < 2^e for every row of the bucket, from the bucket's upper key bits
                 // (a per-bucket LDS table cost its init and 16 KB: +1 % without it)
-                const int e = bucket_exp(kmin, kmax, s, b);
+                const int e = bucket_exp(bm, b);
                 const u64 m = (e < 1024 && rv[u] < INFINITY) ? (u64)ldexp(rv[u], hp.fixb - e) : 0ULL;
                 atomicAdd(&sp[b], one + m);
             }
@@ -567,7 +672,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
 constexpr int RG = FICP_SEL_RG;
 constexpr int RBPB = 1024 / RG;  // buckets per workgroup
 __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int *skip,
-                                                     HistPack hp, const u64 *range) {
+                                                     HistPack hp) {
     if (skip && *skip) return;
     __shared__ unsigned s_c[RG][RBPB];
     __shared__ u64 s_f[RG][RBPB];
@@ -605,8 +710,7 @@ __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int
     // the bucket's sum bracketed by the truncated fixed-point sum (each row loses < 1
     // unit): f * 2^(e - fixb) <= sum < (f + c) * 2^(e - fixb); computed here, one bucket
     // per thread, instead of 16 per thread in the one-workgroup bounds kernel
-    const u64 kmin = ~range[0], kmax = range[1];
-    const int e = bucket_exp(kmin, kmax, sel_shift(kmin, kmax), b);
+    const int e = bucket_exp(w.ctl->map, b);
     double lo, hi;
     if (e >= 1024) {
         lo = hi = c ? INFINITY : 0.0;
@@ -642,8 +746,8 @@ __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int
 // its own thread serialised ~16 dependent evaluations: ~10 us at C3).
 constexpr int MAXACT = HT / (NB / HT);  // active chunks evaluated one bucket per lane
 __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double lam,
-                                                   const double *lam_dev, const u64 *range,
-                                                   const int *skip, int fixb) {
+                                                   const double *lam_dev, const int *skip,
+                                                   int fixb) {
     if (skip && *skip) return;
     if (lam_dev) lam = *lam_dev;
     constexpr int PER = NB / HT;
@@ -654,8 +758,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     __shared__ double eLo[MAXACT * PER];    // lower sum before it
     __shared__ double eHi[MAXACT * PER];    // upper sum through it
     const int t = threadIdx.x;
-    const u64 kmin = ~range[0], kmax = range[1];
-    const int s = sel_shift(kmin, kmax);
+    const BMap bm = w.ctl->map;
     SELPROF(8);
     if (t == 0) s_nact = 0;
     static_assert(PER == 16, "chunk totals of k_sel_reduce");
@@ -680,7 +783,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     SELPROF(11);
     // (the extra 1e-9 covers the fixed-point truncation of the per-bucket lower sums, so
     // that a chunk's bound never exceeds the bound of a bucket inside it)
-    const bool active = ct && (!(block_lb(Cex, ct, Plo, lo_r(kmin + ((u64)(t * PER) << s)), p) -
+    const bool active = ct && (!(block_lb(Cex, ct, Plo, lo_r(bucket_lo(bm, t * PER)), p) -
                                        1e-9 > U1) ||
                                !(p >= 1.0));
     unsigned cc[PER];
@@ -739,7 +842,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
             const int b = s_act[q / PER] * PER + (q % PER);
             const unsigned c = w.hcnt[b];
             if (c) {
-                const double lb = block_lb(eC[q], c, eLo[q], lo_r(kmin + ((u64)b << s)), p);
+                const double lb = block_lb(eC[q], c, eLo[q], lo_r(bucket_lo(bm, b)), p);
                 if (!(lb > U) || !(p >= 1.0)) {
                     if (b < bmin) kb = eC[q];  // rows before this lane's first candidate
                     bmin = min(bmin, (long long)b);
@@ -769,7 +872,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
             for (int j = 0; j < PER; ++j) {
                 const int b = t * PER + j;
                 if (cc[j]) {
-                    const double lb = block_lb(C, cc[j], P, lo_r(kmin + ((u64)b << s)), p);
+                    const double lb = block_lb(C, cc[j], P, lo_r(bucket_lo(bm, b)), p);
                     if (!(lb > U) || !(p >= 1.0)) {
                         if (bmax < 0) kb = C;  // rows before this thread's first candidate
                         bmin = min(bmin, (long long)b);
@@ -797,8 +900,6 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
         w.ctl->kbase = kb;  // rows in buckets < b0
     }
     if (t == 0) {
-        w.ctl->kmin = kmin;
-        w.ctl->s = s;
         w.ctl->b0 = (int)bmin;
         w.ctl->b1 = (int)bmax;
         w.ctl->U = U;
@@ -813,8 +914,8 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
     if (skip && *skip) return;
     __shared__ double s_w[GT / 64];
     __shared__ double s_f[8 * (GT / 64)];
-    const u64 kmin = w.ctl->kmin;
-    const int s = w.ctl->s, b0 = w.ctl->b0, b1 = w.ctl->b1;
+    const BMap bm = w.ctl->map;
+    const int b0 = w.ctl->b0, b1 = w.ctl->b1;
     const int lane = threadIdx.x & 63;
     const int64_t base = (int64_t)blockIdx.x * (GT * GI) + threadIdx.x;
     // all loads first (no load waits behind the append's atomic)
@@ -836,7 +937,7 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
         const int64_t i = base + (int64_t)q * GT;
         bool in = false;
         if (i < n) {
-            const int b = (int)((kk[q] - kmin) >> s);
+            const int b = bucket_of(bm, kk[q]);
             if (b < b0) {
                 acc = acc + rr[q];
                 bel |= 1u << q;
@@ -972,6 +1073,9 @@ __device__ __forceinline__ bool less_ko(u64 ka, uint32_t oa, u64 kb, uint32_t ob
 // write the decision to the iteration state (thread 0)
 __device__ __forceinline__ void publish(IterState *st, const FinalIn &in, double bf, long long bk,
                                         u64 tkey, uint32_t torig) {
+    // the threshold's move since the previous loop-body call of this stage (make_bmap)
+    const bool prev = st->phase == PH_LOOP && st->k > 0 && bk != 0x7fffffffffffffffLL;
+    st->tmove = prev ? (tkey > st->tkey ? tkey - st->tkey : st->tkey - tkey) : 0ULL;
     if (bk == 0x7fffffffffffffffLL) {  // every FRMSD was NaN: the reference keeps (0.0, 0)
         st->k = 0;
         st->frac = 0.0;
@@ -1165,6 +1269,65 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
         blk_sum8_add(cf, in.fsum, scr);
     }
     if (threadIdx.x == 0) publish(st, in, r.bf, r.bk, r.tk, r.to);
+}
+
+// (a0) c <= SMALL_C candidates (the windowed map's normal case: ~20-100 at C3): one candidate
+// per thread, ranked by (key, orig) against all c in LDS (broadcast reads, no bins), one
+// block scan of r in sorted order, FRMSD of every position, first minimum.  Fewer
+// barriers than the binned sort of lds_sort_scan, whose fixed phases dominated at this c.
+constexpr int SMALL_C = 160;  // above it the binned sort ranks faster (390: 5.8 vs 3.4 us)
+__device__ void final_small(const Cand &src, unsigned c, const FinalIn &in, unsigned char *sm,
+                            Scr &scr, IterState *st) {
+    u64 *lk = (u64 *)sm;
+    double *lr = (double *)(sm + HT * 8);
+    uint32_t *lo = (uint32_t *)(sm + HT * 16);
+    uint16_t *pos = (uint16_t *)(sm + HT * 20);
+    const unsigned t = threadIdx.x;
+    u64 k = 0;
+    uint32_t o = 0;
+    if (t < c) {
+        k = src.k[t];
+        o = src.o[t];
+        lk[t] = k;
+        lo[t] = o;
+        lr[t] = src.r[t];
+    }
+    __syncthreads();
+    if (t < c) {
+        unsigned rank = 0;
+        for (unsigned j = 0; j < c; ++j) rank += less_ko(lk[j], lo[j], k, o) ? 1u : 0u;
+        pos[rank] = (uint16_t)t;
+    }
+    __syncthreads();
+    const double v = t < c ? lr[pos[t]] : 0.0;
+    double all;
+    const double ex = blk_excl_scan_d(v, scr, all);
+    double bf = INFINITY;
+    long long bk = 0x7fffffffffffffffLL;
+    if (t < c) {
+        const long long kk = in.K0 + (long long)t + 1;
+        const double f = frmsd_of(kk, in.N, in.S0 + (ex + v), in.lam);
+        if (f < bf) {
+            bf = f;
+            bk = kk;
+        }
+    }
+    blk_argmin(bf, bk, scr);
+    if (in.fs.on && bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
+        double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if ((long long)t < bk - in.K0) fit_row(cf, in.fs, src.p[pos[t]]);
+        blk_sum8_add(cf, in.fsum, scr);
+    }
+    if (t == 0) {
+        u64 tk = 0;
+        uint32_t to = 0;
+        if (bk != 0x7fffffffffffffffLL) {
+            const unsigned e = pos[(unsigned)(bk - in.K0 - 1)];
+            tk = lk[e];
+            to = lo[e];
+        }
+        publish(st, in, bf, bk, tk, to);
+    }
 }
 
 // (a') more than CAP2 candidates that refinement could not narrow (flat FRMSD curves at
@@ -1603,6 +1766,12 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     // 16-B loads here and as many stores at the end: ~1 us each way)
     static_assert(sizeof(IterState) % 4 == 0, "IterState words");
     constexpr int SW = (int)(sizeof(IterState) / 4);
+    // the candidate count and the bounds' outputs first: their latency overlaps the copy
+    // and the S0 reduction below
+    unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    const long long kbase = w.ctl->kbase;
+    const double Ub = w.ctl->U;
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
     if (t < 8) s_fit[t] = 0.0;
     double a = 0.0;
@@ -1620,10 +1789,8 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
             for (int e = 0; e < 8; ++e) cf[e] = cf[e] + w.fparts[8 * p + e];
         blk_sum8_add(cf, s_fit, scr);
     }
-    in.K0 = w.ctl->kbase;
-    in.U = w.ctl->U;
-    unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
+    in.K0 = kbase;
+    in.U = Ub;
     SELPROF(1);
     if (c == 0) {
         if (t == 0) {
@@ -1642,7 +1809,9 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
             __syncthreads();
         }
         if (t == 0) w.ctl->levels += lev;
-        if (c <= (unsigned)CAP) {
+        if (c <= (unsigned)SMALL_C) {
+            final_small(src, c, in, sm, scr, &s_st);
+        } else if (c <= (unsigned)CAP) {
             final_lds<CAP, true>(src, c, in, sm, scr, &s_st);
         } else if (c <= (unsigned)CAP2) {
             final_lds<CAP2, false>(src, c, in, sm, scr, &s_st);
@@ -1706,11 +1875,9 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     const SelWS w = carve(tmp, n);
     const HistPack hp = hist_pack(n);
     hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
-                       range_parts, w, skip, hp);
-    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip, hp,
-                       (const unsigned long long *)range);
-    hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev,
-                       (const unsigned long long *)range, skip, hp.fixb);
+                       range_parts, w, skip, hp, (const IterState *)st);
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip, hp);
+    hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip, hp.fixb);
     const int gb = gather_blocks(n);
     FitSrc fs{};
     if (fit && loop) fs = *fit;  // the fused fit needs the fused loop step (it runs after it)

@@ -122,18 +122,39 @@ int main(int argc, char **argv) {
     const int gb = gather_blocks(n);
     hipEvent_t ev[5];
     for (auto &evx : ev) CK(hipEventCreate(&evx));
-    std::vector<std::vector<float>> tk(4);
+    std::vector<std::vector<float>> tk(4), tkw(4);
     int bad = 0;
+    // even reps: the uniform bucket map (a stage's first call); odd reps: the windowed map
+    // centred on the true threshold key moved by 0, +8, -64, +512 uniform bucket widths
+    // (a later call; the last two put the threshold outside the fine window)
+    const int s_uni = kmx > kmn ? std::max(0, 64 - __builtin_clzll(kmx - kmn) - NB_LOG) : 0;
+    const unsigned long long tk_true = bk > 0 ? key[ord[bk - 1]] : kmn;
+    unsigned cand_u = 0, cand_w[4] = {0, 0, 0, 0};
     for (int it = 0; it < reps; ++it) {
+        IterState hs{};
+        const int wq = (it / 2) % 4;
+        if (it & 1) {
+            const long long offs[4] = {0, 8, -64, 512};
+            const long long d = offs[wq] * (long long)(1ULL << s_uni);
+            unsigned long long c = tk_true + (unsigned long long)d;
+            if (d < 0 && tk_true - kmn < (unsigned long long)(-d)) c = kmn;
+            if (d > 0 && kmx - tk_true < (unsigned long long)d) c = kmx;
+            hs.phase = PH_LOOP;
+            hs.k = 1;
+            hs.tkey = c;
+            hs.tmove = 0;
+        } else {
+            hs.phase = PH_HEAD;
+        }
+        CK(hipMemcpy(st, &hs, sizeof hs, hipMemcpyHostToDevice));
         CK(hipEventRecord(ev[0], 0));
         hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, 0, dkey, dr, n, drange,
-                           (int64_t)0, w, (const int *)nullptr, hist_pack(n));
+                           (int64_t)0, w, (const int *)nullptr, hist_pack(n), (const IterState *)st);
         hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, 0, w, hist_blocks(n),
-                           (const int *)nullptr, hist_pack(n), (const unsigned long long *)drange);
+                           (const int *)nullptr, hist_pack(n));
         CK(hipEventRecord(ev[1], 0));
         hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam, (const double *)nullptr,
-                           (const unsigned long long *)drange, (const int *)nullptr,
-                           hist_pack(n).fixb);
+                           (const int *)nullptr, hist_pack(n).fixb);
         CK(hipEventRecord(ev[2], 0));
         hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
                            (const int *)nullptr, FitSrc{});
@@ -147,7 +168,13 @@ int main(int argc, char **argv) {
         for (int q = 0; q < 4; ++q) {
             float ms;
             CK(hipEventElapsedTime(&ms, ev[q], ev[q + 1]));
-            tk[q].push_back(ms * 1000.f);
+            ((it & 1) ? tkw : tk)[q].push_back(ms * 1000.f);
+        }
+        {
+            SelCtl cc;
+            CK(hipMemcpy(&cc, w.ctl, sizeof cc, hipMemcpyDeviceToHost));
+            if (it & 1) cand_w[wq] = cc.ccount;
+            else cand_u = cc.ccount;
         }
         IterState h;
         CK(hipMemcpy(&h, st, sizeof h, hipMemcpyDeviceToHost));
@@ -177,18 +204,23 @@ int main(int argc, char **argv) {
     SelCtl ctl;
     CK(hipMemcpy(&ctl, w.ctl, sizeof ctl, hipMemcpyDeviceToHost));
     const char *names[4] = {"hist+red", "bounds", "gather", "final"};
-    printf("n=%lld mode=%d lam=%g k=%lld cand=%u buckets=[%d,%d] levels=%u chunked=%u radix=%u "
-           "err=%u bad=%d/%d\n",
-           (long long)n, mode, lam, bk, ctl.ccount, ctl.b0, ctl.b1, stats[1] & 0xffffu,
-           stats[1] >> 16, stats[2], stats[0], bad, reps);
-    float tot = 0.f;
-    for (int q = 0; q < 4; ++q) {
-        std::sort(tk[q].begin(), tk[q].end());
-        const float med = tk[q][tk[q].size() / 2];
-        tot += med;
-        printf("  %-7s %8.2f us\n", names[q], med);
+    printf("n=%lld mode=%d lam=%g k=%lld cand=%u window cand (+0,+8,-64,+512)=%u,%u,%u,%u "
+           "buckets=[%d,%d] levels=%u chunked=%u radix=%u err=%u bad=%d/%d\n",
+           (long long)n, mode, lam, bk, cand_u, cand_w[0], cand_w[1], cand_w[2], cand_w[3], ctl.b0,
+           ctl.b1, stats[1] & 0xffffu, stats[1] >> 16, stats[2], stats[0], bad, reps);
+    for (int wv = 0; wv < 2; ++wv) {
+        auto &tt = wv ? tkw : tk;
+        if (tt[0].empty()) continue;
+        float tot = 0.f;
+        printf("  %s map:", wv ? "window " : "uniform");
+        for (int q = 0; q < 4; ++q) {
+            std::sort(tt[q].begin(), tt[q].end());
+            const float med = tt[q][tt[q].size() / 2];
+            tot += med;
+            printf(" %s %.2f", names[q], med);
+        }
+        printf(" total %.2f us (median)\n", tot);
     }
-    printf("  total   %8.2f us\n", tot);
 #ifdef SEL_PROF
     unsigned long long ts[32];
     CK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_selprof), sizeof ts));

@@ -367,7 +367,9 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
         fits += st["n_fits"]
         calls += st["n_nn_calls"]
         if args.nn_timing == "all" or (args.nn_timing == "first" and s_i == 0):
-            timed_calls += st["n_nn_calls"]
+            # NN launches that searched: a later stage's head reuses the previous call's
+            # outputs (its launch is a no-op, kept in nn["ms"]: conservative)
+            timed_calls += st["n_nn_calls"] - st.get("n_nn_reused", 0)
         if s_i == 0 and args.nn_timing == "first":
             ctx.profile_enable(0)
     barrier()

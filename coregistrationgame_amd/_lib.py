@@ -45,7 +45,7 @@ class Stats(C.Structure):
     _fields_ = [
         ("n_nn_calls", C.c_int32), ("n_fits", C.c_int32), ("iters", C.c_int32 * 2),
         ("k_last", C.c_int64), ("frmsd_last", C.c_double * 2), ("T_total", C.c_double * 9),
-        ("gpu_ms", C.c_double), ("max_trace", C.c_int32), ("_pad", C.c_int32),
+        ("gpu_ms", C.c_double), ("max_trace", C.c_int32), ("n_nn_reused", C.c_int32),
         ("trace_k", _ip64), ("trace_frmsd", _dp), ("trace_lambda", _dp), ("trace_T", _dp),
         ("trace_idx", _ip32),
     ]
@@ -396,7 +396,7 @@ def _make_stats(n, trace, trace_idx, max_trace):
 def _stats_dict(st, keep, n):
     nc = st.n_nn_calls
     nf = st.n_fits
-    out = dict(n_nn_calls=nc, n_fits=nf, iters=(st.iters[0], st.iters[1]), k_last=st.k_last,
+    out = dict(n_nn_calls=nc, n_nn_reused=st.n_nn_reused, n_fits=nf, iters=(st.iters[0], st.iters[1]), k_last=st.k_last,
                frmsd_last=(st.frmsd_last[0], st.frmsd_last[1]),
                T_total=np.array(st.T_total[:]).reshape(3, 3), gpu_ms=st.gpu_ms)
     if keep:

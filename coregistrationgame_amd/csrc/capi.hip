@@ -198,7 +198,8 @@ unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long lo
 // every query from its previous match (grid mode, same work order within one run).
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
             bool want_keys, int warm = 0, const int *skip = nullptr,
-            const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true) {
+            const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true,
+            const int *reuse = nullptr) {
     NNArgs a{};
     a.sx = sx;
     a.sy = sy;
@@ -207,6 +208,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.T = T;
     a.skip = skip;
     a.apply_flag = apply_flag;
+    a.reuse = reuse;
     a.idx = want_idx ? c->idx.as<int32_t>() : nullptr;  // the run loop reads idx only for traces
     a.dist = want_keys ? nullptr : c->dist.as<double>();
     a.r = c->r.as<double>();
@@ -325,6 +327,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
              ficp_stats *st) {
     if (st) {
         st->n_nn_calls = 0;
+        st->n_nn_reused = 0;
         st->n_fits = 0;
         st->iters[0] = st->iters[1] = 0;
         st->k_last = 0;
@@ -416,8 +419,9 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             ProfScope ps(c, P_FIT, "fit");
             HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, &dst->no_fit, c->stream));
         }
+        // (a later stage's head reuses the previous call's outputs: dst->nn_reuse)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
-                    false, tidx != nullptr));
+                    false, tidx != nullptr, &dst->nn_reuse));
         return FICP_OK;
     };
     auto enq_b = [&](int64_t i) -> int {
@@ -489,6 +493,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     if (st) {
         const IterState &h = *c->h_state;
         st->n_nn_calls = h.n_nn;
+        st->n_nn_reused = h.n_reuse;
         st->n_fits = h.n_fit;
         st->iters[0] = h.iters[0];
         st->iters[1] = h.iters[1];

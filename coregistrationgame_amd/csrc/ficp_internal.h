@@ -119,6 +119,8 @@ struct NNArgs {
     int warm_c;                 // grid kernels: start from the previous match held in
                                 // (cx, cy, dz2): its d^2 to the moved query, no record reload
     const int *apply_flag;      // T is applied only while *apply_flag != 0 (nullable: always)
+    const int *reuse;           // grid kernel: a no-op while *reuse != 0 -- the source has not
+                                // moved since the previous call, whose outputs stand (nullable)
 };
 
 // Device-resident state of one ICP stage (written by kernels, read back per iteration).
@@ -146,7 +148,9 @@ struct alignas(16) IterState {
     int done;              // 1 once the run is over: NN, sort and scan are no-ops
     int no_fit;            // 1 unless a loop body is due: the fit is a no-op
     int apply;             // the NN call applies T (a fit ran in this iteration)
-    int pad1;
+    int nn_reuse;          // a later stage's head: the source has not moved since the last NN
+                           // call, whose outputs stand (ficp.py:151-153: _iterate() queries
+                           // the same source again); the NN kernel is a no-op
     // selection threshold of the last fraction call (k_select.hip): the k-th pair of the
     // stable (key, orig) order; the fit selects {i : (key_i, orig_i) <= (tkey, torig)}
     unsigned long long tkey;
@@ -154,7 +158,8 @@ struct alignas(16) IterState {
     // |tkey - previous tkey| when both came from loop-body calls of one stage (else 0):
     // sizes the next call's fine bucket window (k_select.hip make_bmap)
     unsigned long long tmove;
-    unsigned long long pad2;
+    int n_reuse;           // NN calls answered by nn_reuse (ficp_stats::n_nn_reused)
+    int pad2;
 };
 
 // FRMSD(k) = (1 / (k/N)**lambda) * sqrt(S_k / k), in the reference's operation order
@@ -268,6 +273,7 @@ __device__ __forceinline__ void loop_set_flags(IterState &s) {
     s.done = s.phase == PH_DONE;
     s.no_fit = s.phase != PH_LOOP;
     s.apply = s.phase == PH_LOOP;
+    s.nn_reuse = s.phase == PH_HEAD && s.n_nn > 0;
 }
 
 __device__ __forceinline__ void loop_end_stage(IterState &s, const LoopCtl &c) {
@@ -287,6 +293,7 @@ __device__ __forceinline__ void loop_end_stage(IterState &s, const LoopCtl &c) {
 __device__ __forceinline__ void loop_step(IterState *st, const LoopCtl &c) {
     IterState &s = *st;
     if (s.done) return;
+    s.n_reuse += s.nn_reuse;
     const int call = s.n_nn++;
     s.k_last = s.k;
     if (call < c.max_trace) {

@@ -785,7 +785,7 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
 
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
-    if (a.skip && *a.skip) return;
+    if ((a.skip && *a.skip) || (a.reuse && *a.reuse)) return;
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     unsigned long long kmin_c = 0, kmax = 0;
     const double *T = (APPLY && (!a.apply_flag || *a.apply_flag)) ? a.T : nullptr;

@@ -6,18 +6,22 @@ that loader, not FICP, is the wall clock. These loaders read the same CSV files 
 the arrays the engine consumes, in the same order and with the same parsing rules. Rows
 become per-plot slices of SoA arrays. Plots keep their first-appearance order.
 
-* `load_stand(ID, path, mapping, sep, impute_h, naslund_params)`: trees.Stand
+* `load_stand(ID, path, mapping, sep, impute_dbh, impute_h, naslund_params)`: trees.Stand
   (`trees.py:333-451`): the StandID filter, the column mapping, heights in metres via
-  decimetres, and the Näslund height imputation from DBH.
+  decimetres, the Näslund height imputation from DBH and the DBH imputation from height.
 * `load_saved_stand(ID, path)`: trees.SavedStand (`trees.py:478-520`), the format the
   app writes.
 * `load_chm(path, x, y, dist, height_unit, mapping, sep, impute_h)`: CHMPlot
   (`chm_plot.py:102-219`): the radial crop, the height unit, the 45 m cap, and skipping
   rows with neither height nor DBH.
 
-DBH imputation (the inverse Näslund fit by `scipy.optimize.minimize_scalar`,
-`trees.py:84-97`) is not reproduced: no part of the FICP path reads DBH. Diameters are
-returned as read.
+DBH imputation is Tree.get_diameter (`trees.py:84-97`, `110-116`): the inverse Näslund
+height by the same bounded `scipy.optimize.minimize_scalar` call on (0, 100) m, capped at
+1.5 m, for a tree whose DBH is missing (None: no DBH column, an empty or unparseable
+field) and whose height is not None.  `StandArrays.stemdiam_m` is Tree.stemdiam (metres,
+imputed where the reference imputes), so `stemdiam_m * 100` is `Stand.write_out`'s
+Diameter_cm (`trees.py:465-483`); `dbh_cm` keeps the centimetres as read.  No part of the
+FICP path reads DBH.
 """
 from __future__ import annotations
 
@@ -41,6 +45,11 @@ class StandArrays:
     dbh_cm: np.ndarray                # centimetres as read, NaN = missing
     plot_center: np.ndarray           # (P, 2): XC/YC of the plot's first row (Stand), centroid (SavedStand)
     center: tuple = field(default=None)  # the stand centre: mean of the plot centroids
+    stemdiam_m: np.ndarray = field(default=None)  # Tree.stemdiam (m, imputed), NaN = None
+
+    def write_out_diameter_cm(self):
+        """Stand.write_out's Diameter_cm column (trees.py:466-481), in load order."""
+        return self.stemdiam_m * 100.0
 
     def plot(self, p):
         s = slice(self.offsets[p], self.offsets[p + 1])
@@ -93,6 +102,17 @@ def naslund_height(stemdiam_m, params=NASLUND_DEFAULT):
     return 1.3 + (d_cm / (a + b * d_cm)) ** c
 
 
+def naslund_diameter(height_m, params=NASLUND_DEFAULT):
+    """Tree.get_diameter (trees.py:84-97): DBH (m) whose Näslund height is height_m, by the
+    reference's bounded 1-D minimisation on (0, 100), capped at 1.5 m."""
+    from scipy.optimize import minimize_scalar
+
+    def objective(x):
+        return (height_m - naslund_height(x, params)) ** 2
+
+    return min(minimize_scalar(objective, bounds=(0, 100), method="bounded").x, 1.5)
+
+
 def _centroids(x, y, offsets):
     """Plot._update_centroid (trees.py:149-153): np.mean of the (n, 2) C-ordered array."""
     out = np.zeros((len(offsets) - 1, 2))
@@ -121,7 +141,8 @@ def _group(plot_vals):
     return order, ids, offsets
 
 
-def load_stand(ID, path, mapping=None, sep="\t", impute_h=True, naslund_params=None) -> StandArrays:
+def load_stand(ID, path, mapping=None, sep="\t", impute_h=True, naslund_params=None,
+               impute_dbh=True) -> StandArrays:
     import pandas as pd
     recs = pd.read_csv(path, sep=sep)
     cols = set(recs.columns)
@@ -168,6 +189,7 @@ def load_stand(ID, path, mapping=None, sep="\t", impute_h=True, naslund_params=N
     x = np.array([X[i] for i in rows], dtype=float)
     y = np.array([Y[i] for i in rows], dtype=float)
     dbh = np.full(n, np.nan)
+    sd = np.full(n, np.nan)
     h = np.full(n, np.nan)
     params = tuple(naslund_params) if naslund_params is not None else NASLUND_DEFAULT
     for j, i in enumerate(rows):
@@ -180,11 +202,15 @@ def load_stand(ID, path, mapping=None, sep="\t", impute_h=True, naslund_params=N
         height = None if hdm is None else hdm / 10  # Tree stores metres (trees.py:67)
         if height is None and impute_h and dcm is not None:  # Tree.impute_height
             height = naslund_height(dcm / 100, params)
+        stem = None if dcm is None else dcm / 100  # Tree stores metres (trees.py:66)
+        if stem is None and impute_dbh and height is not None:  # Tree.impute_dbh
+            stem = naslund_diameter(height, params)
+        sd[j] = np.nan if stem is None else stem
         h[j] = np.nan if height is None else height
     centers = np.array([[XC[rows[offsets[p]]], YC[rows[offsets[p]]]] for p in range(len(ids))], dtype=float)
     cen = _centroids(x, y, offsets)
     return StandArrays(ID, ids, offsets, np.array([TID[i] for i in rows], dtype=object), x, y, h, dbh,
-                       centers, _stand_center(cen))
+                       centers, _stand_center(cen), sd)
 
 
 def load_saved_stand(ID, path, naslund_params=None) -> StandArrays:
@@ -205,7 +231,7 @@ def load_saved_stand(ID, path, naslund_params=None) -> StandArrays:
         dbh[j] = np.nan if dv is None else dv
     cen = _centroids(x, y, offsets)
     return StandArrays(ID, ids, offsets, recs["TreeID"].to_numpy(dtype=object)[order], x, y, h, dbh,
-                       cen.copy(), _stand_center(cen))
+                       cen.copy(), _stand_center(cen), dbh / 100)
 
 
 def load_chm(path, x=None, y=None, dist=40, height_unit="m", mapping=None, sep="\t", impute_h=False,

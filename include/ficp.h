@@ -51,7 +51,8 @@ typedef struct ficp_stats {
     double T_total[9];       /* out: composite transform of the whole run (row-major) */
     double gpu_ms;           /* out: wall time of the run on the device stream        */
     int32_t max_trace;       /* in : capacity of the trace arrays (NN calls)          */
-    int32_t _pad;
+    int32_t n_nn_reused;     /* out: NN calls answered by the previous call's outputs (a
+                                later stage's head: the source has not moved since)   */
     int64_t *trace_k;        /* [max_trace]      k per NN/fraction call               */
     double *trace_frmsd;     /* [max_trace]      FRMSD at that k                      */
     double *trace_lambda;    /* [max_trace]      lambda in force                      */

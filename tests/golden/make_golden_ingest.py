@@ -30,7 +30,7 @@ import trees as ref_trees  # noqa: E402
 
 
 def stand_record(st):
-    tid, x, y, h, pid, cen = [], [], [], [], [], []
+    tid, x, y, h, sd, pid, cen = [], [], [], [], [], [], []
     for p in st.plots:
         pid.append(str(p.plotid))
         cen.append([float(p.center[0]), float(p.center[1])])
@@ -39,7 +39,11 @@ def stand_record(st):
             x.append(float(t.x))
             y.append(float(t.y))
             h.append(np.nan if t.height is None else float(t.height))
+            sd.append(np.nan if t.stemdiam is None else float(t.stemdiam))
+    # Stand.write_out's Diameter_cm column (trees.py:465-483), in the same tree order
+    wo = st.write_out()["Diameter_cm"].to_numpy(dtype=float)
     return dict(tree_id=np.array(tid), x=np.array(x), y=np.array(y), height=np.array(h),
+                stemdiam=np.array(sd), diameter_cm_out=wo,
                 plot_ids=np.array(pid), sizes=np.array([len(p.trees) for p in st.plots]),
                 plot_center=np.array(cen), center=np.array(st.center, dtype=float))
 
@@ -101,6 +105,13 @@ def main():
     run("stand_mapped", buf.getvalue(), "stand", dict(ID=2, mapping=mapping, sep=",", impute_dbh=False,
                                                        impute_h=True))
     run("stand_noimpute", buf.getvalue(), "stand", dict(ID=1, sep=",", impute_dbh=False, impute_h=False))
+    # DBH imputation (Tree.impute_dbh, trees.py:84-97, 110-116): unparseable DBH fields
+    # with a height, and a file without a DBH column at all
+    run("stand_impute_dbh", buf.getvalue(), "stand", dict(ID=1, sep=",", impute_dbh=True, impute_h=True))
+    buf2 = io.StringIO()
+    pd.DataFrame([{k: v for k, v in r.items() if k != "STEMDIAM"} for r in rows]).to_csv(buf2, index=False)
+    run("stand_no_dbh_column", buf2.getvalue(), "stand", dict(ID=2, sep=",", impute_dbh=True,
+                                                               impute_h=True))
     # CHM detections: units, the 45 m cap, the DBH-only fallback
     crow = [{"X": float(a), "Y": float(b), "IDALS": f"c{i}", "H": float(h), "DBH": float(d)}
             for i, (a, b, h, d) in enumerate(zip(rng.uniform(0, 60, 40), rng.uniform(0, 60, 40),

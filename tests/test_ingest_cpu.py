@@ -24,8 +24,12 @@ def test_loader_matches_reference(name, tmp_path):
         got = ingest.load_chm(f, **kw)
     else:
         ID = kw.pop("ID")
-        kw.pop("impute_dbh", None)
+        if kind == "saved":
+            kw.pop("impute_dbh", None)
         got = (ingest.load_saved_stand if kind == "saved" else ingest.load_stand)(ID, f, **kw)
+        if f"{name}/stemdiam" in Z.files:  # Tree.stemdiam, DBH imputation included
+            np.testing.assert_array_equal(got.stemdiam_m, Z[f"{name}/stemdiam"])
+            np.testing.assert_array_equal(got.write_out_diameter_cm(), Z[f"{name}/diameter_cm_out"])
         assert [str(p) for p in got.plot_ids] == list(Z[f"{name}/plot_ids"])
         np.testing.assert_array_equal(np.diff(got.offsets), Z[f"{name}/sizes"])
         np.testing.assert_array_equal(got.plot_center, Z[f"{name}/plot_center"])

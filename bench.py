@@ -537,7 +537,7 @@ def bench_c5(args, rank, world, local, D, steps, warmup):
         n = m = args.c5_size
     plot = synth.make_plot(n, m, f, seed0, md=md)  # same plot on every rank (replicated source)
     part = PartitionedFICP(plot.source, plot.target, threshold=thr, max_iterations=max_it,
-                           device=local, local_shards=args.local_shards)
+                           device=local, local_shards=args.local_shards, mode=args.c5_mode)
     for _ in range(warmup):
         part.run_resident(lambda0=3.0)
 
@@ -567,9 +567,13 @@ def bench_c5(args, rank, world, local, D, steps, warmup):
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": f"synthetic (SURVEY.md §8(d) generator, seed {seed0}, geo-referenced)",
         "config": {"workload": desc, "n_trees": n, "n_chm": m, "inlier_fraction": f, "match_dims": md,
-                   "shards": world * args.local_shards,
-                   "parallelism": f"CHM layer in {world * args.local_shards} row shards over {world} GPU(s); "
-                                  "2 all-reduces (d2 MIN, idx MIN) per NN call"},
+                   "shards": world * args.local_shards, "mode": args.c5_mode,
+                   "parallelism": (f"CHM layer in {world * args.local_shards} row shards over {world} GPU(s); "
+                                   "2 all-reduces (d2 MIN, idx MIN, 12 B per tree) per NN call"
+                                   if args.c5_mode == "target" else
+                                   f"tree rows in {world * args.local_shards} ranges over {world} GPU(s), layer "
+                                   "replicated; per NN call: range MAX (16 B), histogram SUM (128 KB), "
+                                   "candidate and fit-sum all-gathers")},
         "iterations_per_step": fits / steps, "nn_calls_per_step": calls / steps,
         "correspondences_per_s": calls * n / dt, "roofline": None, "cpu_baseline": None,
     }
@@ -625,6 +629,8 @@ def main():
     ap.add_argument("--plots", type=int, default=0, help="batch workload: number of plots (default 1024)")
     ap.add_argument("--c5-size", type=int, default=0, help="c5 workload: trees = stems (default 8M)")
     ap.add_argument("--local-shards", type=int, default=1, help="c5 workload: shards per GPU")
+    ap.add_argument("--c5-mode", default="source", choices=["source", "target"],
+                    help="c5 workload: split the tree rows (source) or the CHM layer (target)")
     ap.add_argument("--dry-run", action="store_true", help="no GPU work (launcher/process-group check)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"])
     args = ap.parse_args()

@@ -140,6 +140,20 @@ def lib():
         "ficp_select_fit_device": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, C.c_double, _i32,
                                     C.c_double, C.c_double, _ip64, _dp, _dp], C.c_int),
         "ficp_apply_device": ([_vp, _vp, _vp, _i64, _dp], C.c_int),
+        "ficp_set_stream": ([_vp, _vp], C.c_int),
+        "ficp_dist_begin": ([_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _dp, C.c_double, _i32,
+                             _i32, C.c_double, C.c_double, _i32, _i32], C.c_int),
+        "ficp_dist_fit_sums": ([_vp, _vp], C.c_int),
+        "ficp_dist_fit_solve": ([_vp, _vp, _i32], C.c_int),
+        "ficp_dist_nn_shard": ([_vp, _vp, _i64, _vp, _vp], C.c_int),
+        "ficp_dist_select_merged": ([_vp, _vp, _vp, _vp, _vp, _i64], C.c_int),
+        "ficp_dist_nn_local": ([_vp, _vp], C.c_int),
+        "ficp_dist_hist_words": ([], C.c_int),
+        "ficp_dist_hist": ([_vp, _vp, _vp], C.c_int),
+        "ficp_dist_candidates": ([_vp, _vp, _vp, _i32], C.c_int),
+        "ficp_dist_final": ([_vp, _vp, _i32, _i32, _i64], C.c_int),
+        "ficp_dist_wait": ([_vp, _i64, C.POINTER(_i32)], C.c_int),
+        "ficp_dist_end": ([_vp, C.POINTER(Stats)], C.c_int),
         "ficp_dev_alloc": ([_vp, _i64, C.POINTER(_vp)], C.c_int),
         "ficp_dev_free": ([_vp, _vp], C.c_int),
         "ficp_memcpy_h2d": ([_vp, _vp, _vp, _i64], C.c_int),
@@ -371,6 +385,61 @@ class Context:
 
     def synchronize(self):
         _check(lib().ficp_synchronize(self.h))
+
+    # ---- distributed run of one plot, stream-ordered (include/ficp.h ficp_dist_*)
+    def set_stream(self, stream_handle: int):
+        _check(lib().ficp_set_stream(self.h, _vp(stream_handle or 0)))
+
+    def dist_begin(self, mode: int, x_ptr: int, y_ptr: int, z_ptr: int, n_local: int, n_total: int,
+                   n_max: int, row0: int, lambdas, threshold: float, max_iterations: int,
+                   allow_reflection: bool, pivot, world: int, capd: int):
+        lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+        _check(lib().ficp_dist_begin(self.h, int(mode), _vp(x_ptr), _vp(y_ptr), _vp(z_ptr or 0), int(n_local),
+                                     int(n_total), int(n_max), int(row0), len(lam), _p(lam), float(threshold),
+                                     int(max_iterations), int(bool(allow_reflection)), float(pivot[0]),
+                                     float(pivot[1]), int(world), int(capd)))
+
+    def dist_fit_sums(self, sums8_ptr: int):
+        _check(lib().ficp_dist_fit_sums(self.h, _vp(sums8_ptr)))
+
+    def dist_fit_solve(self, sums_ptr: int, world: int):
+        _check(lib().ficp_dist_fit_solve(self.h, _vp(sums_ptr), int(world)))
+
+    def dist_nn_shard(self, ctrl: "Context", idx_offset: int, d2_ptr: int, idx_ptr: int):
+        _check(lib().ficp_dist_nn_shard(self.h, ctrl.h, int(idx_offset), _vp(d2_ptr), _vp(idx_ptr)))
+
+    def dist_select_merged(self, d2_ptr: int, idx_ptr: int, tx_ptr: int, ty_ptr: int, iteration: int):
+        _check(lib().ficp_dist_select_merged(self.h, _vp(d2_ptr), _vp(idx_ptr), _vp(tx_ptr), _vp(ty_ptr),
+                                             int(iteration)))
+
+    def dist_nn_local(self, range2_ptr: int):
+        _check(lib().ficp_dist_nn_local(self.h, _vp(range2_ptr)))
+
+    def dist_hist(self, range2_ptr: int, hist_ptr: int):
+        _check(lib().ficp_dist_hist(self.h, _vp(range2_ptr), _vp(hist_ptr)))
+
+    def dist_candidates(self, hist_ptr: int, pack_ptr: int, capd: int):
+        _check(lib().ficp_dist_candidates(self.h, _vp(hist_ptr), _vp(pack_ptr), int(capd)))
+
+    def dist_final(self, packs_ptr: int, world: int, capd: int, iteration: int):
+        _check(lib().ficp_dist_final(self.h, _vp(packs_ptr), int(world), int(capd), int(iteration)))
+
+    def dist_wait(self, iteration: int) -> bool:
+        v = C.c_int32(0)
+        _check(lib().ficp_dist_wait(self.h, int(iteration), C.byref(v)))
+        return bool(v.value)
+
+    def dist_end(self) -> dict:
+        st, keep = _make_stats(0, True, False, 4096)
+        _check(lib().ficp_dist_end(self.h, C.byref(st)))
+        out = _stats_dict(st, keep, 0)
+        for key in ("frmsd", "lam", "T"):  # a distributed run traces k only
+            out.pop(key, None)
+        return out
+
+
+def dist_hist_words() -> int:
+    return int(lib().ficp_dist_hist_words())
 
 
 def _make_stats(n, trace, trace_idx, max_trace):

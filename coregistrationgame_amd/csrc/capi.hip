@@ -539,6 +539,38 @@ int check_md(int32_t md) {
     return FICP_OK;
 }
 
+// ---- distributed runs (ficp_dist_*): small glue kernels
+constexpr unsigned long long kFlip = 0x8000000000000000ULL;
+constexpr int kDistTrace = 4096;  // k trace capacity of a distributed run (NN calls)
+
+// the key range {~kmin, kmax} of the local rows as int64 words whose signed order is the
+// unsigned order (top bit flipped): the caller's MAX all-reduce gives the global range
+__global__ void k_dist_range_out(const unsigned long long *range, long long *out,
+                                 const int *skip) {
+    if ((skip && *skip) || threadIdx.x != 0) return;
+    out[0] = (long long)(range[0] ^ kFlip);
+    out[1] = (long long)(range[1] ^ kFlip);
+}
+
+__global__ void k_dist_range_in(const long long *in, unsigned long long *range, const int *skip) {
+    if ((skip && *skip) || threadIdx.x != 0) return;
+    range[0] = (unsigned long long)in[0] ^ kFlip;
+    range[1] = (unsigned long long)in[1] ^ kFlip;
+}
+
+__global__ void k_dist_gorig(const uint32_t *worig, int64_t n, int64_t row0, uint32_t *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)(row0 + (worig ? (int64_t)worig[i] : i));
+}
+
+int check_dist(ficp_ctx *c, int mode) {
+    CHK(check_ctx(c));
+    if (c->dist_mode != mode)
+        return fail(FICP_ESTATE, "no %s-partitioned run begun on this context",
+                    mode == 1 ? "target" : "source");
+    return FICP_OK;
+}
+
 void reset_target(ficp_ctx *c, int64_t m, int md) {
     c->has_target = true;
     c->grid_ready = false;
@@ -602,6 +634,9 @@ void ficp_destroy(ficp_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->own_stream) c->stream = c->own_stream;  // a caller's stream is not ours to destroy
+    c->gorig.release();
+    c->drange.release();
     DevBuf *bufs[] = {&c->tx,     &c->ty,         &c->tz,       &c->cell_of,  &c->counts,
                       &c->cell_start, &c->fill,   &c->pts,      &c->scan_tmp, &c->mm_part,
                       &c->mm_out, &c->sx,         &c->sy,       &c->sz,       &c->idx,
@@ -1099,6 +1134,278 @@ int ficp_memcpy_d2d(ficp_ctx *c, void *dst, const void *src, int64_t bytes) {
 int ficp_synchronize(ficp_ctx *c) {
     CHK(check_ctx(c));
     return sync(c);
+}
+
+
+// ===================================================================== distributed runs
+// One plot over several ranks, every step enqueued on the context's
+// stream -- the caller's stream after ficp_set_stream, on which it also runs its
+// collectives -- so no step waits for the host; the host reads one done flag per
+// iteration (ficp_dist_wait), one iteration behind.
+int ficp_set_stream(ficp_ctx *c, void *stream) {
+    CHK(check_ctx(c));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!c->own_stream) c->own_stream = c->stream;
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    if (c->stream == c->own_stream) c->own_stream = nullptr;
+    return FICP_OK;
+}
+
+int ficp_dist_begin(ficp_ctx *c, int32_t mode, double *x, double *y, const double *z,
+                    int64_t n_local, int64_t n_total, int64_t n_max, int64_t row0,
+                    int32_t nstages, const double *lambdas, double threshold,
+                    int32_t max_iterations, int32_t allow_reflection, double pivot_x,
+                    double pivot_y, int32_t world, int32_t capd) {
+    CHK(check_ctx(c));
+    if (mode != 1 && mode != 2) return fail(FICP_EINVAL, "mode must be 1 (target) or 2 (source)");
+    if (!c->has_target) return fail(FICP_ESTATE, "no target set");
+    if (n_local <= 0 || n_local > 0x3fffffff || n_total < n_local || n_max < n_local ||
+        row0 < 0 || row0 + n_local > n_total || n_total > 0x7fffffff || !x || !y ||
+        (c->md == 3 && !z) || nstages < 0 || nstages > kLamIn || (nstages > 0 && !lambdas) ||
+        world < 1 || capd < 1)
+        return fail(FICP_EINVAL, "bad arguments");
+    if (mode == 1 && n_local != n_total) return fail(FICP_EINVAL, "target mode replicates the rows");
+    if (c->m > kMaxGridStems) return fail(FICP_EINVAL, "the distributed run needs the grid NN");
+    c->nn_mode = 2;  // the steps below are written for the grid kernels (any layer size)
+    c->dist_mode = 0;
+    c->dist_n = n_local;
+    c->dist_ntot = n_total;
+    c->dist_nmax = n_max;
+    c->dist_nws = std::max<int64_t>(n_local, (int64_t)world * capd);
+    c->dist_calls = 0;
+    c->dist_px = pivot_x;
+    c->dist_py = pivot_y;
+    c->dist_refl = allow_reflection;
+    c->dist_x = x;
+    c->dist_y = y;
+    c->dist_z = c->md == 3 ? z : nullptr;
+    CHK(ensure_work(c, n_local));
+    CHK(c->sel_tmp.ensure(sel_tmp_bytes(c->dist_nws)));
+    if (c->sel_tmp.gen != c->sel_init_gen) {
+        HIPCHK(launch_select_init(c->sel_tmp.p, c->dist_nws, c->stream));
+        c->sel_init_gen = c->sel_tmp.gen;
+    }
+    CHK(c->drange.ensure(16));
+    if (mode == 2) {  // this rank's rows in the spatial work order of the whole layer's grid
+        CHK(ensure_bbox(c));
+        BSJob gj{}, wj{};
+        CHK(ensure_grid(c, &gj));
+        CHK(build_work_order(c, x, y, c->dist_z, n_local, &wj));
+        if (gj.n > 0 || wj.n > 0)
+            HIPCHK(launch_bsort2(gj.n > 0 ? gj : wj, gj.n > 0 ? wj : BSJob{}, c->stream));
+    }
+    CHK(c->gorig.ensure(n_local * 4));
+    hipLaunchKernelGGL(k_dist_gorig, dim3((unsigned)((n_local + 255) / 256)), dim3(256), 0,
+                       c->stream, mode == 2 ? c->worig.as<uint32_t>() : nullptr, n_local, row0,
+                       c->gorig.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    LoopCtl lc{};
+    lc.nstages = nstages;
+    lc.max_iter = max_iterations;
+    lc.threshold = threshold;
+    for (int e = 0; e < kLamIn; ++e) lc.lam_in[e] = e < nstages ? lambdas[e] : 0.0;
+    // k of every call (one store per call by the loop step): ficp_dist_end's trace_k
+    CHK(c->tr_k.ensure((size_t)kDistTrace * 8));
+    lc.max_trace = kDistTrace;
+    lc.tk = c->tr_k.as<long long>();
+    c->dist_lc = lc;
+    HIPCHK(launch_loop_init(c->state_dev.as<IterState>(), lc, c->stream));
+    c->dist_mode = mode;
+    return FICP_OK;
+}
+
+/* the fit of ficp.py:134 from the previous selection, this rank's rows: 8 sums (device) */
+int ficp_dist_fit_sums(ficp_ctx *c, double *sums8) {
+    CHK(check_ctx(c));
+    if (!c->dist_mode || !sums8) return fail(c->dist_mode ? FICP_EINVAL : FICP_ESTATE, "bad call");
+    IterState *st = c->state_dev.as<IterState>();
+    const bool src = c->dist_mode == 2;
+    FitIn fa{src ? c->wx.as<double>() : c->dist_x, src ? c->wy.as<double>() : c->dist_y,
+             c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(), nullptr,
+             c->gorig.as<uint32_t>(), c->dist_n, c->dist_px, c->dist_py, st};
+    HIPCHK(launch_fit_sums(fa, c->fit_tmp.p, &st->no_fit, sums8, c->stream));
+    return FICP_OK;
+}
+
+/* the solve on the ranks' sums (world x 8, added in rank order); target mode also
+   applies T to the replicated rows here (source mode applies it in the NN step) */
+int ficp_dist_fit_solve(ficp_ctx *c, const double *sums, int32_t world) {
+    CHK(check_ctx(c));
+    if (!c->dist_mode || !sums || world < 1) return fail(c->dist_mode ? FICP_EINVAL : FICP_ESTATE, "bad call");
+    IterState *st = c->state_dev.as<IterState>();
+    HIPCHK(launch_fit_solve_ranks(sums, world, c->dist_px, c->dist_py, c->dist_refl, st,
+                                  &st->no_fit, c->stream));
+    if (c->dist_mode == 1)
+        HIPCHK(launch_apply_xy_flags(c->dist_x, c->dist_y, c->dist_n, st->T, &st->done, &st->apply,
+                                     c->stream));
+    return FICP_OK;
+}
+
+/* target mode: NN of the replicated rows against this context's shard (as ficp_nn_device),
+   a no-op once the controller's run is over */
+int ficp_dist_nn_shard(ficp_ctx *c, ficp_ctx *ctrl, int64_t idx_offset, double *d2, int32_t *idx) {
+    CHK(check_dist(ctrl, 1));
+    CHK(check_ctx(c));
+    if (!c->has_target) return fail(FICP_ESTATE, "no target set");
+    const int64_t n = ctrl->dist_n;
+    if (!d2 || !idx || idx_offset < 0 || idx_offset + c->m > 0x7fffffff)
+        return fail(FICP_EINVAL, "bad arguments");
+    if (c->stream != ctrl->stream) return fail(FICP_ESTATE, "shard and controller streams differ");
+    if (c->m == 0) {
+        HIPCHK(launch_fill_inf(d2, idx, n, c->stream));
+        return FICP_OK;
+    }
+    CHK(ensure_work(c, n));
+    NNArgs a{};
+    a.sx = ctrl->dist_x;
+    a.sy = ctrl->dist_y;
+    a.sz = c->md == 3 ? ctrl->dist_z : nullptr;
+    a.n = n;
+    a.idx = idx;
+    a.r = d2;
+    a.tx = c->tx.as<double>();
+    a.ty = c->ty.as<double>();
+    a.skip = &ctrl->state_dev.as<IterState>()->done;
+    if (c->m > kMaxGridStems) return fail(FICP_EINVAL, "the distributed run needs the grid NN");
+    c->nn_mode = 2;
+    CHK(ensure_bbox(c));
+    CHK(ensure_grid(c));
+    HIPCHK(launch_nn_grid(a, c->gv, c->md, c->stream, false));
+    HIPCHK(launch_add_offset(idx, n, idx_offset, c->stream));
+    return FICP_OK;
+}
+
+/* target mode: the merged (d2, idx) -> selection + loop step (ficp.py:73-86, 122-154);
+   the iteration's done flag goes to slot `iteration` of the pinned ring */
+int ficp_dist_select_merged(ficp_ctx *c, const double *d2, const int32_t *idx, const double *tx,
+                            const double *ty, int64_t iteration) {
+    CHK(check_dist(c, 1));
+    if (!d2 || !idx || !tx || !ty || iteration < 0) return fail(FICP_EINVAL, "bad arguments");
+    const int64_t n = c->dist_n;
+    IterState *st = c->state_dev.as<IterState>();
+    HIPCHK(launch_corr_from_merge(d2, idx, tx, ty, n, c->key.as<unsigned long long>(),
+                                  c->r.as<double>(), c->ccx.as<double>(), c->ccy.as<double>(),
+                                  range_ptr(c), c->stream));
+    const int slot = (int)(iteration % kLoopRing);
+    __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
+    HIPCHK(launch_select(c->key.as<unsigned long long>(), nullptr, c->r.as<double>(), n, 0.0,
+                         &st->lam_cur, range_ptr(c), (n + 255) / 256, c->sel_tmp.p, st, &st->done,
+                         &c->dist_lc, &c->h_flags[slot], c->stream, nullptr));
+    c->dist_calls += 1;
+    return FICP_OK;
+}
+
+/* source mode: NN of this rank's rows (T applied first, certified reuse from the second
+   call) against the whole layer; range2 (int64[2], device) = the rows' key range words
+   for the caller's MAX all-reduce */
+int ficp_dist_nn_local(ficp_ctx *c, int64_t *range2) {
+    CHK(check_dist(c, 2));
+    if (!range2) return fail(FICP_EINVAL, "bad arguments");
+    IterState *st = c->state_dev.as<IterState>();
+    CHK(nn_call(c, c->wx.as<double>(), c->wy.as<double>(), c->md == 3 ? c->wz.as<double>() : nullptr,
+                c->dist_n, st->T, true, c->dist_calls == 0 ? 1 : 2, &st->done, &st->apply, true,
+                false, &st->nn_reuse));
+    hipLaunchKernelGGL(k_dist_range_out, dim3(1), dim3(64), 0, c->stream, range_ptr(c),
+                       (long long *)range2, &st->done);
+    HIPCHK(hipGetLastError());
+    return FICP_OK;
+}
+
+/* source mode: the local histogram under the global range (int64[2] from the MAX
+   all-reduce) -> hist (int64[2 * 8192], device) for the caller's SUM all-reduce */
+int ficp_dist_hist(ficp_ctx *c, const int64_t *range2, int64_t *hist) {
+    CHK(check_dist(c, 2));
+    if (!range2 || !hist) return fail(FICP_EINVAL, "bad arguments");
+    IterState *st = c->state_dev.as<IterState>();
+    hipLaunchKernelGGL(k_dist_range_in, dim3(1), dim3(64), 0, c->stream, (const long long *)range2,
+                       range_ptr(c), &st->done);
+    HIPCHK(hipGetLastError());
+    HIPCHK(launch_select_dist_hist(c->key.as<unsigned long long>(), c->r.as<double>(), c->dist_n,
+                                   c->dist_nmax, range_ptr(c), c->sel_tmp.p, c->dist_nws, st,
+                                   &st->done, (long long *)hist, c->stream));
+    return FICP_OK;
+}
+
+int ficp_dist_hist_words(void) { return sel_hist_words(); }
+
+/* source mode: bounds from the summed histogram, this rank's candidates packed into
+   pack (int64[4 + 3 capd], device) for the caller's all-gather */
+int ficp_dist_candidates(ficp_ctx *c, const int64_t *hist, int64_t *pack, int32_t capd) {
+    CHK(check_dist(c, 2));
+    if (!hist || !pack || capd < 1) return fail(FICP_EINVAL, "bad arguments");
+    IterState *st = c->state_dev.as<IterState>();
+    HIPCHK(launch_select_dist_gather(c->key.as<unsigned long long>(), c->gorig.as<uint32_t>(),
+                                     c->r.as<double>(), c->dist_n, c->dist_ntot, c->dist_nmax,
+                                     (const long long *)hist, 0.0, &st->lam_cur, c->sel_tmp.p,
+                                     c->dist_nws, &st->done, (long long *)pack, capd, c->stream));
+    return FICP_OK;
+}
+
+/* source mode: the final selection on the gathered packs (world x (4 + 3 capd), rank
+   order) + the loop step; the done flag goes to slot `iteration` of the pinned ring */
+int ficp_dist_final(ficp_ctx *c, const int64_t *packs, int32_t world, int32_t capd,
+                    int64_t iteration) {
+    CHK(check_dist(c, 2));
+    if (!packs || world < 1 || capd < 1 || (int64_t)world * capd > c->dist_nws || iteration < 0)
+        return fail(FICP_EINVAL, "bad arguments");
+    IterState *st = c->state_dev.as<IterState>();
+    const int slot = (int)(iteration % kLoopRing);
+    __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
+    HIPCHK(launch_select_dist_final((const long long *)packs, world, capd, c->dist_ntot, 0.0,
+                                    &st->lam_cur, c->sel_tmp.p, c->dist_nws, st, &st->done,
+                                    &c->dist_lc, &c->h_flags[slot], c->stream));
+    c->dist_calls += 1;
+    return FICP_OK;
+}
+
+/* host: wait for iteration `iteration`'s done flag (*done = 1: the run is over) */
+int ficp_dist_wait(ficp_ctx *c, int64_t iteration, int32_t *done) {
+    CHK(check_ctx(c));
+    if (!c->dist_mode || !done || iteration < 0) return fail(FICP_EINVAL, "bad call");
+    int v = 0;
+    CHK(poll_flag(c, &c->h_flags[iteration % kLoopRing], v));
+    *done = v != 0;
+    return FICP_OK;
+}
+
+/* end of the run: source mode writes this rank's XY back to the caller's rows; stats as
+   ficp_run's (without traces) */
+int ficp_dist_end(ficp_ctx *c, ficp_stats *st) {
+    CHK(check_ctx(c));
+    if (!c->dist_mode) return fail(FICP_ESTATE, "no distributed run begun");
+    const int mode = c->dist_mode;
+    c->dist_mode = 0;
+    if (mode == 2)
+        HIPCHK(launch_scatter_xy(c->worig.as<uint32_t>(), c->wx.as<double>(), c->wy.as<double>(),
+                                 c->dist_n, c->dist_x, c->dist_y, c->stream));
+    HIPCHK(launch_select_stats(c->sel_tmp.p, c->dist_nws, c->sel_stats.as<unsigned>(), c->stream));
+    c->h_rep->misc[1] = c->h_rep->misc[2] = c->h_rep->misc[3] = 0u;
+    CHK(report_wait(c, ReportSeg{c->state_dev.p, &c->h_rep->st, (int)(sizeof(IterState) / 4)},
+                    ReportSeg{c->sel_stats.p, &c->h_rep->misc[1], 3}, ReportSeg{}));
+    const IterState &h = c->h_rep->st;
+    if (!h.done) return fail(FICP_EHIP, "distributed ICP loop did not finish");
+    if (c->h_rep->misc[1] & 2u)
+        return fail(FICP_EHIP, "a rank's selection candidates exceeded the pack capacity");
+    if (c->h_rep->misc[1]) return fail(FICP_EHIP, "fraction selection raised error flag %u", c->h_rep->misc[1]);
+    if (st) {
+        st->n_nn_calls = h.n_nn;
+        st->n_nn_reused = h.n_reuse;
+        st->n_fits = h.n_fit;
+        st->iters[0] = h.iters[0];
+        st->iters[1] = h.iters[1];
+        st->k_last = h.k_last;
+        st->frmsd_last[0] = h.frmsd_last[0];
+        st->frmsd_last[1] = h.frmsd_last[1];
+        memcpy(st->T_total, h.Ttot, sizeof st->T_total);
+        st->gpu_ms = 0.0;
+        const int nc = std::min(std::min(h.n_nn, st->max_trace), kDistTrace);
+        if (nc > 0 && st->trace_k) {
+            HIPCHK(hipMemcpyAsync(st->trace_k, c->tr_k.p, (size_t)nc * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+            CHK(sync(c));
+        }
+    }
+    return FICP_OK;
 }
 
 }  // extern "C"

@@ -147,6 +147,19 @@ struct ficp_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
     BatchBufs *batch = nullptr;  // capi_batch.hip
+
+    // distributed run of one plot over several ranks (capi.hip, ficp_dist_*)
+    hipStream_t own_stream = nullptr;  // the context's stream while a caller's stream is set
+    int dist_mode = 0;                 // 0 none, 1 target-partitioned, 2 source-partitioned
+    int64_t dist_n = 0, dist_ntot = 0, dist_nmax = 0, dist_nws = 0;
+    int64_t dist_calls = 0;            // NN steps enqueued in this run (the first is cold)
+    double dist_px = 0.0, dist_py = 0.0;
+    int dist_refl = 0;
+    double *dist_x = nullptr, *dist_y = nullptr;  // the caller's rows (device)
+    const double *dist_z = nullptr;
+    LoopCtl dist_lc{};
+    DevBuf gorig;                      // caller index (row0 + local) of each work-order row
+    DevBuf drange;                     // int64 range words of the local rows (top bit flipped)
 };
 
 namespace ficp_capi {

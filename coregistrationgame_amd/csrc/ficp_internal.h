@@ -528,7 +528,32 @@ int64_t fit_scratch_offset();
 hipError_t launch_fit_init(void *tmp, hipStream_t s);
 hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState *st,
                       const int *skip, hipStream_t s);
+// distributed runs (capi_dist.hip): this rank's 8 fit sums; the solve on the ranks' sums
+hipError_t launch_fit_sums(const FitIn &a, void *tmp, const int *skip, double *out8,
+                           hipStream_t s);
+hipError_t launch_fit_solve_ranks(const double *sums, int world, double px, double py,
+                                  int allow_refl, IterState *st, const int *skip, hipStream_t s);
+// distributed selection (k_select.hip): local histogram -> integer totals (int64[2 * 8192]);
+// from the summed totals: bounds, local candidates packed (int64[4 + 3 capd]); from the
+// gathered packs: the final selection with the fused loop step
+int sel_hist_words();
+hipError_t launch_select_dist_hist(const unsigned long long *key, const double *r, int64_t n,
+                                   int64_t n_max, const unsigned long long *range, void *tmp,
+                                   int64_t n_ws, const IterState *st, const int *skip,
+                                   long long *hist_out, hipStream_t s);
+hipError_t launch_select_dist_gather(const unsigned long long *key, const uint32_t *orig,
+                                     const double *r, int64_t n, int64_t n_total, int64_t n_max,
+                                     const long long *hist, double lam, const double *lam_dev,
+                                     void *tmp, int64_t n_ws, const int *skip, long long *pack,
+                                     int capd, hipStream_t s);
+hipError_t launch_select_dist_final(const long long *packs, int world, int capd, int64_t n_total,
+                                    double lam, const double *lam_dev, void *tmp, int64_t n_ws,
+                                    IterState *st, const int *skip, const LoopCtl *loop,
+                                    int *host_flag, hipStream_t s);
 hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hipStream_t s);
+// apply T while !*skip and *apply_flag (device flags of the loop state)
+hipError_t launch_apply_xy_flags(double *x, double *y, int64_t n, const double *T, const int *skip,
+                                 const int *apply_flag, hipStream_t s);
 hipError_t launch_sum_sq_diff(const double *sx, const double *sy, const double *sz,
                               const double *cx, const double *cy, const double *cz, int64_t k,
                               int md, void *tmp, double *out, hipStream_t s);

@@ -1390,6 +1390,14 @@ hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, dou
     return hipGetLastError();
 }
 
+hipError_t launch_apply_xy_flags(double *x, double *y, int64_t n, const double *T, const int *skip,
+                                const int *apply_flag, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_apply_inplace, dim3(nblk(n)), dim3(256), 0, s, x, y, n, T, skip,
+                       apply_flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_apply_xy(double *x, double *y, int64_t n, const double *T, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_apply_inplace, dim3(nblk(n)), dim3(256), 0, s, x, y, n, T,

@@ -89,6 +89,7 @@ constexpr int GI = FICP_GI;  // gather: rows per thread (~1 block per CU at 1M r
 
 // error bits of SelCtl::err (sticky; the host checks them after a run)
 constexpr unsigned ERR_EMPTY = 1u;  // candidate set empty (cannot happen with finite r)
+constexpr unsigned ERR_CAP = 2u;    // distributed run: a rank's candidates exceeded the capacity
 
 constexpr int NL = 2048, NF = 4096, NF_LOG = 12, NC_LOG = 11;
 static_assert(NL + NF + NL == NB, "bucket map regions");
@@ -671,8 +672,13 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
 #endif
 constexpr int RG = FICP_SEL_RG;
 constexpr int RBPB = 1024 / RG;  // buckets per workgroup
+// the bucket's bracket and the 16-bucket chunk totals from its integer count and sum
+// (lanes of one wave hold 64 consecutive buckets)
+__device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsigned c, u64 f,
+                                            const HistPack &hp);
+
 __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int *skip,
-                                                     HistPack hp) {
+                                                     HistPack hp, long long *iout) {
     if (skip && *skip) return;
     __shared__ unsigned s_c[RG][RBPB];
     __shared__ u64 s_f[RG][RBPB];
@@ -707,6 +713,16 @@ __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int
         c += s_c[h][bl];
         f += s_f[h][bl];
     }
+    if (iout) {  // distributed run: this rank's integer totals, summed over ranks outside
+        iout[b] = (long long)c;
+        iout[NB + b] = (long long)f;
+        return;
+    }
+    reduce_tail(w, b, bl, c, f, hp);
+}
+
+__device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsigned c, u64 f,
+                                            const HistPack &hp) {
     // the bucket's sum bracketed by the truncated fixed-point sum (each row loses < 1
     // unit): f * 2^(e - fixb) <= sum < (f + c) * 2^(e - fixb); computed here, one bucket
     // per thread, instead of 16 per thread in the one-workgroup bounds kernel
@@ -1853,9 +1869,119 @@ __global__ void k_sel_read_stats(SelWS w, unsigned *out) {
     }
 }
 
+// ---- distributed selection (source rows split over ranks) -------
+// Every rank holds the NN results of its own rows.  The histogram's integer totals are
+// summed over the ranks (exact, order-free), so every rank derives the same bounds and
+// candidate buckets; each rank packs its candidates and the sum of its rows below them,
+// the ranks' packs are gathered, and every rank runs the same final selection on the
+// concatenation (the S_base parts added in rank order: identical k everywhere).
+// Pack layout (int64 words): [0] count, [1] S_base bits, [2] overflow, [3] 0,
+// then capd keys, capd caller indices, capd r bits.
+
+// bracket + chunk totals from the ranks' summed integer histogram (64 buckets per block)
+__global__ __launch_bounds__(64) void k_sel_finish(SelWS w, const long long *hist,
+                                                   const int *skip, HistPack hp) {
+    if (skip && *skip) return;
+    const int bl = threadIdx.x, b = blockIdx.x * 64 + bl;
+    reduce_tail(w, b, bl, (unsigned)hist[b], (u64)hist[NB + b], hp);
+}
+
+__global__ __launch_bounds__(HT) void k_sel_pack(SelWS w, int nparts, const int *skip,
+                                                 long long *out, int capd) {
+    if (skip && *skip) return;
+    __shared__ Scr scr;
+    const unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    double a = 0.0;
+    for (int p = threadIdx.x; p < nparts; p += HT) a = a + w.parts[p];  // fixed order per thread
+    const double sb = blk_sum(a, scr);
+    const unsigned cc = min(c, (unsigned)capd);
+    if (threadIdx.x == 0) {
+        out[0] = (long long)cc;
+        out[1] = __double_as_longlong(sb);
+        out[2] = c > (unsigned)capd ? 1 : 0;
+        out[3] = 0;
+    }
+    for (unsigned j = threadIdx.x; j < cc; j += HT) {
+        out[4 + j] = (long long)w.ka[j];
+        out[4 + capd + j] = (long long)w.oa[j];
+        out[4 + 2 * (int64_t)capd + j] = __double_as_longlong(w.ra[j]);
+    }
+}
+
+__global__ __launch_bounds__(HT) void k_sel_unpack(SelWS w, const long long *all, int world,
+                                                   int capd, const int *skip) {
+    if (skip && *skip) return;
+    const int64_t stride = 4 + 3 * (int64_t)capd;
+    unsigned base = 0, over = 0;
+    for (int q = 0; q < world; ++q) {
+        const long long *pk = all + q * stride;
+        const unsigned cq = (unsigned)pk[0];
+        for (unsigned j = threadIdx.x; j < cq; j += HT) {
+            w.ka[base + j] = (u64)pk[4 + j];
+            w.oa[base + j] = (uint32_t)pk[4 + capd + j];
+            w.ra[base + j] = __longlong_as_double(pk[4 + 2 * (int64_t)capd + j]);
+            w.pa[base + j] = 0u;
+        }
+        if (threadIdx.x == 0) w.parts[q] = __longlong_as_double(pk[1]);
+        over |= (unsigned)pk[2];
+        base += cq;
+    }
+    if (threadIdx.x == 0) {
+        __hip_atomic_exchange(&w.ctl->ccount, base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (over) __hip_atomic_fetch_or(&w.ctl->err, ERR_CAP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace
 
 int64_t sel_tmp_bytes(int64_t n) { return carve_bytes(n, nullptr, nullptr); }
+
+int sel_hist_words() { return 2 * NB; }
+
+hipError_t launch_select_dist_hist(const unsigned long long *key, const double *r, int64_t n,
+                                   int64_t n_max, const unsigned long long *range, void *tmp,
+                                   int64_t n_ws, const IterState *st, const int *skip,
+                                   long long *hist_out, hipStream_t s) {
+    const SelWS w = carve(tmp, n_ws);
+    const HistPack hp = hist_pack(n_max);
+    hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n_max)), dim3(HHT), 0, s, key, r, n,
+                       const_cast<unsigned long long *>(range), (int64_t)0, w, skip, hp, st);
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n_max), skip,
+                       hp, hist_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_dist_gather(const unsigned long long *key, const uint32_t *orig,
+                                     const double *r, int64_t n, int64_t n_total, int64_t n_max,
+                                     const long long *hist, double lam, const double *lam_dev,
+                                     void *tmp, int64_t n_ws, const int *skip, long long *pack,
+                                     int capd, hipStream_t s) {
+    const SelWS w = carve(tmp, n_ws);
+    const HistPack hp = hist_pack(n_max);
+    hipLaunchKernelGGL(k_sel_finish, dim3(NB / 64), dim3(64), 0, s, w, hist, skip, hp);
+    hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n_total, lam, lam_dev, skip,
+                       hp.fixb);
+    const int gb = gather_blocks(n);
+    if (n > 0)
+        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip,
+                           FitSrc{});
+    hipLaunchKernelGGL(k_sel_pack, dim3(1), dim3(HT), 0, s, w, n > 0 ? gb : 0, skip, pack, capd);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_dist_final(const long long *packs, int world, int capd, int64_t n_total,
+                                    double lam, const double *lam_dev, void *tmp, int64_t n_ws,
+                                    IterState *st, const int *skip, const LoopCtl *loop,
+                                    int *host_flag, hipStream_t s) {
+    const SelWS w = carve(tmp, n_ws);
+    hipLaunchKernelGGL(k_sel_unpack, dim3(1), dim3(HT), 0, s, w, packs, world, capd, skip);
+    LoopCtl lc{};
+    if (loop) lc = *loop;
+    hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, world, n_total, lam, lam_dev, st,
+                       skip, lc, loop ? 1 : 0, host_flag, FitSrc{});
+    return hipGetLastError();
+}
 
 hipError_t launch_select_init(void *tmp, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(1024), 0, s, carve(tmp, n));
@@ -1876,7 +2002,8 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     const HistPack hp = hist_pack(n);
     hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
                        range_parts, w, skip, hp, (const IterState *)st);
-    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip, hp);
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip, hp,
+                       (long long *)nullptr);
     hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip, hp.fixb);
     const int gb = gather_blocks(n);
     FitSrc fs{};

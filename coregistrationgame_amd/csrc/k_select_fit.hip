@@ -266,11 +266,12 @@ __device__ __forceinline__ bool fit_threshold(const FitIn &a, unsigned long long
 // per block (MI355X_MICROARCH.md hand-off table, first row); the last block resets the
 // counter (atomic exchange) for the next launch.
 __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow_refl,
-                           IterState *st, double *s);
+                           IterState *st, double *s, double *out8);
 
+// out8 (distributed runs): the last block stores the 8 sums there instead of solving
 __global__ __launch_bounds__(FIT_B) void k_fit_sums(FitIn a, double *part, unsigned *ctr,
                                                  int allow_refl, IterState *st,
-                                                 const int *skip) {
+                                                 const int *skip, double *out8) {
     if (skip && *skip) return;
     __shared__ double s[256];
     __shared__ int s_last;
@@ -352,11 +353,11 @@ __global__ __launch_bounds__(FIT_B) void k_fit_sums(FitIn a, double *part, unsig
     }
     __syncthreads();
     if (!s_last) return;
-    fit_finish(a, part, (int)gridDim.x, allow_refl, st, s);
+    fit_finish(a, part, (int)gridDim.x, allow_refl, st, s, out8);
 }
 
 __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow_refl,
-                           IterState *st, double *s) {
+                           IterState *st, double *s, double *out8) {
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int b = threadIdx.x; b < nb; b += FIT_B) {  // fixed order per thread
         double v[8];
@@ -381,6 +382,10 @@ __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow
         double t = s[e];
         for (int w = 1; w < FIT_W; ++w) t = t + s[8 * w + e];
         c[e] = t;
+    }
+    if (out8) {
+        for (int e = 0; e < 8; ++e) out8[e] = c[e];
+        return;
     }
     const double k = a.key ? (double)a.st->k : (double)a.n;
     fit_solve(c, k, a.px, a.py, allow_refl, st);
@@ -476,7 +481,35 @@ hipError_t launch_fit(const FitIn &a, int allow_reflection, void *tmp, IterState
     unsigned *ctr = (unsigned *)tmp;
     double *part = (double *)((char *)tmp + FIT_PART);
     hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FIT_B), 0, s, a, part, ctr, allow_reflection, st,
-                       skip);
+                       skip, (double *)nullptr);
+    return hipGetLastError();
+}
+
+// distributed runs: this rank's 8 fit sums (k_fit_sums without the solve), then, once the
+// caller has gathered every rank's sums, the solve on their sum in rank order
+hipError_t launch_fit_sums(const FitIn &a, void *tmp, const int *skip, double *out8,
+                           hipStream_t s) {
+    const int nb = (int)std::max<int64_t>(1, (a.n + FIT_TILE - 1) / FIT_TILE);
+    unsigned *ctr = (unsigned *)tmp;
+    double *part = (double *)((char *)tmp + FIT_PART);
+    hipLaunchKernelGGL(k_fit_sums, dim3(nb), dim3(FIT_B), 0, s, a, part, ctr, 0,
+                       const_cast<IterState *>(a.st), skip, out8);
+    return hipGetLastError();
+}
+
+__global__ void k_fit_solve_ranks(const double *sums, int world, double px, double py,
+                                  int allow_refl, IterState *st, const int *skip) {
+    if ((skip && *skip) || threadIdx.x != 0) return;
+    double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int q = 0; q < world; ++q)
+        for (int e = 0; e < 8; ++e) c[e] = c[e] + sums[8 * q + e];
+    fit_solve(c, (double)st->k, px, py, allow_refl, st);
+}
+
+hipError_t launch_fit_solve_ranks(const double *sums, int world, double px, double py,
+                                  int allow_refl, IterState *st, const int *skip, hipStream_t s) {
+    hipLaunchKernelGGL(k_fit_solve_ranks, dim3(1), dim3(64), 0, s, sums, world, px, py, allow_refl,
+                       st, skip);
     return hipGetLastError();
 }
 

@@ -178,6 +178,42 @@ int ficp_select_fit_device(ficp_ctx *ctx, const double *x, const double *y, int6
 /* apply_transform_2d_xy_only (ficp.py:112-119) in place on device-resident XY. */
 int ficp_apply_device(ficp_ctx *ctx, double *x, double *y, int64_t n, const double T[9]);
 
+/* --- distributed run of one plot, stream-ordered (C5) --------------------- */
+/* The whole of ficp.py:149-154 for one plot split over ranks, with every step enqueued on
+   the context's stream; the caller runs its collectives (RCCL via torch.distributed) on the
+   same stream, so no step waits for the host.  Per iteration (one NN call) the host
+   enqueues the steps below and then waits for the previous iteration's done flag
+   (ficp_dist_wait); iterations enqueued past the end are no-ops.  Device pointers.
+   mode 1, target-partitioned: every rank holds all n rows and a shard of the layer:
+     fit_sums -> fit_solve(world 1; applies T) -> nn_shard per shard -> caller: MIN merge
+     of (d2, idx) as for ficp_nn_device -> select_merged.
+   mode 2, source-partitioned: every rank holds the whole layer and rows [row0, row0 +
+   n_local) of n_total: fit_sums -> caller: all-gather (8 f64 per rank) -> fit_solve ->
+   nn_local -> caller: MAX all-reduce of range2 (2 int64) -> hist -> caller: SUM
+   all-reduce of hist (ficp_dist_hist_words() int64) -> candidates -> caller: all-gather
+   of the packs (4 + 3 capd int64 per rank) -> final.  Every rank derives the same k,
+   threshold and T from the exact integer histogram and the rank-ordered sums. */
+int ficp_set_stream(ficp_ctx *ctx, void *hip_stream);  /* NULL: the context's own stream */
+int ficp_dist_begin(ficp_ctx *ctx, int32_t mode, double *x, double *y, const double *z,
+                    int64_t n_local, int64_t n_total, int64_t n_max, int64_t row0,
+                    int32_t nstages, const double *lambdas, double threshold,
+                    int32_t max_iterations, int32_t allow_reflection, double pivot_x,
+                    double pivot_y, int32_t world, int32_t capd);
+int ficp_dist_fit_sums(ficp_ctx *ctx, double *sums8);
+int ficp_dist_fit_solve(ficp_ctx *ctx, const double *sums, int32_t world);
+int ficp_dist_nn_shard(ficp_ctx *shard, ficp_ctx *ctrl, int64_t idx_offset, double *d2,
+                       int32_t *idx);
+int ficp_dist_select_merged(ficp_ctx *ctx, const double *d2, const int32_t *idx,
+                            const double *tx, const double *ty, int64_t iteration);
+int ficp_dist_nn_local(ficp_ctx *ctx, int64_t *range2);
+int ficp_dist_hist_words(void);
+int ficp_dist_hist(ficp_ctx *ctx, const int64_t *range2, int64_t *hist);
+int ficp_dist_candidates(ficp_ctx *ctx, const int64_t *hist, int64_t *pack, int32_t capd);
+int ficp_dist_final(ficp_ctx *ctx, const int64_t *packs, int32_t world, int32_t capd,
+                    int64_t iteration);
+int ficp_dist_wait(ficp_ctx *ctx, int64_t iteration, int32_t *done);
+int ficp_dist_end(ficp_ctx *ctx, ficp_stats *stats);
+
 /* --- device memory helpers (for callers without their own allocator) ---- */
 int ficp_dev_alloc(ficp_ctx *ctx, int64_t bytes, void **ptr);
 int ficp_dev_free(ficp_ctx *ctx, void *ptr);

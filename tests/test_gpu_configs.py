@@ -124,6 +124,16 @@ def test_c5_8M_partitioned_vs_oracle_and_single(oracle):
     np.testing.assert_allclose(out[:, :2], single[:, :2], atol=1e-6, rtol=0)
     np.testing.assert_array_equal(bits(out[:, 2]), bits(p.source[:, 2]))
     assert part.lambda_val == 0.95
+    del out
+    # the source-partitioned mode (tree rows split 8 ways, the layer replicated)
+    spart = PartitionedFICP(p.source, p.target, threshold=float("-inf"), max_iterations=10, local_shards=8,
+                            mode="source")
+    sout = spart.run()
+    assert spart.last_stats["n_nn_calls"] == 22
+    np.testing.assert_array_equal(np.array(spart.last_stats["k"]), icp.last_stats["k"])
+    np.testing.assert_allclose(sout[:, :2], single[:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(bits(sout[:, 2]), bits(p.source[:, 2]))
+    del sout, spart
     # the unsplit run's trajectory vs the oracle's: k of every pinned call (at 8M rows some
     # calls are rounding-level FRMSD ties, conftest.K_GAP_PIN_LARGE; measured: call 6 has a
     # 3e-14 gap and lands one k apart, the trajectory rejoins at the next call), final XY

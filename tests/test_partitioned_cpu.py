@@ -99,3 +99,68 @@ def test_merge_shards_gloo():
         im = np.frombuffer(got[r][1], np.int32)
         np.testing.assert_array_equal(dm[1:], dmin[1:])
         np.testing.assert_array_equal(im, exp_i)
+
+
+# ------------------------------------------------ source-partitioned exchanges (mode "source")
+def _src_case(ranks, seed):
+    """Per-rank exchange records: key range words (int64, flipped top bit), integer
+    histogram totals, 8 fit sums and a candidate pack."""
+    rng = np.random.default_rng(seed)
+    ranges = [rng.integers(-2**62, 2**62, 2) for _ in range(ranks)]
+    hists = [rng.integers(0, 2**40, 16) for _ in range(ranks)]
+    sums = [rng.normal(0, 1e3, 8) for _ in range(ranks)]
+    packs = [rng.integers(-2**60, 2**60, 10) for _ in range(ranks)]
+    return ranges, hists, sums, packs
+
+
+def test_source_merges_local():
+    from coregistrationgame_amd.partitioned import gather_ranked, merge_hist, merge_range
+    ranges, hists, sums, packs = _src_case(5, 3)
+    T = torch.from_numpy
+    np.testing.assert_array_equal(merge_range([T(r) for r in ranges]).numpy(), np.max(ranges, axis=0))
+    np.testing.assert_array_equal(merge_hist([T(h) for h in hists]).numpy(), np.sum(hists, axis=0))
+    np.testing.assert_array_equal(gather_ranked([T(s) for s in sums]).numpy(), np.stack(sums))
+    np.testing.assert_array_equal(gather_ranked([T(p) for p in packs]).numpy(), np.stack(packs))
+
+
+def _source_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from coregistrationgame_amd.partitioned import gather_ranked, merge_hist, merge_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ranges, hists, sums, packs = _src_case(2 * world, 11)
+        mine = slice(2 * rank, 2 * rank + 2)  # this process holds ranks 2r and 2r+1
+        T = torch.from_numpy
+        r = merge_range([T(x) for x in ranges[mine]], world=world)
+        h = merge_hist([T(x) for x in hists[mine]], world=world)
+        s = gather_ranked([T(x) for x in sums[mine]], world=world)
+        p = gather_ranked([T(x) for x in packs[mine]], world=world)
+        q.put((rank, r.numpy().tobytes(), h.numpy().tobytes(), s.numpy().tobytes(), p.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_source_merges_gloo():
+    """The source mode's exchanges over gloo, world size 2 with two ranks per process: the
+    range MAX, the exact integer histogram SUM, and the rank-ordered gathers of the fit
+    sums and candidate packs are identical on every process."""
+    world = 2
+    ranges, hists, sums, packs = _src_case(2 * world, 11)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_source_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {g[0]: g[1:] for g in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        rb, hb, sb, pb = got[r]
+        np.testing.assert_array_equal(np.frombuffer(rb, np.int64), np.max(ranges, axis=0))
+        np.testing.assert_array_equal(np.frombuffer(hb, np.int64), np.sum(hists, axis=0))
+        np.testing.assert_array_equal(np.frombuffer(sb, np.float64).reshape(-1, 8), np.stack(sums))
+        np.testing.assert_array_equal(np.frombuffer(pb, np.int64).reshape(-1, 10), np.stack(packs))

@@ -41,7 +41,7 @@ def main(tag, prefix="r1"):
                    "active_dispatches": len(act), "active_avg_us": sum(act) / len(act),
                    "median_us": med}
     (dst / f"{prefix}_c3_trace_summary.json").write_text(json.dumps(summ, indent=1))
-    tl = subprocess.run([sys.executable, str(REPO / "tools" / "timeline.py"), str(trace)],
+    tl = subprocess.run([sys.executable, str(REPO / "tools" / "timeline.py"), str(trace)],  # FICP_TL_RUN picks the run
                         capture_output=True, text=True, check=True).stdout
     (dst / f"{prefix}_c3_timeline.txt").write_text(tl)
     pmc = json.loads((REPO / "gpurun_out" / tag / "pmc" / "summary.json").read_text())

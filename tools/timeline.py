@@ -11,7 +11,10 @@ marker = sys.argv[2] if len(sys.argv) > 2 else "k_minmax2_partial"
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
-a, b = starts[-2], starts[-1]
+# the run to show: FICP_TL_RUN (default -1, the last complete one; the default bench
+# command ends with the drop-in host-path runs, whose first NN calls are cold)
+ri = int(__import__("os").environ.get("FICP_TL_RUN", "-1"))
+a, b = starts[ri - 1], starts[ri]
 run = rows[a:b]
 t0 = int(run[0]["Start_Timestamp"])
 prev_end = t0

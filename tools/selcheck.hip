@@ -151,7 +151,7 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, 0, dkey, dr, n, drange,
                            (int64_t)0, w, (const int *)nullptr, hist_pack(n), (const IterState *)st);
         hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, 0, w, hist_blocks(n),
-                           (const int *)nullptr, hist_pack(n));
+                           (const int *)nullptr, hist_pack(n), (long long *)nullptr);
         CK(hipEventRecord(ev[1], 0));
         hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam, (const double *)nullptr,
                            (const int *)nullptr, hist_pack(n).fixb);

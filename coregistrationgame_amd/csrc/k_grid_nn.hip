@@ -783,8 +783,19 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
     finish(a, S, i, qz, b, kmin_c, kmax);
 }
 
+// 7 waves per SIMD: without the hint the kernel's 106 SGPRs allow 6 (MI355X_MICROARCH.md
+// residency rule); with it the compiler keeps 94 (40 spilled to VGPR lanes, 71 VGPRs):
+// NN 43.4 -> 42.3 us per C3 call.  8 spills VGPRs to scratch (44 us).
+#ifndef FICP_NN_WPE
+#define FICP_NN_WPE 7
+#endif
+#if FICP_NN_WPE > 0
+#define NN_WPE __attribute__((amdgpu_waves_per_eu(FICP_NN_WPE, FICP_NN_WPE)))
+#else
+#define NN_WPE
+#endif
 template <int MD, bool APPLY>
-__global__ __launch_bounds__(256) void k_nn_grid(NNArgs a, GridView g) {
+__global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
     if ((a.skip && *a.skip) || (a.reuse && *a.reuse)) return;
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     unsigned long long kmin_c = 0, kmax = 0;
@@ -864,8 +875,16 @@ __device__ __forceinline__ GridView plot_view(const PlotGrid &pg, const TPt *pts
 // uncertified queries are then packed onto its first lanes, GS lanes per query when
 // few remain, each scanning with its own plot's grid (a workgroup may straddle plots).
 // The cold call runs the plain scan and stores G = 0.  Converged plots are skipped.
+#ifndef FICP_NNB_WPE
+#define FICP_NNB_WPE 6  // 84 -> 80 VGPRs, 5 -> 6 waves per SIMD: batch NN 375 -> 367 us per launch
+#endif
+#if FICP_NNB_WPE > 0
+#define NNB_WPE __attribute__((amdgpu_waves_per_eu(FICP_NNB_WPE, FICP_NNB_WPE)))
+#else
+#define NNB_WPE
+#endif
 template <int MD>
-__global__ __launch_bounds__(256) void k_nn_grid_batch(NNArgs a, const int32_t *__restrict__ plot_of,
+__global__ __launch_bounds__(256) NNB_WPE void k_nn_grid_batch(NNArgs a, const int32_t *__restrict__ plot_of,
                                                        const PlotGrid *__restrict__ grids,
                                                        const TPt *__restrict__ pts, int64_t m,
                                                        const int32_t *__restrict__ cell_start,

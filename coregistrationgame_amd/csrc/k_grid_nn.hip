@@ -175,15 +175,17 @@ __device__ __forceinline__ void disk_scan(const GridView &g, const Stems &S, dou
 // FICP_NN_UNROLL loads in flight.  The row-by-row walk made every row's loads wait for
 // the previous row's stems (about 8 dependent memory latencies per query at C3; batched:
 // 4).  Rows at offset >= 2 follow row by row, as before.
+// sa <= sb: the columns [sa, sb] of these three rows were evaluated already (the cold
+// start's 3x3 block): each row's chord is split around them, so no stem is evaluated twice
 template <int MD>
 __device__ __forceinline__ void disk_scan_batched(const GridView &g, const Stems &S, double qx,
                                                   double qy, double qz, int cy, double mq,
-                                                  Best &b) {
-    int p0[3], len[3];
+                                                  Best &b, int sa = 1, int sb = 0) {
+    int p0[6], len[6];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        p0[r] = 0;
-        len[r] = 0;
+        p0[2 * r] = p0[2 * r + 1] = 0;
+        len[2 * r] = len[2 * r + 1] = 0;
         const int yy = cy + r - 1;
         if (yy < 0 || yy >= g.gy) continue;
         const double gy = band_gap(qy, g.y0, g.h, yy, yy + 1, mq);
@@ -193,15 +195,30 @@ __device__ __forceinline__ void disk_scan_batched(const GridView &g, const Stems
         const int xl = cell_coord(qx - w, g.x0, g.inv_h, g.gx);
         const int xh = cell_coord(qx + w, g.x0, g.inv_h, g.gx);
         const int32_t *row = g.cell_start + (int64_t)yy * g.gx;
-        p0[r] = row[xl];
-        len[r] = row[xh + 1] - p0[r];
+        // [xl, xh] minus [sa, sb]: [xl, min(xh, sa - 1)] and [max(xl, sb + 1), xh]
+        const int a1 = sa <= sb ? min(xh, sa - 1) : xh;
+        const int a2 = sa <= sb ? max(xl, sb + 1) : xh + 1;
+        if (a1 >= xl) {
+            p0[2 * r] = row[xl];
+            len[2 * r] = row[a1 + 1] - p0[2 * r];
+        }
+        if (a2 <= xh) {
+            p0[2 * r + 1] = row[a2];
+            len[2 * r + 1] = row[xh + 1] - p0[2 * r + 1];
+        }
     }
-    const int l01 = len[0] + len[1], tot = l01 + len[2];
+    int tot = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) tot += len[r];
     for (int t = 0; t < tot; t += FICP_NN_UNROLL) {
 #pragma unroll
         for (int u = 0; u < FICP_NN_UNROLL; ++u) {
-            const int q = min(t + u, tot - 1);
-            const int slot = q < len[0] ? p0[0] + q : (q < l01 ? p0[1] + (q - len[0]) : p0[2] + (q - l01));
+            int q = min(t + u, tot - 1), slot = 0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {  // the segment holding position q
+                if (q >= 0 && q < len[r]) slot = p0[r] + q;
+                q -= len[r];
+            }
             eval_slot<MD>(S, slot, qx, qy, qz, b);
         }
     }
@@ -237,6 +254,7 @@ __device__ __forceinline__ void grid_nn(const GridView &g, const Stems &S, doubl
     const int cx = cell_coord(qx, g.x0, g.inv_h, g.gx);
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
     const double mq = query_margin(g, qx, qy);
+    int sa = 1, sb = 0;  // columns of rows cy-1..cy+1 evaluated by the cold start
     if (!(b.d2 < INFINITY)) {
         // cold start (no previous match): the 3x3 cells around q as one batch -- a bound
         // near the true distance (the own cell's stem alone was often 5-13 m away in 3-D,
@@ -262,6 +280,8 @@ __device__ __forceinline__ void grid_nn(const GridView &g, const Stems &S, doubl
                 eval_slot<MD>(S, slot, qx, qy, qz, b);
             }
         }
+        sa = xa;
+        sb = xb;
         for (int r = 2; !(b.d2 < INFINITY); ++r) {  // empty 3x3 block: grow square rings
             const int xa = cx - r, xb = cx + r, ya = cy - r, yb = cy + r;
             if (xa < 0 && ya < 0 && xb >= g.gx && yb >= g.gy) break;  // empty layer
@@ -278,7 +298,7 @@ __device__ __forceinline__ void grid_nn(const GridView &g, const Stems &S, doubl
         }
         if (!(b.d2 < INFINITY)) return;
     }
-    if (FICP_NN_BATCHED) disk_scan_batched<MD>(g, S, qx, qy, qz, cy, mq, b);
+    if (FICP_NN_BATCHED) disk_scan_batched<MD>(g, S, qx, qy, qz, cy, mq, b, sa, sb);
     else disk_scan<MD>(g, S, qx, qy, qz, cy, mq, b);
 }
 

@@ -26,7 +26,7 @@
 
 struct BatchBufs {
     DevBuf so, to, plot_of, tplot, grids, st, bb, lams;
-    DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp;
+    DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp, bs_tmp;
     DevBuf key, gap, r, ccx, ccy, bp, dz2, wkey, skey, wrow, srow, wr, sr;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
     int *h_flag = nullptr;                 // coherent pinned ring: plots still running
@@ -41,7 +41,7 @@ void batch_release(BatchBufs *b) {
                       &b->r,        &b->ccx,     &b->ccy,      &b->wkey,  &b->skey,  &b->wrow,
                       &b->srow,     &b->wr,      &b->sr,       &b->sx,    &b->sy,    &b->sz,
                       &b->tx,       &b->ty,      &b->tz,       &b->stage, &b->bp,
-                      &b->dz2};
+                      &b->dz2,      &b->bs_tmp};
     for (DevBuf *d : bufs) d->release();
     if (b->h_flag) (void)hipHostFree(b->h_flag);
     delete b;
@@ -108,13 +108,28 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
     HIPCHK(hipMemcpyAsync(b.grids.p, grids.data(), (size_t)nplots * sizeof(PlotGrid),
                           hipMemcpyHostToDevice, c->stream));
     CHK(b.tplot.ensure(m * 4));
+    CHK(b.cell_start.ensure((ncells + 1) * 4));
+    CHK(b.pts.ensure(m * sizeof(TPt)));
+    HIPCHK(launch_fill_plot_ids(b.to.as<int64_t>(), nplots, b.tplot.as<int32_t>(), c->stream));
+    if (bsort_supported(m, ncells) && !getenv("FICP_GRID_ATOMIC")) {
+        // the two-level bucket sort of the single-plot grid (k_bsort.hip) keyed by the
+        // global cell id of each stem's plot grid: 1.3 -> ~0.25 ms per 1024-plot batch
+        CHK(b.bs_tmp.ensure(bsort_tmp_bytes(m, ncells)));
+        BSortGeom bg{};
+        bg.mode = 2;
+        bg.plot = b.tplot.as<int32_t>();
+        bg.grids = b.grids.as<PlotGrid>();
+        BSortOut bo{};
+        bo.pts = b.pts.as<TPt>();
+        bo.cell_start = b.cell_start.as<int32_t>();
+        HIPCHK(launch_bsort(tx, ty, md == 3 ? tz : nullptr, m, bg, ncells, bo, b.bs_tmp.p, c->stream));
+        return FICP_OK;
+    }
+    // counting sort with global atomics (grids the bucket sort cannot plan)
     CHK(b.cell_of.ensure(m * 4));
     CHK(b.counts.ensure((ncells + 1) * 4));
     CHK(b.fill.ensure((ncells + 1) * 4));
-    CHK(b.cell_start.ensure((ncells + 1) * 4));
-    CHK(b.pts.ensure(m * sizeof(TPt)));
     CHK(b.scan_tmp.ensure(scan_tmp_elems(ncells) * 4 + 64));
-    HIPCHK(launch_fill_plot_ids(b.to.as<int64_t>(), nplots, b.tplot.as<int32_t>(), c->stream));
     HIPCHK(launch_atomic_zero32((uint32_t *)b.counts.p, ncells + 1, c->stream));
     HIPCHK(launch_atomic_zero32((uint32_t *)b.fill.p, ncells + 1, c->stream));
     HIPCHK(launch_batch_grid_count(tx, ty, m, b.tplot.as<int32_t>(), b.grids.as<PlotGrid>(),

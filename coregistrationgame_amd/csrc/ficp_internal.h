@@ -377,10 +377,13 @@ hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, dou
 // Two-level bucket sort of points by a grid key (k_bsort.hip).  mode 0: key = cell id
 // cy * gx + cx (grid layout: TPt records + cell_start); mode 1: 8x8-supertile order
 // (work order: SoA coordinates + caller index).  Order: (key, point index).
+struct PlotGrid;
 struct BSortGeom {
     double x0, y0, inv_h;
     int gx, gy;
-    int mode;
+    int mode;                // 2: many plots (C4): key = cell_base + cell of the point's plot
+    const int32_t *plot;     // mode 2: plot of each point
+    const PlotGrid *grids;   // mode 2: per-plot geometry
 };
 struct BSortPlan {
     int fs;         // fine bits (key & ((1 << fs) - 1))

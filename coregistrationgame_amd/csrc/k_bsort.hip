@@ -42,8 +42,16 @@ __device__ __forceinline__ int bs_coord(double v, double v0, double inv_h, int g
 }
 
 // key of a point: mode 0 = cell id cy * gx + cx (the grid layout); mode 1 = 8x8-supertile
-// order (supertile row-major, then the cell inside it row-major)
-__device__ __forceinline__ uint32_t bs_key(double x, double y, const BSortGeom &g) {
+// order (supertile row-major, then the cell inside it row-major); mode 2 = the global cell
+// id of the batch grids (the point's plot's cell_base + its cell in that plot's grid, as
+// k_batch_grid_count)
+__device__ __forceinline__ uint32_t bs_key(double x, double y, const BSortGeom &g, int64_t i) {
+    if (g.mode == 2) {
+        const PlotGrid &pg = g.grids[g.plot[i]];
+        const int cx = bs_coord(x, pg.x0, pg.inv_h, pg.gx);
+        const int cy = bs_coord(y, pg.y0, pg.inv_h, pg.gy);
+        return (uint32_t)(pg.cell_base + (long long)cy * pg.gx + cx);
+    }
     const int cx = bs_coord(x, g.x0, g.inv_h, g.gx);
     const int cy = bs_coord(y, g.y0, g.inv_h, g.gy);
     if (g.mode == 0) return (uint32_t)cy * (uint32_t)g.gx + (uint32_t)cx;
@@ -82,7 +90,8 @@ __global__ __launch_bounds__(BT) void k_bs_count(BSPair P) {
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (i + (int64_t)u * BT < i1) atomicAdd(&h[bs_key(xv[u], yv[u], g) >> p.fs], 1u);
+            if (i + (int64_t)u * BT < i1)
+                atomicAdd(&h[bs_key(xv[u], yv[u], g, i + (int64_t)u * BT) >> p.fs], 1u);
     }
     __syncthreads();
     uint32_t *c = counts + (int64_t)bid * p.nbk;
@@ -178,8 +187,9 @@ __global__ __launch_bounds__(BT) void k_bs_scatter(BSPair P) {
         uint32_t slot[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            slot[u] = (i + (int64_t)u * BT < i1) ? atomicAdd(&fill[bs_key(xv[u], yv[u], g) >> p.fs], 1u)
-                                                  : 0u;
+            slot[u] = (i + (int64_t)u * BT < i1)
+                          ? atomicAdd(&fill[bs_key(xv[u], yv[u], g, i + (int64_t)u * BT) >> p.fs], 1u)
+                          : 0u;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t q = i + (int64_t)u * BT;
@@ -243,7 +253,7 @@ __global__ __launch_bounds__(B4T) void k_bs_bucket(BSPair P) {
     for (uint32_t e = threadIdx.x; e < cnt; e += B4T) {
         const TPt t = rec[lo + e];
         if (small) lrec[e] = t;
-        atomicAdd(&fc[bs_key(t.x, t.y, g) & mask], 1u);
+        atomicAdd(&fc[bs_key(t.x, t.y, g, t.idx) & mask], 1u);
     }
     __syncthreads();
     // exclusive scan of the fine counts (nf <= BMAXF; PF per thread)
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(B4T) void k_bs_bucket(BSPair P) {
     if (small) {
         for (uint32_t e = threadIdx.x; e < cnt; e += B4T) {
             const TPt t = lrec[e];
-            const uint32_t f = bs_key(t.x, t.y, g) & mask;
+            const uint32_t f = bs_key(t.x, t.y, g, t.idx) & mask;
             const uint32_t s = fc[f] + atomicAdd(&ff[f], 1u);
             lcomp[s] = ((uint64_t)f << 32) | (uint64_t)(uint32_t)t.idx;
             lsrc[s] = (uint16_t)e;
@@ -298,7 +308,7 @@ __global__ __launch_bounds__(B4T) void k_bs_bucket(BSPair P) {
     } else {  // a bucket larger than the LDS tile: the same ordering through global scratch
         for (uint32_t e = threadIdx.x; e < cnt; e += B4T) {
             const TPt t = rec[lo + e];
-            const uint32_t f = bs_key(t.x, t.y, g) & mask;
+            const uint32_t f = bs_key(t.x, t.y, g, t.idx) & mask;
             const uint32_t s = fc[f] + atomicAdd(&ff[f], 1u);
             gcomp[lo + s] = ((uint64_t)f << 32) | (uint64_t)(uint32_t)t.idx;
             gpos[lo + s] = e;

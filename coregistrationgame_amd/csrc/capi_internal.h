@@ -228,8 +228,8 @@ inline int sync(ficp_ctx *c) {
 // margin = the search bounds' rounding allowance.
 inline void plan_grid(double x0, double x1, double y0, double y1, int64_t m, double &h,
                       int64_t &gx, int64_t &gy, double &margin) {
-    static const double kPerCell =
-        getenv("FICP_GRID_PER_CELL") ? atof(getenv("FICP_GRID_PER_CELL")) : 1.0;
+    const char *pc = getenv("FICP_GRID_PER_CELL");   // read per plan (tests switch it)
+    const double kPerCell = pc && atof(pc) > 0.0 ? atof(pc) : 1.0;
     const double sxr = x1 - x0, syr = y1 - y0;
     if (m <= 1 || (sxr <= 0.0 && syr <= 0.0)) h = 1.0;
     else if (sxr > 0.0 && syr > 0.0) h = sqrt(sxr * syr * kPerCell / (double)m);

@@ -129,13 +129,24 @@ __global__ void k_batch_init(const int64_t *so, const int64_t *to, int nplots, i
 //     minimum (strict <, ascending k).
 // The bucket sums only feed the bounds (kMarg covers their rounding); every FRMSD value
 // compared comes from the deterministic S_base + window prefix sums.
-constexpr int ST = 512;          // threads
+#ifndef FICP_BSEL_ST
+#define FICP_BSEL_ST 512
+#endif
+#ifndef FICP_BSEL_RCACHE
+#define FICP_BSEL_RCACHE 1  // r kept in registers too (0: re-read from L2 in its two passes)
+#endif
+constexpr bool BSEL_RCACHE = FICP_BSEL_RCACHE;
+#ifndef FICP_BSEL_RPT
+#define FICP_BSEL_RPT 32
+#endif
+constexpr int ST = FICP_BSEL_ST; // threads
 constexpr int SWV = ST / 64;
 constexpr int SB = 2048;         // buckets
 constexpr int SB_LOG = 11;
 constexpr int SPER = SB / ST;    // buckets per thread in the scans
-constexpr int RPT = 32;          // rows per thread kept in registers (plots <= 16384 rows)
+constexpr int RPT = FICP_BSEL_RPT;  // rows per thread kept in registers (plots <= ST * RPT rows)
 constexpr int SRP = 4;           // window rows per thread per scan chunk
+constexpr int BMAXACT = ST / SPER;  // active bound chunks evaluated one bucket per lane
 
 typedef unsigned long long u64;
 
@@ -315,7 +326,7 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed &r) {
         _Pragma("unroll") for (int q = 0; q < RPT; ++q) {                           \
             const int64_t i = b + t + (int64_t)q * ST;                              \
             const u64 kk = kc[q];                                                   \
-            const double rv = rc[q];                                                \
+            const double rv = BSEL_RCACHE ? rc[q] : (i < e ? r[i] : INFINITY);       \
             (void)i;                                                                \
             BODY                                                                    \
         }                                                                           \
@@ -328,8 +339,18 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed &r) {
         }                                                                           \
     }
 
+#ifdef FICP_BSEL_PROF
+#define BSEL_T(i) bt_[i] = wall_clock64()
+#else
+#define BSEL_T(i)
+#endif
+#if defined(FICP_BSEL_WPE) && FICP_BSEL_WPE > 0
+#define BSEL_WPE __attribute__((amdgpu_waves_per_eu(FICP_BSEL_WPE, FICP_BSEL_WPE)))
+#else
+#define BSEL_WPE
+#endif
 template <bool CACHED>
-__global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key,
+__global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restrict__ key,
                                                      const double *__restrict__ r,
                                                      const int64_t *__restrict__ so,
                                                      const double *__restrict__ lams,
@@ -339,23 +360,31 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
     __shared__ double s_sum[SB];    // sums, then per-bucket fill counters (as unsigned)
     __shared__ SelRed red;
     __shared__ long long s_k[2];
+    __shared__ int s_act[BMAXACT];               // active chunks (thread ids)
+    __shared__ int s_nact;
+    __shared__ long long s_eC[BMAXACT * SPER];   // rows before each of their buckets
+    __shared__ double s_eP[BMAXACT * SPER];      // sum of r before it
     const int p = blockIdx.x;
     const int t = threadIdx.x;
     if (st[p].phase == PH_DONE) return;  // uniform per workgroup
+#ifdef FICP_BSEL_PROF
+    long long bt_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     const double lam = lams[st[p].stage];
     const double pe = 2.0 * lam + 1.0;
     const int64_t b = so[p], e = so[p + 1];
     const long long N = e - b;
     u64 kc[CACHED ? RPT : 1];
-    double rc[CACHED ? RPT : 1];
+    double rc[CACHED && BSEL_RCACHE ? RPT : 1];
     if (CACHED) {
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
             const int64_t i = b + t + (int64_t)q * ST;
             kc[q] = i < e ? key[i] : ~0ULL;
-            rc[q] = i < e ? r[i] : INFINITY;
+            if (BSEL_RCACHE) rc[q] = i < e ? r[i] : INFINITY;
         }
     }
+    BSEL_T(0);
     // 1. key range of the finite rows
     u64 amin = 0, kmax = 0;
     unsigned nfin = 0;
@@ -376,12 +405,14 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
     const u64 kmin = ~amin;
     const int nb = fb::bits_of(kmax - kmin);
     const int sh = nb > SB_LOG ? nb - SB_LOG : 0;
+    BSEL_T(1);
     // 2. histogram
 #pragma unroll
     for (int j = 0; j < SPER; ++j) {
         s_cnt[t * SPER + j] = 0u;
         s_sum[t * SPER + j] = 0.0;
     }
+    if (t == 0) s_nact = 0;
     __syncthreads();
     SEL_ROWS(if (rv < INFINITY) {
         const int bk = (int)((kk - kmin) >> sh);
@@ -389,6 +420,7 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
         atomicAdd(&s_sum[bk], rv);
     })
     __syncthreads();
+    BSEL_T(2);
     // 3. bounds over the buckets (thread t owns buckets t*SPER .. t*SPER + SPER - 1)
     unsigned c[SPER];
     double sm[SPER];
@@ -404,39 +436,95 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
     unsigned Cex = tc;
     double Pex = ts;
     blk_excl_scan2(Cex, Pex, red);
-    double U = INFINITY;
-    {
-        long long C = Cex;
-        double P = Pex;
+    BSEL_T(8);
+    // coarse to fine (as k_select.hip k_sel_bounds): U1 = the bound at each thread's chunk
+    // end; a chunk whose lower bound (its rows are all >= its first bucket's lo_r) exceeds
+    // U1 holds neither the minimising bucket end nor a candidate bucket, so only the few
+    // chunks near the minimum evaluate their buckets (every thread evaluating its 4
+    // buckets twice was ~40 % of the workgroup's time: 24 fp64 log2 per thread)
+    double U1 = tc ? fb::h_of((long long)Cex + tc, Pex + ts, pe) + fb::kMarg : INFINITY;
+    U1 = blk_min_d(U1, red);
+    BSEL_T(9);
+    // (the extra 1e-9 covers the different rounding of the chunk's and its buckets' sums)
+    const bool active = tc && (!(fb::block_lb(Cex, tc, Pex, fb::lo_r(kmin + ((u64)(t * SPER) << sh)), pe) -
+                                     1e-9 > U1) ||
+                               !(pe >= 1.0));
+    // the active chunks' buckets, one per lane: a chunk walked by its own thread chained
+    // ~24 dependent fp64 log2 (8 us per plot at C4); per-lane they take two rounds
+    if (active) {
+        const int a = atomicAdd(&s_nact, 1);
+        if (a < BMAXACT) {
+            s_act[a] = t;
+            long long C = Cex;
+            double P = Pex;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) {
-            if (c[j]) {
+            for (int j = 0; j < SPER; ++j) {
+                s_eC[a * SPER + j] = C;  // rows and sum before bucket j of the chunk
+                s_eP[a * SPER + j] = P;
                 C += c[j];
                 P = P + sm[j];
-                U = fmin(U, fb::h_of(C, P, pe) + fb::kMarg);
             }
         }
     }
-    U = blk_min_d(U, red);
+    __syncthreads();
+    const int nact = s_nact;
+    double U = INFINITY;
     long long bmin = SB, bmax = -1;
-    {
-        long long C = Cex;
-        double P = Pex;
+    if (nact <= BMAXACT) {
+        static_assert(BMAXACT * SPER <= ST, "one work item per lane");
+        const int q = t;
+        const bool has = q < nact * SPER;
+        const int bk = has ? s_act[q / SPER] * SPER + (q % SPER) : 0;
+        const unsigned cq = has ? s_cnt[bk] : 0u;
+        const long long C0 = has ? s_eC[q] : 0;
+        const double P0 = has ? s_eP[q] : 0.0;
+        // the same additions in the same order as the chunk walk: same bits; the bucket's
+        // end value and its lower bound in one round of independent log2
+        double lb = INFINITY;
+        if (cq) {
+            U = fb::h_of(C0 + cq, P0 + s_sum[bk], pe) + fb::kMarg;
+            lb = fb::block_lb(C0, cq, P0, fb::lo_r(kmin + ((u64)bk << sh)), pe);
+        }
+        BSEL_T(10);
+        U = fmin(blk_min_d(U, red), U1);
+        if (cq && (!(lb > U) || !(pe >= 1.0))) {
+            bmin = bk;
+            bmax = bk;
+        }
+    } else {  // many active chunks (pe < 1: every non-empty one): each walks its buckets
+        if (active) {
+            long long C = Cex;
+            double P = Pex;
 #pragma unroll
-        for (int j = 0; j < SPER; ++j) {
-            const int bk = t * SPER + j;
-            if (c[j]) {
-                const double lb = fb::block_lb(C, c[j], P, fb::lo_r(kmin + ((u64)bk << sh)), pe);
-                if (!(lb > U) || !(pe >= 1.0)) {
-                    bmin = min(bmin, (long long)bk);
-                    bmax = max(bmax, (long long)bk);
+            for (int j = 0; j < SPER; ++j) {
+                if (c[j]) {
+                    C += c[j];
+                    P = P + sm[j];
+                    U = fmin(U, fb::h_of(C, P, pe) + fb::kMarg);
                 }
             }
-            C += c[j];
-            P = P + sm[j];
+        }
+        U = fmin(blk_min_d(U, red), U1);
+        if (active) {
+            long long C = Cex;
+            double P = Pex;
+#pragma unroll
+            for (int j = 0; j < SPER; ++j) {
+                const int bk = t * SPER + j;
+                if (c[j]) {
+                    const double lb = fb::block_lb(C, c[j], P, fb::lo_r(kmin + ((u64)bk << sh)), pe);
+                    if (!(lb > U) || !(pe >= 1.0)) {
+                        bmin = min(bmin, (long long)bk);
+                        bmax = max(bmax, (long long)bk);
+                    }
+                }
+                C += c[j];
+                P = P + sm[j];
+            }
         }
     }
     blk_minmax_ll(bmin, bmax, red);
+    BSEL_T(11);
     // bucket starts (rows before each bucket) replace the counts; fill counters zeroed
     unsigned *fill = reinterpret_cast<unsigned *>(s_sum);
     {
@@ -454,6 +542,7 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
     __syncthreads();
     const long long K0 = s_k[0];
     const long long W = s_k[1] - K0;
+    BSEL_T(3);
     // 4. sum of r below the window (deterministic), window rows to scratch
     double sb = 0.0;
     SEL_ROWS(if (rv < INFINITY) {
@@ -468,6 +557,7 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
         }
     })
     const double S_base = blk_sum_d(sb, red);  // its barriers also publish the scratch
+    BSEL_T(4);
     // 5. exact (key, row) order of the window: rank inside the row's bucket
     for (long long q = t; q < W; q += ST) {
         const u64 kq = ws.wkey[b + q];
@@ -486,6 +576,7 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
         ws.sr[pos] = ws.wr[b + q];
     }
     __syncthreads();
+    BSEL_T(5);
     // 6. prefix sums in window order, FRMSD of every window position, first minimum
     double run = S_base, bf = INFINITY;
     long long bk = 0x7fffffffffffffffLL;
@@ -514,7 +605,16 @@ __global__ __launch_bounds__(ST) void k_batch_select(const u64 *__restrict__ key
         }
         run = run + tot;
     }
+    BSEL_T(6);
     blk_argmin(bf, bk, red);
+    BSEL_T(7);
+#ifdef FICP_BSEL_PROF
+    if (t == 0 && (p % 97) == 5)
+        printf("BSEL p=%d N=%lld W=%lld sh=%d t: %lld %lld %lld %lld %lld %lld %lld | %lld %lld %lld %lld %lld\n", p, N, W, sh,
+               bt_[1] - bt_[0], bt_[2] - bt_[1], bt_[3] - bt_[2], bt_[4] - bt_[3], bt_[5] - bt_[4],
+               bt_[6] - bt_[5], bt_[7] - bt_[6], bt_[8] - bt_[2], bt_[9] - bt_[8], bt_[10] - bt_[9],
+               bt_[11] - bt_[10], bt_[3] - bt_[11]);
+#endif
     if (t == 0) {
         if (bk == 0x7fffffffffffffffLL) {  // every FRMSD NaN: the reference keeps (0.0, 0)
             st[p].k = 0;

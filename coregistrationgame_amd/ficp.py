@@ -92,7 +92,11 @@ class FractionalICP:
         return self._context().frmsd(a, b, num_elements, self.match_dims, fraction, self.lambda_val)
 
     def get_n_first_elements(self, num_elements, distances):
-        """argsort(distances)[:num_elements] -- ficp.py:62-63 (stable: ties by index)."""
+        """argsort(distances)[:num_elements] -- ficp.py:62-63.
+
+        Deliberate deviation: ties are ordered by index (a stable sort).  The reference's
+        np.argsort default (quicksort) is not stable, so its choice among equal distances
+        at the cut can differ; tie-at-k parity is unpinned."""
         d = np.asarray(distances, dtype=float).ravel()
         if d.size == 0:
             return np.zeros(0, dtype=np.intp)

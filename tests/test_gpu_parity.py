@@ -300,10 +300,12 @@ def test_run_vs_oracle_100k(oracle):
 
 
 # every environment switch of libficp.so that changes which kernels run (the only ones
-# left): the fused fit, and the two fallback paths the bucket sort takes for
-# layers it cannot plan (global-atomic grid build, 64-bit radix work order), forced here
+# left): the fused fit, the two fallback paths the bucket sort takes for
+# layers it cannot plan (global-atomic grid build, 64-bit radix work order), forced here,
+# and the grid density (points per cell: more per cell, more cells per disk scan)
 KNOBS = [{}, {"FICP_FUSE_FIT": "1"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
-         {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "1"}]
+         {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "1"},
+         {"FICP_GRID_PER_CELL": "4"}]
 
 
 @pytest.mark.parametrize("knobs,md", [(k, 3) for k in KNOBS] + [({}, 2), ({"FICP_GRID_ATOMIC": "1"}, 2)],

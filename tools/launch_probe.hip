@@ -64,5 +64,32 @@ int main() {
             if (rep) printf("%-18s %7.2f us per launch\n", c.name, ms * 1000.f / N);
         }
     }
+    // the same dependent chain captured into hipGraphs: one graph of 1000 kernels, and a
+    // graph of 7 (one loop body) launched 1000 / 7 times
+    for (int len : {1000, 7}) {
+        for (int grid : {1, 128}) {
+            hipGraph_t g;
+            hipGraphExec_t ge;
+            CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+            for (int i = 0; i < len; ++i)
+                hipLaunchKernelGGL(k_chain, dim3(grid), dim3(256), 0, s, d);
+            CK(hipStreamEndCapture(s, &g));
+            CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            const int reps = 1000 / len;
+            for (int rep = 0; rep < 2; ++rep) {
+                CK(hipEventRecord(e0, s));
+                for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge, s));
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (rep)
+                    printf("graph of %4d, chain %dx256 %7.2f us per kernel\n", len, grid,
+                           ms * 1000.f / (reps * len));
+            }
+            CK(hipGraphExecDestroy(ge));
+            CK(hipGraphDestroy(g));
+        }
+    }
     return 0;
 }

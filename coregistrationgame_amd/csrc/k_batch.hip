@@ -46,11 +46,23 @@ __global__ __launch_bounds__(BB) void k_batch_bbox(const double *tx, const doubl
     __shared__ double s[4][BB];
     const int p = blockIdx.x;
     double a0 = INFINITY, a1 = -INFINITY, b0 = INFINITY, b1 = -INFINITY;
-    for (int64_t j = to[p] + threadIdx.x; j < to[p + 1]; j += BB) {
-        a0 = fmin(a0, tx[j]);
-        a1 = fmax(a1, tx[j]);
-        b0 = fmin(b0, ty[j]);
-        b1 = fmax(b1, ty[j]);
+    // 8 rows per thread in flight (one row per trip was one load latency per row)
+    const int64_t je = to[p + 1];
+    for (int64_t j0 = to[p] + threadIdx.x; j0 < je; j0 += 8 * BB) {
+        double vx[8], vy[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t j = j0 + (int64_t)u * BB;
+            vx[u] = j < je ? tx[j] : NAN;  // fmin / fmax ignore NaN
+            vy[u] = j < je ? ty[j] : NAN;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a0 = fmin(a0, vx[u]);
+            a1 = fmax(a1, vx[u]);
+            b0 = fmin(b0, vy[u]);
+            b1 = fmax(b1, vy[u]);
+        }
     }
     s[0][threadIdx.x] = a0;
     s[1][threadIdx.x] = a1;
@@ -147,6 +159,7 @@ constexpr int SPER = SB / ST;    // buckets per thread in the scans
 constexpr int RPT = FICP_BSEL_RPT;  // rows per thread kept in registers (plots <= ST * RPT rows)
 constexpr int SRP = 4;           // window rows per thread per scan chunk
 constexpr int BMAXACT = ST / SPER;  // active bound chunks evaluated one bucket per lane
+constexpr int WCAP = 1024;          // candidate windows up to this many rows stay in LDS
 
 typedef unsigned long long u64;
 
@@ -360,6 +373,9 @@ __global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restr
     __shared__ double s_sum[SB];    // sums, then per-bucket fill counters (as unsigned)
     __shared__ SelRed red;
     __shared__ long long s_k[2];
+    __shared__ u64 l_wk[WCAP], l_sk[WCAP];       // a small window's rows (phases 4-6)
+    __shared__ double l_wr[WCAP], l_sr[WCAP];
+    __shared__ uint32_t l_wrow[WCAP], l_srow[WCAP];
     __shared__ int s_act[BMAXACT];               // active chunks (thread ids)
     __shared__ int s_nact;
     __shared__ long long s_eC[BMAXACT * SPER];   // rows before each of their buckets
@@ -543,37 +559,45 @@ __global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restr
     const long long K0 = s_k[0];
     const long long W = s_k[1] - K0;
     BSEL_T(3);
-    // 4. sum of r below the window (deterministic), window rows to scratch
+    // 4. sum of r below the window (deterministic), window rows to scratch: LDS when the
+    // window is small (the normal case: tens of rows), the global scratch otherwise
+    const bool inl = W <= WCAP;
+    u64 *wk = inl ? l_wk : ws.wkey + b;
+    uint32_t *wrw = inl ? l_wrow : ws.wrow + b;
+    double *wr = inl ? l_wr : ws.wr + b;
+    u64 *sk = inl ? l_sk : ws.skey + b;
+    uint32_t *srw = inl ? l_srow : ws.srow + b;
+    double *sr = inl ? l_sr : ws.sr + b;
     double sb = 0.0;
     SEL_ROWS(if (rv < INFINITY) {
         const int bk = (int)((kk - kmin) >> sh);
         if (bk < bmin) {
             sb = sb + rv;
         } else if (bk <= bmax) {
-            const int64_t slot = b + (int64_t)s_cnt[bk] - K0 + atomicAdd(&fill[bk], 1u);
-            ws.wkey[slot] = kk;
-            ws.wrow[slot] = (uint32_t)i;
-            ws.wr[slot] = rv;
+            const int64_t slot = (int64_t)s_cnt[bk] - K0 + atomicAdd(&fill[bk], 1u);
+            wk[slot] = kk;
+            wrw[slot] = (uint32_t)i;
+            wr[slot] = rv;
         }
     })
     const double S_base = blk_sum_d(sb, red);  // its barriers also publish the scratch
     BSEL_T(4);
     // 5. exact (key, row) order of the window: rank inside the row's bucket
     for (long long q = t; q < W; q += ST) {
-        const u64 kq = ws.wkey[b + q];
-        const uint32_t rq = ws.wrow[b + q];
+        const u64 kq = wk[q];
+        const uint32_t rq = wrw[q];
         const int bk = (int)((kq - kmin) >> sh);
         const long long s0 = (long long)s_cnt[bk] - K0;
         const long long s1 = (long long)(bk + 1 < SB ? s_cnt[bk + 1] : nfin) - K0;
         long long rank = 0;
         for (long long j = s0; j < s1; ++j) {
-            const u64 kj = ws.wkey[b + j];
-            rank += (kj < kq) || (kj == kq && ws.wrow[b + j] < rq);
+            const u64 kj = wk[j];
+            rank += (kj < kq) || (kj == kq && wrw[j] < rq);
         }
-        const int64_t pos = b + s0 + rank;
-        ws.skey[pos] = kq;
-        ws.srow[pos] = rq;
-        ws.sr[pos] = ws.wr[b + q];
+        const int64_t pos = s0 + rank;
+        sk[pos] = kq;
+        srw[pos] = rq;
+        sr[pos] = wr[q];
     }
     __syncthreads();
     BSEL_T(5);
@@ -586,7 +610,7 @@ __global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restr
         double acc = 0.0;
 #pragma unroll
         for (int q = 0; q < SRP; ++q) {
-            v[q] = (j0 + q < W) ? ws.sr[b + j0 + q] : 0.0;
+            v[q] = (j0 + q < W) ? sr[j0 + q] : 0.0;
             acc = acc + v[q];
         }
         double tot;
@@ -624,8 +648,8 @@ __global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restr
             st[p].k = bk;
             st[p].frac = (double)bk / (double)N;
             st[p].frmsd = bf;
-            st[p].tkey = ws.skey[b + (bk - K0 - 1)];
-            st[p].trow = (long long)ws.srow[b + (bk - K0 - 1)];
+            st[p].tkey = sk[bk - K0 - 1];
+            st[p].trow = (long long)srw[bk - K0 - 1];
         }
     }
 }
@@ -649,24 +673,57 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
     const unsigned long long tk = st[p].tkey;
     const double px = grids[p].px, py = grids[p].py;
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t i = b + threadIdx.x; i < e; i += BB) {
-        const unsigned long long ki = key[i];
-        if (ki < tk || (ki == tk && i <= t)) {
-            const double xs = sx[i] - px, ys = sy[i] - py;
-            const double xt = cx[i] - px, yt = cy[i] - py;
-            c[0] = c[0] + xs;
-            c[1] = c[1] + ys;
-            c[2] = c[2] + xt;
-            c[3] = c[3] + yt;
-            c[4] = c[4] + xs * xt;
-            c[5] = c[5] + xs * yt;
-            c[6] = c[6] + ys * xt;
-            c[7] = c[7] + ys * yt;
+    // FU rows per thread in flight, every load issued before the predicate (the row loop
+    // with a key load and then the dependent row loads took two round trips per row:
+    // 32 us per launch at 128 plots, where the launch is one latency-bound round)
+    constexpr int FU = 8;
+    for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += (int64_t)BB * FU) {
+        unsigned long long kv[FU];
+        double xs[FU], ys[FU], xt[FU], yt[FU];
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const int64_t i = i0 + (int64_t)u * BB;
+            const bool in = i < e;
+            kv[u] = in ? key[i] : ~0ULL;
+            xs[u] = in ? sx[i] : 0.0;
+            ys[u] = in ? sy[i] : 0.0;
+            xt[u] = in ? cx[i] : 0.0;
+            yt[u] = in ? cy[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {  // the thread's rows in the same order as one by one
+            const int64_t i = i0 + (int64_t)u * BB;
+            if (i < e && (kv[u] < tk || (kv[u] == tk && i <= t))) {
+                const double a0 = xs[u] - px, a1 = ys[u] - py;
+                const double b0 = xt[u] - px, b1 = yt[u] - py;
+                c[0] = c[0] + a0;
+                c[1] = c[1] + a1;
+                c[2] = c[2] + b0;
+                c[3] = c[3] + b1;
+                c[4] = c[4] + a0 * b0;
+                c[5] = c[5] + a0 * b1;
+                c[6] = c[6] + a1 * b0;
+                c[7] = c[7] + a1 * b1;
+            }
         }
     }
+    // fixed tree: wave butterfly, then the waves in order (eight 8-step LDS trees with a
+    // barrier per step cost ~64 barriers here)
+    constexpr int FW = BB / 64;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) c[q] = bsum(c[q], s);
+    for (int q = 0; q < 8; ++q) c[q] = wave_sum_d(c[q]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[8 * (threadIdx.x >> 6) + q] = c[q];
+    __syncthreads();
     if (threadIdx.x != 0) return;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        double v = s[q];
+#pragma unroll
+        for (int w = 1; w < FW; ++w) v = v + s[8 * w + q];
+        c[q] = v;
+    }
     const double kk = (double)k;
     const double csx = c[0] / kk, csy = c[1] / kk, ctx = c[2] / kk, cty = c[3] / kk;
     const double H0 = c[4] - c[0] * ctx, H1 = c[5] - c[0] * cty;

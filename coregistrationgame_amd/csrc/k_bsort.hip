@@ -343,7 +343,16 @@ BSortPlan bsort_plan(int64_t n, int64_t nkeys) {
     p.fs = std::max(0, kb - want);
     p.nbk = (int)std::max<int64_t>(1, (nkeys + (((int64_t)1) << p.fs) - 1) >> p.fs);
     p.nb1 = (int)std::min<int64_t>(256, std::max<int64_t>(1, (n + slice - 1) / slice));
-    p.bcap = (int)std::min<int64_t>(4096, 2 * bpts);
+    // LDS tile: twice the mean bucket (at 10M points the 16384 buckets hold ~610 points:
+    // a 512 tile sent most of them through the global-scratch path, 467 us per C4 grid
+    // build), within 64 KB of LDS so two workgroups still share a CU
+    {
+        const int64_t mean = (n + p.nbk - 1) / p.nbk;
+        int64_t cap = std::max<int64_t>(2 * bpts, ((2 * mean + 255) / 256) * 256);
+        const int64_t fit = (65536 - (int64_t)2 * 4 * (((int64_t)1) << p.fs)) / (int64_t)(sizeof(TPt) + 8 + 2);
+        cap = std::min<int64_t>(cap, std::max<int64_t>(2 * bpts, (fit / 256) * 256));
+        p.bcap = (int)std::min<int64_t>(4096, cap);
+    }
     p.per = (n + p.nb1 - 1) / p.nb1;
     return p;
 }

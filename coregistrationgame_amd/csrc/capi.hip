@@ -11,6 +11,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+
 #include <algorithm>
 #include <cmath>
 #include <map>
@@ -25,13 +27,23 @@ namespace ficp_capi {
 thread_local std::string g_err;
 
 // Wait for a done flag that a kernel stores into coherent pinned memory (-1 = not yet
-// written).  The stream is queried now and then so that a device error or a drained
-// stream without the store ends the wait instead of spinning forever.
+// written).  After 20 ms of waiting the stream is queried now and then, so that a device
+// error or a drained stream without the store ends the wait instead of spinning forever.
+// Not earlier: each hipStreamQuery left a ~6 us idle gap in the queue (one per loop
+// iteration at C3, between the NN launch and the next selection; rocprofv3 runtime +
+// kernel trace).
 int poll_flag(ficp_ctx *c, int *flag, int &v) {
+    std::chrono::steady_clock::time_point t0{};
     for (uint64_t spin = 1;; ++spin) {
         v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);
         if (v != -1) return FICP_OK;
         if ((spin & 1023) == 0) {
+            const auto now = std::chrono::steady_clock::now();
+            if (spin == 1024) t0 = now;
+            if (now - t0 < std::chrono::milliseconds(20)) {
+                __builtin_ia32_pause();
+                continue;
+            }
             const hipError_t e = hipStreamQuery(c->stream);
             if (e == hipSuccess) {
                 v = __atomic_load_n(flag, __ATOMIC_ACQUIRE);

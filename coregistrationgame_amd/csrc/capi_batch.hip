@@ -29,6 +29,8 @@ struct BatchBufs {
     DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp, bs_tmp;
     DevBuf key, gap, r, ccx, ccy, bp, dz2, wkey, skey, wrow, srow, wr, sr;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
+    DevBuf fpart, fctr;                    // batch fit: per-chunk sums, per-plot arrivals
+    unsigned fctr_init_gen = 0;            // fctr allocation whose counters are zeroed
     int *h_flag = nullptr;                 // coherent pinned ring: plots still running
 };
 constexpr int kBatchRing = 4;
@@ -41,7 +43,7 @@ void batch_release(BatchBufs *b) {
                       &b->r,        &b->ccx,     &b->ccy,      &b->wkey,  &b->skey,  &b->wrow,
                       &b->srow,     &b->wr,      &b->sr,       &b->sx,    &b->sy,    &b->sz,
                       &b->tx,       &b->ty,      &b->tz,       &b->stage, &b->bp,
-                      &b->dz2,      &b->bs_tmp};
+                      &b->dz2,      &b->bs_tmp,  &b->fpart,   &b->fctr};
     for (DevBuf *d : bufs) d->release();
     if (b->h_flag) (void)hipHostFree(b->h_flag);
     delete b;
@@ -213,6 +215,12 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         a.dz2 = md == 3 ? b.dz2.as<double>() : nullptr;
         a.cert_block = 8;
         PlotState *st = b.st.as<PlotState>();
+        CHK(b.fpart.ensure((size_t)nplots * (size_t)batch_fit_chunks(max_rows) * 64));
+        CHK(b.fctr.ensure((size_t)nplots * 4));
+        if (b.fctr.gen != b.fctr_init_gen) {  // fresh allocation: zero its atomic words
+            HIPCHK(launch_batch_fit_ctr_zero(b.fctr.as<unsigned>(), nplots, c->stream));
+            b.fctr_init_gen = b.fctr.gen;
+        }
         // every plot makes at most nstages * (max_iter + 1) NN calls
         const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1) + 1;
         auto enqueue = [&](int64_t bit) -> int {
@@ -222,8 +230,8 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                 ProfScope ps(c, P_FIT, "batch_fit");
                 HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
                                         b.key.as<unsigned long long>(), b.so.as<int64_t>(),
-                                        b.grids.as<PlotGrid>(), nplots, allow_refl, st,
-                                        c->stream));
+                                        b.grids.as<PlotGrid>(), nplots, max_rows, allow_refl, st,
+                                        b.fpart.as<double>(), b.fctr.as<unsigned>(), c->stream));
             }
             a.warm_c = bit > 0 ? 1 : 0;
             {

@@ -604,10 +604,15 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
                                 const PlotState *st, int md, hipStream_t s);
 hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
                              PlotState *st, hipStream_t s);
+// plot chunks of the batch fit (k_batch_fit) for plots of at most max_rows rows
+int batch_fit_chunks(int64_t max_rows);
+// part: nplots * batch_fit_chunks(max_rows) * 8 doubles; ctr: nplots arrival counters
+// (atomics only: zero them once per allocation with launch_batch_fit_ctr_zero)
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
                             const double *cy, const unsigned long long *key, const int64_t *so,
-                            const PlotGrid *grids, int nplots, int allow_refl, PlotState *st,
-                            hipStream_t s);
+                            const PlotGrid *grids, int nplots, int64_t max_rows, int allow_refl,
+                            PlotState *st, double *part, unsigned *ctr, hipStream_t s);
+hipError_t launch_batch_fit_ctr_zero(unsigned *ctr, int n, hipStream_t s);
 // Per-plot FRMSD-optimal fraction (ficp.py:73-86), one workgroup per live plot: bucket
 // histogram of the plot's keys, bounds, exact sort of the candidate window only; sets
 // k, frac, frmsd and the threshold pair (tkey, trow).  Scratch: 3 x n words of 8 B and

@@ -25,18 +25,6 @@ namespace {
 
 constexpr int BB = 256;  // threads per per-plot workgroup (bbox, fit)
 
-__device__ __forceinline__ double bsum(double v, double *s) {
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (int w = BB / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) s[threadIdx.x] = s[threadIdx.x] + s[threadIdx.x + w];
-        __syncthreads();
-    }
-    const double r = s[0];
-    __syncthreads();
-    return r;
-}
-
 __device__ __forceinline__ bool better(double f, long long k, double bf, long long bk) {
     return f < bf || (f == bf && k < bk);
 }
@@ -655,16 +643,26 @@ __global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restr
 }
 #undef SEL_ROWS
 
-// one workgroup per looping plot: rigid fit on the plot's first k trees of the order
+// Rigid fit of every looping plot on its first k trees of the order: the plot's rows in
+// chunks of FCH (one workgroup each, 8 rows per thread in flight), each chunk's 8 sums
+// handed to the plot's last arriving chunk (sc1 stores, one agent-scope atomic add per
+// workgroup on the plot's counter, sc1 loads: the k_fit_sums pattern), which adds them in
+// chunk order and solves.  The chunking depends on the plot alone, so a plot's result does
+// not depend on the rest of the batch.  (One workgroup per plot streamed 410 MB at 6.8
+// TB/s with 1024 plots, but with 128 plots per GPU -- the N = 8 share -- a single round
+// of 128 workgroups took 13 us per launch.)
+constexpr int FCH = BB * 8;
 __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double *sy,
                                                   const double *cx, const double *cy,
                                                   const unsigned long long *key,
                                                   const int64_t *so, const PlotGrid *grids,
-                                                  int allow_refl, PlotState *st) {
-    __shared__ double s[BB];
-    const int p = blockIdx.x;
+                                                  int allow_refl, PlotState *st, double *part,
+                                                  unsigned *ctr, int gmax) {
+    __shared__ double s[8 * (BB / 64)];
+    __shared__ int s_last;
+    const int p = blockIdx.x / gmax, g = blockIdx.x % gmax;
     if (st[p].phase != PH_LOOP) {
-        if (threadIdx.x == 0) st[p].apply = 0;
+        if (g == 0 && threadIdx.x == 0) st[p].apply = 0;
         return;
     }
     const int64_t b = so[p], e = so[p + 1];
@@ -672,12 +670,13 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
     const int64_t t = st[p].trow;  // the k-th row of the (key, row) order (k_batch_select)
     const unsigned long long tk = st[p].tkey;
     const double px = grids[p].px, py = grids[p].py;
+    const int gp = (int)((e - b + FCH - 1) / FCH);  // chunks of this plot (<= gmax)
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // FU rows per thread in flight, every load issued before the predicate (the row loop
-    // with a key load and then the dependent row loads took two round trips per row:
-    // 32 us per launch at 128 plots, where the launch is one latency-bound round)
+    // every load issued before the predicate (a row loop with a key load and then the
+    // dependent row loads took two round trips per row)
     constexpr int FU = 8;
-    for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += (int64_t)BB * FU) {
+    {
+        const int64_t i0 = b + (int64_t)g * FCH + threadIdx.x;
         unsigned long long kv[FU];
         double xs[FU], ys[FU], xt[FU], yt[FU];
 #pragma unroll
@@ -691,7 +690,7 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
             yt[u] = in ? cy[i] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < FU; ++u) {  // the thread's rows in the same order as one by one
+        for (int u = 0; u < FU; ++u) {
             const int64_t i = i0 + (int64_t)u * BB;
             if (i < e && (kv[u] < tk || (kv[u] == tk && i <= t))) {
                 const double a0 = xs[u] - px, a1 = ys[u] - py;
@@ -707,8 +706,7 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
             }
         }
     }
-    // fixed tree: wave butterfly, then the waves in order (eight 8-step LDS trees with a
-    // barrier per step cost ~64 barriers here)
+    // the chunk's sums: wave butterfly, then the waves in order (fixed tree)
     constexpr int FW = BB / 64;
 #pragma unroll
     for (int q = 0; q < 8; ++q) c[q] = wave_sum_d(c[q]);
@@ -716,14 +714,30 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
 #pragma unroll
         for (int q = 0; q < 8; ++q) s[8 * (threadIdx.x >> 6) + q] = c[q];
     __syncthreads();
-    if (threadIdx.x != 0) return;
+    if (g >= gp) return;  // (uniform) no rows in this chunk
+    if (threadIdx.x < 8) {
+        double v = s[threadIdx.x];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        double v = s[q];
-#pragma unroll
-        for (int w = 1; w < FW; ++w) v = v + s[8 * w + q];
-        c[q] = v;
+        for (int w = 1; w < FW; ++w) v = v + s[8 * w + threadIdx.x];
+        __hip_atomic_store(&part[8 * ((int64_t)p * gmax + g) + threadIdx.x], v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool last = __hip_atomic_fetch_add(&ctr[p], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == (unsigned)gp - 1u;
+        if (last) __hip_atomic_exchange(&ctr[p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) c[q] = 0.0;
+    for (int h = 0; h < gp; ++h)  // the chunks in order
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            c[q] = c[q] + __hip_atomic_load(&part[8 * ((int64_t)p * gmax + h) + q], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
     const double kk = (double)k;
     const double csx = c[0] / kk, csy = c[1] / kk, ctx = c[2] / kk, cty = c[3] / kk;
     const double H0 = c[4] - c[0] * ctx, H1 = c[5] - c[0] * cty;
@@ -867,13 +881,30 @@ hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, i
     return hipGetLastError();
 }
 
+int batch_fit_chunks(int64_t max_rows) {
+    return (int)std::max<int64_t>(1, (max_rows + FCH - 1) / FCH);
+}
+
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
                             const double *cy, const unsigned long long *key, const int64_t *so,
-                            const PlotGrid *grids, int nplots, int allow_refl, PlotState *st,
-                            hipStream_t s) {
+                            const PlotGrid *grids, int nplots, int64_t max_rows, int allow_refl,
+                            PlotState *st, double *part, unsigned *ctr, hipStream_t s) {
     if (nplots <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_batch_fit, dim3(nplots), dim3(BB), 0, s, sx, sy, cx, cy, key, so, grids,
-                       allow_refl, st);
+    const int gmax = batch_fit_chunks(max_rows);
+    hipLaunchKernelGGL(k_batch_fit, dim3((unsigned)nplots * (unsigned)gmax), dim3(BB), 0, s, sx, sy,
+                       cx, cy, key, so, grids, allow_refl, st, part, ctr, gmax);
+    return hipGetLastError();
+}
+
+__global__ void k_zero_u32_atomic(unsigned *p, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        __hip_atomic_exchange(&p[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t launch_batch_fit_ctr_zero(unsigned *ctr, int n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_zero_u32_atomic, dim3((unsigned)std::min(1024, (n + 255) / 256)), dim3(256), 0,
+                       s, ctr, n);
     return hipGetLastError();
 }
 

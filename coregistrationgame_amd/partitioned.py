@@ -116,7 +116,12 @@ def merge_local(d2s, idxs):
 
 
 class PartitionedFICP:
-    CAPD = 8192  # source mode: candidates one rank may contribute per NN call
+    # source mode: candidates one rank may contribute per NN call: at least CAPD, and 1/64
+    # of the rank's largest row range (a stage's first call, on the uniform bucket map, can
+    # leave ~1e-3 of the rows as candidates: 8M rows on one rank overflowed 8192).  More
+    # than that raises FicpError (ERR_CAP); split the rows over more shards.
+    CAPD = 8192
+    CAPD_FRAC = 64
 
     def __init__(self, source, target, lambda_val=3.0, threshold=1e-6, max_iterations=1000,
                  allow_reflection=False, *, mode="target", group=None, device=None, local_shards=1):
@@ -188,11 +193,13 @@ class PartitionedFICP:
                        sums=torch.zeros(8, dtype=f64, device=dev))
         else:
             hw = _lib.dist_hist_words()
+            n_max = max(c for _, c in parts)
+            self.capd = max(self.CAPD, -(-n_max // self.CAPD_FRAC))
             res.update(sums=[torch.zeros(8, dtype=f64, device=dev) for _ in mine],
                        range2=[torch.zeros(2, dtype=i64, device=dev) for _ in mine],
                        hist=[torch.zeros(hw, dtype=i64, device=dev) for _ in mine],
-                       pack=[torch.zeros(4 + 3 * self.CAPD, dtype=i64, device=dev) for _ in mine],
-                       n_max=max(c for _, c in parts))
+                       pack=[torch.zeros(4 + 3 * self.capd, dtype=i64, device=dev) for _ in mine],
+                       n_max=n_max)
         self._res = res
         return res
 
@@ -274,7 +281,7 @@ class PartitionedFICP:
             for c, (off, cnt) in zip(ctxs, mine):
                 c.dist_begin(2, src[0].data_ptr() + 8 * off, src[1].data_ptr() + 8 * off,
                              zp + 8 * off if md == 3 else 0, cnt, n, res["n_max"], off, lams, self.threshold,
-                             self.max_iterations, self.allow_reflection, res["pivot"], W, self.CAPD)
+                             self.max_iterations, self.allow_reflection, res["pivot"], W, self.capd)
             step, last = self._step_source, ctxs[-1]
         cap = 2 * (max(int(self.max_iterations), 0) + 1)
         done, j = False, 0
@@ -321,8 +328,8 @@ class PartitionedFICP:
             c.dist_hist(rg.data_ptr(), h.data_ptr())
         hg = merge_hist(res["hist"], self.group, world)
         for c, pk in zip(ctxs, res["pack"]):
-            c.dist_candidates(hg.data_ptr(), pk.data_ptr(), self.CAPD)
+            c.dist_candidates(hg.data_ptr(), pk.data_ptr(), self.capd)
         packs = gather_ranked(res["pack"], self.group, world)
         for c in ctxs:
-            c.dist_final(packs.data_ptr(), W, self.CAPD, j)
+            c.dist_final(packs.data_ptr(), W, self.capd, j)
         res["_keep"] = (sums, rg, hg, packs)

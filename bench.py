@@ -62,6 +62,11 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    # rehearsal of N ranks on fewer GPUs (gloo only: RCCL refuses two ranks on one GPU):
+    # FICP_BENCH_SHARE_GPU=<gpus> maps rank r to GPU r % gpus
+    share = int(os.environ.get("FICP_BENCH_SHARE_GPU", "0") or 0)
+    if share > 0:
+        local %= share
     return rank, world, local
 
 

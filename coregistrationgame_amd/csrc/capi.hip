@@ -240,9 +240,9 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             a.warm_c = warm == 2 ? 1 : 0;
             // certified reuse of the match (nn_query_cert): the bound G and the match slot;
             // a workgroup's uncertified queries packed, up to 8 lanes per query
-            CHK(c->gap.ensure(n * 8));
+            CHK(c->gap.ensure(n * sizeof(gap_t)));
             CHK(c->bp.ensure(n * 4));
-            a.gap = c->gap.as<double>();
+            a.gap = c->gap.as<gap_t>();
             a.out_bp = c->bp.as<int32_t>();
             a.cert_block = 8;
         }

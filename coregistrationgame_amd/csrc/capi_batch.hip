@@ -176,7 +176,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         }
         CHK(b.plot_of.ensure(n * 4));
         CHK(b.key.ensure(n * 8));
-        CHK(b.gap.ensure(n * 8));
+        CHK(b.gap.ensure(n * sizeof(gap_t)));
         CHK(b.dz2.ensure(n * 8));
         CHK(b.r.ensure(n * 8));
         CHK(b.ccx.ensure(n * 8));
@@ -211,7 +211,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         a.out_bp = b.bp.as<int32_t>();
         // certified reuse of each query's match (k_grid_nn.hip cert_try): the first call
         // of the batch is cold (every plot starts there), the rest are warm
-        a.gap = b.gap.as<double>();
+        a.gap = b.gap.as<gap_t>();
         a.dz2 = md == 3 ? b.dz2.as<double>() : nullptr;
         a.cert_block = 8;
         PlotState *st = b.st.as<PlotState>();

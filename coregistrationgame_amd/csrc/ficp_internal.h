@@ -89,6 +89,11 @@ struct GridView {
     int64_t m;                  // stems (pts entries); m * 32 < 2^31 (buffer descriptor)
 };
 
+// The certified-reuse bound G per query (k_grid_nn.hip cert_try): fp32, rounded toward
+// -inf, so the stored value stays a lower bound (4 B read + 4 B written per certified
+// query instead of 8 + 8; C3 it/s unchanged against fp64 within noise, all -m gpu green).
+typedef float gap_t;
+
 // Per-launch NN arguments.
 struct NNArgs {
     double *sx;                 // source x (updated in place when T != nullptr)
@@ -111,7 +116,7 @@ struct NNArgs {
                                 // call (warm start; nullable, entries < 0 ignored)
     int32_t *out_bp;            // grid kernels: out: grid slot matched (nullable; may alias)
     double *dz2;                // grid kernels: out: dz^2 of the match (nullable; md 3)
-    double *gap;                // grid kernels: in/out: certified-reuse bound (nullable;
+    gap_t *gap;                 // grid kernels: in/out: certified-reuse bound (nullable;
                                 // needs cx, cy, dz2, out_bp; k_grid_nn.hip nn_query_cert)
     int cert_block;             // grid kernels, with gap and warm_c: > 0 packs each workgroup's
                                 // uncertified queries onto its first lanes, up to this many

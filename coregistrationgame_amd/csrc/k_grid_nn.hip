@@ -556,6 +556,9 @@ __device__ __forceinline__ void cover_scan(const GridView &g, const Stems &S, do
 #endif
 
 // rounding allowance of the certificate's distances (coordinates up to ~1e7 m: ulp ~2e-9 m)
+// G stored rounded down: a lower bound stays a lower bound (a few 1e-7 m at G ~ 5 m)
+__device__ __forceinline__ gap_t gap_rd(double g) { return __double2float_rd(g); }
+
 __device__ __forceinline__ double cert_eps(const GridView &g, double qx, double qy) {
     return 2.0 * g.margin + 1e-12 * (fabs(qx) + fabs(qy)) + 1e-9;
 }
@@ -605,7 +608,7 @@ __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, con
     mv = sqrt(mx * mx + my * my);
     const double G = a.gap[i] - mv - eps;
     if (!(d2w < INFINITY && sqrt(d2w) + eps < G)) return false;
-    a.gap[i] = G;
+    a.gap[i] = gap_rd(G);
     if (a.idx) a.idx[i] = (int)load_zid(S.r, a.out_bp[i]).z;
     const double d = sqrt(d2w);
     const unsigned long long k = ordkey(d);
@@ -677,7 +680,7 @@ __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, co
         }
         gnew = fmin(sqrt(b.s2), rc - mq) - eps;
     }
-    a.gap[i] = b.slot >= 0 ? gnew : 0.0;
+    a.gap[i] = gap_rd(b.slot >= 0 ? gnew : 0.0);
     a.out_bp[i] = b.slot;
     finish(a, S, i, qz, Best{b.d2, b.id, max(b.slot, 0)}, kmin_c, kmax);
 }
@@ -749,7 +752,7 @@ __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView 
         return;
     }
     const double gnew = fmin(sqrt(b.s2), rc - mq) - eps;
-    a.gap[i] = gnew;
+    a.gap[i] = gap_rd(gnew);
     finish(a, S, i, qz, Best{b.d2, b.id, max(b.slot, 0)}, kmin_c, kmax);
 }
 
@@ -862,7 +865,7 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
             // call, which scans every query with its cover.  A cold scan with the cover
             // cost more than that first warm call saved (C3: +1.8 % without it)
             nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
-            a.gap[i] = 0.0;
+            a.gap[i] = 0;
         } else if (a.gap) {
             nn_query_cert<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
         } else {
@@ -962,7 +965,7 @@ __global__ __launch_bounds__(256) NNB_WPE void k_nn_grid_batch(NNArgs a, const i
     } else if (live) {
         const GridView g = plot_view(grids[p], pts, cell_start, m);
         nn_query<MD>(a, g, S, i, T, kmin_c, kmax);
-        if (a.gap) a.gap[i] = 0.0;  // the cold call stores no certificate (k_nn_grid)
+        if (a.gap) a.gap[i] = 0;  // the cold call stores no certificate (k_nn_grid)
     }
 }
 

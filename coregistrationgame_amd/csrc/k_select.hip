@@ -39,6 +39,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 
 namespace ficp {
 
@@ -90,6 +91,7 @@ constexpr int GI = FICP_GI;  // gather: rows per thread (~1 block per CU at 1M r
 // error bits of SelCtl::err (sticky; the host checks them after a run)
 constexpr unsigned ERR_EMPTY = 1u;  // candidate set empty (cannot happen with finite r)
 constexpr unsigned ERR_CAP = 2u;    // distributed run: a rank's candidates exceeded the capacity
+constexpr unsigned ERR_SPIN = 4u;   // k_sel_bounds_gather: the bounds flag never came (bounded wait)
 
 constexpr int NL = 2048, NF = 4096, NF_LOG = 12, NC_LOG = 11;
 static_assert(NL + NF + NL == NB, "bucket map regions");
@@ -109,6 +111,8 @@ struct SelCtl {
     unsigned err;          // sticky error bits (agent-scope atomics only)
     unsigned levels;       // statistics: refinement levels run (plain, final kernel only)
     unsigned radix;        // statistics: radix fallbacks (plain, final kernel only)
+    unsigned pad_;
+    u64 bpub;              // k_sel_bounds_gather: (launch token << 32) | (b0 << 16) | b1
 };
 
 struct SelWS {
@@ -580,7 +584,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
                                                  u64 *range, int64_t nparts, SelWS w,
                                                  const int *skip, HistPack hp,
                                                  const IterState *st) {
-    if (skip && *skip) return;
+    const int sk = skip ? *skip : 0;  // checked after the first rows' loads have issued
     __shared__ u64 sp[NB];
     __shared__ u64 s_u[HHT / 64], s_v[HHT / 64];
 #ifndef FICP_HIST_U
@@ -601,6 +605,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
         rv[u] = q < i1 ? r[q] : 0.0;
     }
     const BPrev pv = bprev_of(st);
+    if (sk) return;
     for (int b = threadIdx.x; b < NB; b += HHT) sp[b] = 0ULL;
     u64 kmin, kmax;
     if (nparts > 0) {
@@ -679,7 +684,7 @@ __device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsig
 
 __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int *skip,
                                                      HistPack hp, long long *iout) {
-    if (skip && *skip) return;
+    const int sk = skip ? *skip : 0;  // checked after the copies' loads (no writes before)
     __shared__ unsigned s_c[RG][RBPB];
     __shared__ u64 s_f[RG][RBPB];
     const int bl = threadIdx.x % RBPB, g = threadIdx.x / RBPB;
@@ -704,6 +709,7 @@ __global__ __launch_bounds__(1024) void k_sel_reduce(SelWS w, int nhb, const int
         c += (unsigned)(v >> hp.shift);
         f += v & mask;
     }
+    if (sk) return;
     s_c[g][bl] = c;
     s_f[g][bl] = f;
     __syncthreads();
@@ -761,11 +767,13 @@ __device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsig
 // only for the chunks that can hold the minimum, one bucket per lane (a chunk walked by
 // its own thread serialised ~16 dependent evaluations: ~10 us at C3).
 constexpr int MAXACT = HT / (NB / HT);  // active chunks evaluated one bucket per lane
-__global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double lam,
-                                                   const double *lam_dev, const int *skip,
-                                                   int fixb) {
-    if (skip && *skip) return;
-    if (lam_dev) lam = *lam_dev;
+// returns the candidate bucket range [b0, b1] packed as (b0 << 16) | b1 (every thread)
+// (kBoundsSkipped when *skip: the launch is a no-op).  Every load that does not depend on
+// another (skip flag, lambda, bucket map, chunk totals) issues before the first wait.
+constexpr unsigned kBoundsSkipped = 0xffffffffu;
+__device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
+                                                const double *lam_dev, const int *skip,
+                                                int fixb) {
     constexpr int PER = NB / HT;
     __shared__ Scr scr;
     __shared__ int s_act[MAXACT];
@@ -773,15 +781,20 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     __shared__ long long eC[MAXACT * PER];  // rows before bucket j of active chunk a
     __shared__ double eLo[MAXACT * PER];    // lower sum before it
     __shared__ double eHi[MAXACT * PER];    // upper sum through it
+    __shared__ unsigned eN[MAXACT * PER];   // its count
     const int t = threadIdx.x;
-    const BMap bm = w.ctl->map;
-    SELPROF(8);
-    if (t == 0) s_nact = 0;
     static_assert(PER == 16, "chunk totals of k_sel_reduce");
     // this thread's chunk of PER consecutive buckets: totals from k_sel_reduce; the
     // buckets themselves are loaded only by the chunks that stay active below
+    const int sk = skip ? *skip : 0;
+    const double lamv = lam_dev ? *lam_dev : lam;
+    const BMap bm = w.ctl->map;
     const long long ct = w.acnt[t];
     const double tlo = w.alo[t], thi = w.ahi[t];
+    if (sk) return kBoundsSkipped;
+    lam = lamv;
+    SELPROF(8);
+    if (t == 0) s_nact = 0;
     SELPROF(9);
     long long Cex = ct;
     double Plo = tlo, Phi = thi;
@@ -834,6 +847,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
             for (int j = 0; j < PER; ++j) {
                 eC[a * PER + j] = C;
                 eLo[a * PER + j] = PL;
+                eN[a * PER + j] = cc[j];
                 C += cc[j];
                 PL = PL + blo[j];
                 PH = PH + bhi[j];
@@ -848,15 +862,14 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
     if (nact <= MAXACT) {
         // one bucket per lane: work item q = (active chunk q / PER, bucket q % PER)
         for (int q = t; q < nact * PER; q += HT) {
-            const int b = s_act[q / PER] * PER + (q % PER);
-            const unsigned c = w.hcnt[b];
+            const unsigned c = eN[q];
             if (c) U = fmin(U, h_of(eC[q] + c, eHi[q], p) + kMarg);
         }
         U = fmin(blk_min_d(U, scr), U1);
         SELPROF(12);
         for (int q = t; q < nact * PER; q += HT) {
             const int b = s_act[q / PER] * PER + (q % PER);
-            const unsigned c = w.hcnt[b];
+            const unsigned c = eN[q];
             if (c) {
                 const double lb = block_lb(eC[q], c, eLo[q], lo_r(bucket_lo(bm, b)), p);
                 if (!(lb > U) || !(p >= 1.0)) {
@@ -922,18 +935,27 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
         __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     SELPROF(14);
+    return ((unsigned)bmin << 16) | (unsigned)bmax;
 }
 
-__global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_t *orig,
-                                                   const double *r, int64_t n, SelWS w,
-                                                   const int *skip, FitSrc fs) {
-    if (skip && *skip) return;
+__global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double lam,
+                                                   const double *lam_dev, const int *skip,
+                                                   int fixb) {
+    bounds_body(w, N, lam, lam_dev, skip, fixb);
+}
+
+// gen != 0: the candidate buckets come from block 0 of the same launch (k_sel_bounds_gather),
+// published in ctl->bpub with the token gen; the rows' loads are issued before the wait
+__device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig, const double *r,
+                                            int64_t n, SelWS w, FitSrc fs, int blk,
+                                            unsigned gen, const int *skip) {
+    const int sk = skip ? *skip : 0;  // checked after the rows' loads have issued
     __shared__ double s_w[GT / 64];
     __shared__ double s_f[8 * (GT / 64)];
-    const BMap bm = w.ctl->map;
-    const int b0 = w.ctl->b0, b1 = w.ctl->b1;
+    __shared__ int s_b[2];
+    const BMap bm = w.ctl->map;  // k_sel_hist's (an earlier launch)
     const int lane = threadIdx.x & 63;
-    const int64_t base = (int64_t)blockIdx.x * (GT * GI) + threadIdx.x;
+    const int64_t base = (int64_t)blk * (GT * GI) + threadIdx.x;
     // all loads first (no load waits behind the append's atomic)
     u64 kk[GI];
     double rr[GI];
@@ -942,6 +964,35 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
         const int64_t i = base + (int64_t)q * GT;
         kk[q] = i < n ? key[i] : 0ULL;
         rr[q] = i < n ? r[i] : 0.0;
+    }
+    if (sk) return;
+    int b0, b1;
+    if (gen) {
+        if (threadIdx.x == 0) {
+            // {gen, b0, b1} is one 8-B granule stored sc1 by block 0: an sc1 poll sees it
+            // whole (MI355X_MICROARCH.md hand-off table), no acquire fence.  Bounded wait:
+            // block 0 is dispatched first and never waits, so the flag comes; should it not
+            // (2^20 polls, >= ~30 ms), raise ERR_SPIN (the host fails the run), no hang
+            unsigned it = 0;
+            u64 v;
+            while (((v = __hip_atomic_load(&w.ctl->bpub, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) >> 32) != gen) {
+                if (++it == (1u << 20)) {
+                    __hip_atomic_fetch_or(&w.ctl->err, ERR_SPIN, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_b[0] = (int)((v >> 16) & 0xffffu);
+            s_b[1] = (int)(v & 0xffffu);
+        }
+        __syncthreads();
+        b0 = s_b[0];
+        b1 = s_b[1];
+    } else {
+        b0 = w.ctl->b0;
+        b1 = w.ctl->b1;
     }
     double acc = 0.0;
     unsigned inm = 0;   // bit q: row q is a candidate
@@ -1034,13 +1085,43 @@ __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int q = 0; q < GT / 64; ++q) t = t + s_w[q];
-        w.parts[blockIdx.x] = t;
+        w.parts[blk] = t;
     }
     if (fs.on && threadIdx.x < 8) {
         double t = 0.0;
         for (int q = 0; q < GT / 64; ++q) t = t + s_f[8 * q + threadIdx.x];
-        w.fparts[8 * blockIdx.x + threadIdx.x] = t;
+        w.fparts[8 * blk + threadIdx.x] = t;
     }
+}
+
+__global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_t *orig,
+                                                   const double *r, int64_t n, SelWS w,
+                                                   const int *skip, FitSrc fs) {
+    gather_body(key, orig, r, n, w, fs, blockIdx.x, 0u, skip);
+}
+
+// k_sel_bounds and k_sel_gather as one launch: block 0 computes the candidate buckets
+// (bounds_body, GT == HT threads) and publishes [b0, b1] with the launch's token gen
+// (unique per launch) in one 8-B sc1 store; blocks 1.. load their rows meanwhile, poll
+// the word, then gather.  One launch boundary less per NN call, and the rows' loads overlap the bounds.
+static_assert(GT == HT, "k_sel_bounds_gather: block 0 runs bounds_body with HT threads");
+__global__ __launch_bounds__(GT) void k_sel_bounds_gather(const u64 *key, const uint32_t *orig,
+                                                          const double *r, int64_t n, SelWS w,
+                                                          double lam, const double *lam_dev,
+                                                          const int *skip, int fixb, FitSrc fs,
+                                                          unsigned gen) {
+    if (blockIdx.x == 0) {
+        const unsigned bb = bounds_body(w, n, lam, lam_dev, skip, fixb);
+        if (bb != kBoundsSkipped && threadIdx.x == 0) {
+            // thread 0 reset ccount (atomic) inside bounds_body: drain it before the flag,
+            // so no gather block's append can precede the reset
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&w.ctl->bpub, ((u64)gen << 32) | bb, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    gather_body(key, orig, r, n, w, fs, blockIdx.x - 1, gen, skip);
 }
 
 // ---------------------------------------------------------- the final workgroup
@@ -1765,12 +1846,20 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
                                                   const double *lam_dev, IterState *st,
                                                   const int *skip, LoopCtl lc, int fuse_loop,
                                                   int *host_flag, FitSrc fs) {
-    if (skip && *skip) {
+    // the independent loads (skip flag, lambda, the candidate count and the bounds'
+    // outputs) issue together, before the first wait
+    const int sk = skip ? *skip : 0;
+    const double lamv = lam_dev ? *lam_dev : lam;
+    unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    const long long kbase = w.ctl->kbase;
+    const double Ub = w.ctl->U;
+    if (sk) {
         if (host_flag && threadIdx.x == 0)
             __hip_atomic_store(host_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
-    if (lam_dev) lam = *lam_dev;
+    lam = lamv;
     __shared__ __align__(16) unsigned char sm[SMEM];
     __shared__ Scr scr;
     __shared__ IterState s_st;  // thread 0's working copy of the state (one load, one store)
@@ -1782,12 +1871,6 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     // 16-B loads here and as many stores at the end: ~1 us each way)
     static_assert(sizeof(IterState) % 4 == 0, "IterState words");
     constexpr int SW = (int)(sizeof(IterState) / 4);
-    // the candidate count and the bounds' outputs first: their latency overlaps the copy
-    // and the S0 reduction below
-    unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    const long long kbase = w.ctl->kbase;
-    const double Ub = w.ctl->U;
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
     if (t < 8) s_fit[t] = 0.0;
     double a = 0.0;
@@ -1858,6 +1941,7 @@ __global__ void k_sel_init(SelWS w) {
         __hip_atomic_exchange(&w.ctl->err, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         w.ctl->levels = 0;
         w.ctl->radix = 0;
+        __hip_atomic_store(&w.ctl->bpub, (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2004,11 +2088,14 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
                        range_parts, w, skip, hp, (const IterState *)st);
     hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip, hp,
                        (long long *)nullptr);
-    hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip, hp.fixb);
     const int gb = gather_blocks(n);
     FitSrc fs{};
     if (fit && loop) fs = *fit;  // the fused fit needs the fused loop step (it runs after it)
-    hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs);
+    static std::atomic<unsigned> s_gen{0};  // launch tokens, unique per process
+    unsigned gen = ++s_gen;
+    if (gen == 0) gen = ++s_gen;  // 0 means "no flag"
+    hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n, w, lam,
+                       lam_dev, skip, hp.fixb, fs, gen);
     LoopCtl lc{};
     if (loop) lc = *loop;
     hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, gb, n, lam, lam_dev, st, skip, lc,

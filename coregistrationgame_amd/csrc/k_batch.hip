@@ -370,13 +370,15 @@ __global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restr
     __shared__ double s_eP[BMAXACT * SPER];      // sum of r before it
     const int p = blockIdx.x;
     const int t = threadIdx.x;
-    if (st[p].phase == PH_DONE) return;  // uniform per workgroup
+    // the phase, the stage and the plot's row range load together (one latency, not two)
+    const int ph = st[p].phase, stg = st[p].stage;
+    const int64_t b = so[p], e = so[p + 1];
+    if (ph == PH_DONE) return;  // uniform per workgroup
 #ifdef FICP_BSEL_PROF
     long long bt_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    const double lam = lams[st[p].stage];
+    const double lam = lams[stg];
     const double pe = 2.0 * lam + 1.0;
-    const int64_t b = so[p], e = so[p + 1];
     const long long N = e - b;
     u64 kc[CACHED ? RPT : 1];
     double rc[CACHED && BSEL_RCACHE ? RPT : 1];
@@ -661,11 +663,13 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
     __shared__ double s[8 * (BB / 64)];
     __shared__ int s_last;
     const int p = blockIdx.x / gmax, g = blockIdx.x % gmax;
-    if (st[p].phase != PH_LOOP) {
+    // the phase and the plot's row range load together (one latency, not two)
+    const int ph = st[p].phase;
+    const int64_t b = so[p], e = so[p + 1];
+    if (ph != PH_LOOP) {
         if (g == 0 && threadIdx.x == 0) st[p].apply = 0;
         return;
     }
-    const int64_t b = so[p], e = so[p + 1];
     const long long k = st[p].k;  // k >= 1 in the loop phase
     const int64_t t = st[p].trow;  // the k-th row of the (key, row) order (k_batch_select)
     const unsigned long long tk = st[p].tkey;

@@ -819,10 +819,13 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
 #endif
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
-    if ((a.skip && *a.skip) || (a.reuse && *a.reuse)) return;
+    // the three flags load together (the apply flag's load used to wait for the other two)
+    const int sk = a.skip ? *a.skip : 0, ru = a.reuse ? *a.reuse : 0;
+    const int ap = (APPLY && a.apply_flag) ? *a.apply_flag : 1;
+    if (sk || ru) return;
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     unsigned long long kmin_c = 0, kmax = 0;
-    const double *T = (APPLY && (!a.apply_flag || *a.apply_flag)) ? a.T : nullptr;
+    const double *T = (APPLY && ap) ? a.T : nullptr;
     if (a.cert_block && a.gap && a.warm_c) {
         // block-compacted: certificates first, then the workgroup's uncertified queries
         // packed densely onto its lanes (GS lanes per query when there are few of them)

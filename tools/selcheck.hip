@@ -153,11 +153,19 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, 0, w, hist_blocks(n),
                            (const int *)nullptr, hist_pack(n), (long long *)nullptr);
         CK(hipEventRecord(ev[1], 0));
-        hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam, (const double *)nullptr,
-                           (const int *)nullptr, hist_pack(n).fixb);
-        CK(hipEventRecord(ev[2], 0));
-        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
-                           (const int *)nullptr, FitSrc{});
+        if (it & 2) {  // reps 2, 3 of every 4 (both maps): the library's one-launch form
+            static unsigned gen = 0;
+            CK(hipEventRecord(ev[2], 0));
+            hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, 0, dkey, dorig, dr,
+                               n, w, lam, (const double *)nullptr, (const int *)nullptr,
+                               hist_pack(n).fixb, FitSrc{}, ++gen);
+        } else {
+            hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam,
+                               (const double *)nullptr, (const int *)nullptr, hist_pack(n).fixb);
+            CK(hipEventRecord(ev[2], 0));
+            hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
+                               (const int *)nullptr, FitSrc{});
+        }
         CK(hipEventRecord(ev[3], 0));
         LoopCtl lc{};
         hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, 0, w, gb, n, lam,

@@ -244,15 +244,18 @@ __global__ __launch_bounds__(256) void k_frac_final(const BestRec *tbest, int nb
 __device__ __forceinline__ bool fit_threshold(const FitIn &a, unsigned long long &tk,
                                               int64_t &to) {
     if (!a.key) return true;  // every row selected
+    // k and the threshold pair load together (the pair's loads used to wait for k's)
     const long long k = a.st->k;
+    const unsigned long long tk0 = a.st->tkey;
+    const int64_t to0 = a.st->torig;
     if (k <= 0) {
         tk = 0;
         to = -1;
         return false;
     }
     if (!a.order) {  // threshold pair from the bucketed selection
-        tk = a.st->tkey;
-        to = a.st->torig;
+        tk = tk0;
+        to = to0;
         return false;
     }
     const int64_t tp = (int64_t)a.order[k - 1];
@@ -272,12 +275,15 @@ __device__ void fit_finish(const FitIn &a, const double *part, int nb, int allow
 __global__ __launch_bounds__(FIT_B) void k_fit_sums(FitIn a, double *part, unsigned *ctr,
                                                  int allow_refl, IterState *st,
                                                  const int *skip, double *out8) {
-    if (skip && *skip) return;
+    // the skip flag and the threshold state load together; the rows after the skip test
+    // (a no-op launch, 3 per C3 run, would otherwise read every row)
+    const int sk = skip ? *skip : 0;
     __shared__ double s[256];
     __shared__ int s_last;
     unsigned long long tk = 0;
     int64_t ti = 0;
     const bool all = fit_threshold(a, tk, ti);
+    if (sk) return;
     const int64_t i0 = (int64_t)blockIdx.x * FIT_TILE + threadIdx.x;
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // FIT_I rows per thread in chunks of 4, every load of a chunk in flight at once.  The

@@ -222,6 +222,15 @@ def cpu_info():
     return model, os.cpu_count() or 1, affinity
 
 
+def cgroup_cpus():
+    """CPUs the job's cgroup quota allows (cpu.max 'quota period'), or None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 def _oracle():
     sys.path.insert(0, str(REPO / "oracle"))
     import ficp_oracle
@@ -246,6 +255,11 @@ def cpu_baseline(plot, threads):
     t0 = time.perf_counter()
     _, tr1 = orc.run(plot.source, plot.target, threshold=float("-inf"), max_iterations=1, nthreads=1)
     dt1 = time.perf_counter() - t0
+    # every CPU this process may run on (os.sched_getaffinity; SURVEY.md §8(d) "Threads: 1
+    # and os.cpu_count()"), same sample as `value`
+    t0 = time.perf_counter()
+    _, tra = orc.run(plot.source, plot.target, threshold=float("-inf"), max_iterations=2, nthreads=affinity)
+    dta = time.perf_counter() - t0
     ns, per = [], []
     for n in (2000, 4000, 8000, 16000):
         p = synth.make_plot(n, n, 0.6, 1_000_000 + n, md=3)
@@ -259,9 +273,13 @@ def cpu_baseline(plot, threads):
     return {"value": tr["n_fits"] / dt, "unit": "iterations/s", "cores": threads, "kind": "port",
             "sample": f"C3 plot (1M x 1M, md=3): 2 stages x 2 loop bodies ({tr['n_calls']} NN calls, "
                       f"{tr['n_fits']} fits) in {dt:.2f} s; kd-tree built once, O(N) FRMSD scan, "
-                      f"{threads} OpenMP threads",
+                      f"{threads} OpenMP threads (the job's CPU share, $OMP_NUM_THREADS)",
             "cpu_model": model, "host_logical_cpus": logical, "affinity_cpus": affinity,
-            "threads_all": threads,
+            "threads_job_share": threads, "cgroup_cpu_quota": cgroup_cpus(),
+            "threads_all": affinity,
+            "value_threads_all": tra["n_fits"] / dta,
+            "sample_threads_all": f"same sample as value ({tra['n_fits']} loop bodies) in {dta:.2f} s, "
+                                  f"{affinity} OpenMP threads (every CPU in this process's affinity mask)",
             "value_1thread": tr1["n_fits"] / dt1,
             "sample_1thread": f"same plot, 2 stages x 1 loop body ({tr1['n_calls']} NN calls) in {dt1:.2f} s, 1 thread",
             "literal_samples": {"n": ns, "s_per_iteration": per},
@@ -291,46 +309,79 @@ def cpu_baseline_batch(plots, threads, budget_s=10.0):
                       f"{dt:.2f} s; kd-tree built once per plot, O(N) FRMSD scan, {threads} OpenMP threads"}
 
 
-def host_path_cost(plot, device, reps=3):
+def host_path_cost(plot, device, reps=5):
     """The drop-in call shape of app.py:658-660: FractionalICP(src, tgt).run() from numpy
-    arrays, a new instance (and library context) per call, result back in numpy.  Also
-    the same sequence through the context with its phases timed: constructor copies,
-    context creation, set_target (H2D of the CHM layer + grid build), run (H2D of the
-    source, work order, device loop, caller-order scatter, D2H), and the device loop's
-    own time (ficp_stats.gpu_ms)."""
+    arrays, a new instance per call, result back in numpy.  The instances borrow pooled
+    library contexts (_lib.borrowed), so the first call of a process also pays the pool's
+    context creation and device allocations (ms_first_run) and later calls do not
+    (ms_per_run = median of the later calls).  The breakdown is the facade's own phase
+    stamps of the same calls (FractionalICP.last_stats["host_ms"], the library's
+    "lib_host_ms"): they tile the call, and `unaccounted_ms` is what they miss."""
     from coregistrationgame_amd import FractionalICP
-    md = 3
-    tot = []
-    for _ in range(reps):
+    tot, phases = [], []
+    for _ in range(reps + 1):
         t0 = time.perf_counter()
         icp = FractionalICP(plot.source, plot.target, device=device)
         icp.run()
         tot.append(1e3 * (time.perf_counter() - t0))
-        icp.close()
-    ph = {"copy_ms": [], "context_ms": [], "set_target_ms": [], "run_ms": [], "gpu_loop_ms": []}
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        src = np.array(plot.source, dtype=np.float64, order="C", copy=True)
-        tgt = np.ascontiguousarray(plot.target[:, :md])
-        t1 = time.perf_counter()
-        ctx = _lib.Context(device)
-        t2 = time.perf_counter()
-        ctx.set_target(tgt, md)
-        ctx.synchronize()
-        t3 = time.perf_counter()
-        st = ctx.run(src, [3.0, 0.95], 1e-6, 1000, False)
-        t4 = time.perf_counter()
-        ctx.close()
-        for k, v in (("copy_ms", t1 - t0), ("context_ms", t2 - t1), ("set_target_ms", t3 - t2),
-                     ("run_ms", t4 - t3)):
-            ph[k].append(1e3 * v)
-        ph["gpu_loop_ms"].append(st["gpu_ms"])
-    out = {"ms_per_run": float(np.median(tot)), "ms_first_run": tot[0],
-           "iterations_per_s": None, "breakdown_median_ms": {k: float(np.median(v)) for k, v in ph.items()}}
-    b = out["breakdown_median_ms"]
-    b["run_minus_gpu_loop_ms"] = b["run_ms"] - b["gpu_loop_ms"]
-    out["note"] = ("numpy in/out per call (app.py:658-660); run_minus_gpu_loop = source H2D + work order + "
-                   "result D2H + host overhead")
+        st = icp.last_stats
+        ph = dict(st["host_ms"])
+        lib = st["lib_host_ms"]
+        ph["run.upload_ms"] = lib["upload"]
+        ph["run.loop_ms"] = lib["loop"]
+        ph["run.gpu_loop_ms"] = st["gpu_ms"]
+        ph["run.result_ms"] = lib["result"]
+        ph["run.other_ms"] = ph["run"] - lib["upload"] - lib["loop"] - lib["result"]
+        phases.append(ph)
+        del icp
+    warm = tot[1:]
+    med = {k: float(np.median([p[k] for p in phases[1:]])) for k in phases[1]}
+    top = ("ctor_copies", "copy_source", "borrow", "set_target", "run", "release")
+    tiled = sum(med[k] for k in top)
+    out = {"ms_per_run": float(np.median(warm)), "ms_first_run": tot[0], "runs": len(warm),
+           "breakdown_median_ms": {k.replace("ctor_copies", "ctor_copies_ms").replace("copy_source", "copy_source_ms")
+                                   .replace("borrow", "borrow_ms").replace("set_target", "set_target_ms")
+                                   .replace("release", "release_ms") if not k.startswith("run") else
+                                   (k if k != "run" else "run_ms"): v for k, v in med.items()},
+           "tiled_ms": tiled, "unaccounted_ms": float(np.median(warm)) - tiled,
+           "note": ("numpy in/out per call (app.py:658-660), pooled library context; run_ms = the library's "
+                    "ficp_run (run.upload + run.loop + run.result + run.other; run.gpu_loop is the device "
+                    "loop inside run.loop)")}
+    return out
+
+
+def app_scale_join(device, with_cpu=True):
+    """The production caller's size: one Join per field plot of stand 10 (Data/2014 plots vs
+    the Data/2019 stems, 2-D fallback, app.py:630-661), the 16 real plots kept as data in
+    tests/golden/run_real_stand10.npz.  GPU path: FractionalICP(src, tgt).run() per plot (a
+    new instance each, as join_plot does); CPU path beside it: the pinned C oracle, one
+    thread, same plots.  The reference itself took 2.6-5.7 ms per plot in the build
+    container (it cannot run on the GPU box)."""
+    from coregistrationgame_amd import FractionalICP
+    f = np.load(REPO / "tests" / "golden" / "run_real_stand10.npz")
+    tgt = f["tgt"]
+    plots = [f[f"{int(pid)}/src"] for pid in f["plot_ids"]]
+    FractionalICP(plots[0], tgt, device=device).run()  # pool warm-up (not timed)
+    per = []
+    for rep in range(3):
+        for src in plots:
+            t0 = time.perf_counter()
+            FractionalICP(src, tgt, device=device).run()
+            per.append(1e3 * (time.perf_counter() - t0))
+    out = {"plots": len(plots), "n_trees": [int(len(p)) for p in plots], "n_chm": int(len(tgt)), "match_dims": 2,
+           "gpu_ms_per_join_median": float(np.median(per)), "gpu_ms_per_join_max": float(np.max(per)),
+           "gpu_ms_per_join_min": float(np.min(per))}
+    if with_cpu:
+        orc = _oracle()
+        cpu = []
+        for rep in range(3):
+            for src in plots:
+                t0 = time.perf_counter()
+                orc.run(src, tgt, nthreads=1)
+                cpu.append(1e3 * (time.perf_counter() - t0))
+        out.update({"cpu_oracle_ms_per_join_median": float(np.median(cpu)),
+                    "cpu_oracle_ms_per_join_max": float(np.max(cpu)), "cpu_threads": 1,
+                    "reference_ms_per_join_container": [2.6, 5.7]})
     return out
 
 
@@ -421,10 +472,13 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
         a.free()
     ctx.close()
     if rank == 0 and world == 1 and with_cpu:
-        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(plot, threads)
+        # the host-side measurements first: the CPU baseline's OpenMP threads keep spinning
+        # after their regions and, under the job's CPU quota, slowed the host path ~2x
         if wl == "c3":
             out["host_path"] = host_path_cost(plot, local)
+            out["app_scale_join"] = app_scale_join(local)
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(plot, threads)
     elif out is not None:
         out["cpu_baseline"] = None
     return out

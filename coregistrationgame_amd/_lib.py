@@ -5,10 +5,13 @@ every entry point raises -- there is no CPU fallback in the product.
 """
 from __future__ import annotations
 
+import atexit
+import contextlib
 import ctypes as C
 import os
 import re
 import subprocess
+import threading
 from pathlib import Path
 
 import numpy as np
@@ -47,7 +50,7 @@ class Stats(C.Structure):
         ("k_last", C.c_int64), ("frmsd_last", C.c_double * 2), ("T_total", C.c_double * 9),
         ("gpu_ms", C.c_double), ("max_trace", C.c_int32), ("n_nn_reused", C.c_int32),
         ("trace_k", _ip64), ("trace_frmsd", _dp), ("trace_lambda", _dp), ("trace_T", _dp),
-        ("trace_idx", _ip32),
+        ("trace_idx", _ip32), ("host_ms", C.c_double * 4),
     ]
 
 
@@ -115,6 +118,7 @@ def lib():
         "ficp_create": ([C.c_int, C.POINTER(_vp)], C.c_int),
         "ficp_destroy": ([_vp], None),
         "ficp_set_nn_mode": ([_vp, _i32], C.c_int),
+        "ficp_set_fault": ([_vp, _i32], C.c_int),
         "ficp_profile_enable": ([_vp, _i32], C.c_int),
         "ficp_profile_report": ([_vp, C.c_char_p, _i64], C.c_int),
         "ficp_set_target": ([_vp, _dp, _i64, _i64, _i32], C.c_int),
@@ -214,6 +218,7 @@ class Context:
         self.h = h
         self.md = None
         self.m = 0
+        self.nn_mode = int(nn_mode)
         if nn_mode:
             self.set_nn_mode(nn_mode)
 
@@ -236,6 +241,10 @@ class Context:
 
     def set_nn_mode(self, mode: int):
         _check(lib().ficp_set_nn_mode(self.h, int(mode)))
+
+    def set_fault(self, mask: int):
+        """Test-only fault injection (include/ficp.h ficp_set_fault)."""
+        _check(lib().ficp_set_fault(self.h, int(mask)))
 
     def profile_enable(self, mask: int):
         _check(lib().ficp_profile_enable(self.h, int(mask)))
@@ -438,6 +447,67 @@ class Context:
         return out
 
 
+# ----------------------------------------------------------------- context pool
+# A context owns a HIP stream, pinned host blocks and (after its first run) every device
+# buffer of the path, capacity-cached.  Creating one per FractionalICP (app.py:658 makes a
+# new instance per Join) cost ~7 ms at C3 in allocations (tools/host_probe.py), more than
+# the whole device loop, so the facades borrow contexts from this pool for the duration
+# of each call and give them back.  Contexts are never shared between two calls at once.
+_pool_lock = threading.Lock()
+_pool: dict[tuple[int, int], list[Context]] = {}
+POOL_MAX_IDLE = int(os.environ.get("FICP_POOL_MAX_IDLE", "2"))  # idle contexts kept per (device, mode)
+
+
+def acquire_context(device: int | None = None, nn_mode: int = NN_AUTO) -> Context:
+    dev = default_device() if device is None else int(device)
+    with _pool_lock:
+        idle = _pool.get((dev, int(nn_mode)))
+        if idle:
+            return idle.pop()
+    return Context(dev, nn_mode)
+
+
+def release_context(ctx: Context | None):
+    if ctx is None or not getattr(ctx, "h", None):
+        return
+    with _pool_lock:
+        idle = _pool.setdefault((ctx.device, ctx.nn_mode), [])
+        if len(idle) < POOL_MAX_IDLE:
+            idle.append(ctx)
+            return
+    ctx.close()
+
+
+@contextlib.contextmanager
+def borrowed(device: int | None = None, nn_mode: int = NN_AUTO):
+    """A pooled context for the duration of one call."""
+    ctx = acquire_context(device, nn_mode)
+    try:
+        yield ctx
+    except BaseException:
+        ctx.close()  # a failed call may leave device state behind: do not pool it
+        raise
+    else:
+        release_context(ctx)
+
+
+def drain_pool():
+    """Destroy every idle pooled context (frees their device and pinned memory)."""
+    with _pool_lock:
+        items = [c for lst in _pool.values() for c in lst]
+        _pool.clear()
+    for c in items:
+        c.close()
+
+
+def pool_size() -> int:
+    with _pool_lock:
+        return sum(len(v) for v in _pool.values())
+
+
+atexit.register(drain_pool)  # before the HIP runtime unloads
+
+
 def dist_hist_words() -> int:
     return int(lib().ficp_dist_hist_words())
 
@@ -467,7 +537,8 @@ def _stats_dict(st, keep, n):
     nf = st.n_fits
     out = dict(n_nn_calls=nc, n_nn_reused=st.n_nn_reused, n_fits=nf, iters=(st.iters[0], st.iters[1]), k_last=st.k_last,
                frmsd_last=(st.frmsd_last[0], st.frmsd_last[1]),
-               T_total=np.array(st.T_total[:]).reshape(3, 3), gpu_ms=st.gpu_ms)
+               T_total=np.array(st.T_total[:]).reshape(3, 3), gpu_ms=st.gpu_ms,
+               lib_host_ms=dict(upload=st.host_ms[0], loop=st.host_ms[1], result=st.host_ms[2]))
     if keep:
         m = st.max_trace
         out["k"] = keep["k"][:min(nc, m)].copy()

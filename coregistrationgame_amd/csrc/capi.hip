@@ -59,6 +59,15 @@ int poll_flag(ficp_ctx *c, int *flag, int &v) {
 
 namespace {
 
+// the selection's sticky error bits (k_select.hip ERR_*) by name
+std::string sel_err_text(unsigned e) {
+    std::string s = "fraction selection raised error flag " + std::to_string(e) + " (results invalid):";
+    if (e & 1u) s += " ERR_EMPTY (no candidate row)";
+    if (e & 2u) s += " ERR_CAP (a rank's candidates exceeded the pack capacity)";
+    if (e & 4u) s += " ERR_SPIN (the bounds hand-off of k_sel_bounds_gather never arrived)";
+    return s;
+}
+
 // bounding box of the CHM layer (grid geometry and the fit's pivot), once per target
 // Run the report kernel (device segments -> coherent pinned host memory) and poll its
 // flag: one short host wait instead of hipMemcpyAsync + hipStreamSynchronize.
@@ -346,13 +355,14 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         st->frmsd_last[0] = st->frmsd_last[1] = INFINITY;
         for (int e = 0; e < 9; ++e) st->T_total[e] = (e % 4 == 0) ? 1.0 : 0.0;
         st->gpu_ms = 0.0;
+        for (double &h : st->host_ms) h = 0.0;
     }
     if (n == 0 || c->m == 0) return FICP_OK;  // ficp.py:66-68 + 125-126: nothing moves
     if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large (max 2^30 - 1)");
     CHK(ensure_work(c, n));
     CHK(ensure_bbox(c));
     uint32_t *tflag = sort_timeout_flag(c->sort_tmp.p, n);
-    HIPCHK(launch_run_start(tflag, &c->h_rep->t[0], c->stream));
+    HIPCHK(launch_run_start(tflag, &c->h_rep->t[0], c->stream, sel_err_word(c->sel_tmp.p, n)));
     double *wx = sx, *wy = sy;
     const double *wz = sz;
     const uint32_t *worig = nullptr;
@@ -445,7 +455,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
                                  &dst->lam_cur, range_ptr(c), nn_range_parts(n, c->m, use_grid(c, n)),
                                  c->sel_tmp.p, dst, &dst->done, fused ? &lc : nullptr,
                                  fused ? &c->h_flags[slot] : nullptr, c->stream,
-                                 (fused && fuse_fit) ? &fsrc : nullptr));
+                                 (fused && fuse_fit) ? &fsrc : nullptr, c->fault));
         }
         if (!fused) {
             if (tidx)
@@ -537,7 +547,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", c->h_misc[0]);
     c->sel_levels = c->h_misc[2];
     c->sel_radix = c->h_misc[3];
-    if (c->h_misc[1]) return fail(FICP_EHIP, "fraction selection raised error flag %u", c->h_misc[1]);
+    if (c->h_misc[1]) return fail(FICP_EHIP, "%s", sel_err_text(c->h_misc[1]).c_str());
     return FICP_OK;
 }
 
@@ -660,6 +670,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->bp,     &c->dz2,        &c->gap,      &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
                       &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp, &c->bs_tmp2};
     for (DevBuf *b : bufs) b->release();
+    c->pin.release();
     batch_release(c->batch);
     c->batch = nullptr;
     for (auto &r : c->recs) {
@@ -677,6 +688,12 @@ void ficp_destroy(ficp_ctx *c) {
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+int ficp_set_fault(ficp_ctx *c, int32_t mask) {
+    if (!c) return fail(FICP_EINVAL, "null context");
+    c->fault = mask;
+    return FICP_OK;
 }
 
 int ficp_set_nn_mode(ficp_ctx *c, int32_t mode) {
@@ -767,9 +784,8 @@ int ficp_nn(ficp_ctx *c, const double *src, int64_t n, int64_t ld, int32_t *idx,
     CHK(ensure_work(c, n));
     CHK(nn_call(c, c->sx.as<double>(), c->sy.as<double>(), c->sz.as<double>(), n, nullptr,
                 false));
-    HIPCHK(hipMemcpyAsync(idx, c->idx.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(dist, c->dist.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-    return sync(c);
+    CHK(d2h_staged(c, idx, c->idx.p, (size_t)n * 4));
+    return d2h_staged(c, dist, c->dist.p, (size_t)n * 8);
 }
 
 int ficp_optimal_fraction(ficp_ctx *c, const double *src, int64_t lds, const double *corr,
@@ -846,13 +862,16 @@ int ficp_argsort(ficp_ctx *c, const double *d, int64_t n, int64_t *order) {
     HIPCHK(launch_sort(c->key.as<unsigned long long>(), nullptr, n, range_ptr(c),
                        c->order.as<uint32_t>(), nullptr, nullptr, c->sort_tmp.p, nullptr,
                        c->stream));
-    uint32_t tf = 0;
-    HIPCHK(hipMemcpyAsync(&tf, tflag, 4, hipMemcpyDeviceToHost, c->stream));
-    std::vector<uint32_t> tmp((size_t)n);
-    HIPCHK(hipMemcpyAsync(tmp.data(), c->order.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    CHK(c->pin.ensure((size_t)n * 4 + 64));
+    uint32_t *tmp = c->pin.as<uint32_t>();
+    uint32_t *tf = tmp + ((n + 15) & ~(int64_t)15);
+    HIPCHK(hipMemcpyAsync(tf, tflag, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(tmp, c->order.p, n * 4, hipMemcpyDeviceToHost, c->stream));
     CHK(sync(c));
-    if (tf) return fail(FICP_EHIP, "sort look-back timed out (results invalid)");
-    for (int64_t i = 0; i < n; ++i) order[i] = tmp[(size_t)i];
+    if (*tf) return fail(FICP_EHIP, "sort look-back timed out (results invalid)");
+    host_parallel(n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) order[i] = tmp[i];
+    });
     return FICP_OK;
 }
 
@@ -893,8 +912,7 @@ int ficp_apply_xy(ficp_ctx *c, const double *pts, int64_t n, int64_t ld, const d
     HIPCHK(launch_apply_xy(c->sx.as<double>(), c->sy.as<double>(), n, dT, c->stream));
     HIPCHK(launch_interleave_xy(c->sx.as<double>(), c->sy.as<double>(), n, c->stage2.as<double>(),
                                 c->stream));
-    HIPCHK(hipMemcpyAsync(out_xy, c->stage2.p, n * 16, hipMemcpyDeviceToHost, c->stream));
-    return sync(c);
+    return d2h_staged(c, out_xy, c->stage2.p, (size_t)n * 16);
 }
 
 int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
@@ -907,19 +925,26 @@ int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
     if (n == 0 || c->m == 0)
         return run_core(c, nullptr, nullptr, nullptr, 0, nstages, lambdas, threshold,
                         max_iterations, allow_reflection, stats);
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = clk::now();
     CHK(upload_rows(c, src, n, ld, c->md, c->sx, c->sy, &c->sz));
+    const auto t1 = clk::now();
     CHK(run_core(c, c->sx.as<double>(), c->sy.as<double>(),
                  c->md == 3 ? c->sz.as<double>() : nullptr, n, nstages, lambdas, threshold,
                  max_iterations, allow_reflection, stats));
+    const auto t2 = clk::now();
     CHK(c->stage2.ensure(n * 16));
     HIPCHK(launch_interleave_xy(c->sx.as<double>(), c->sy.as<double>(), n, c->stage2.as<double>(),
                                 c->stream));
-    std::vector<double> xy((size_t)n * 2);
-    HIPCHK(hipMemcpyAsync(xy.data(), c->stage2.p, n * 16, hipMemcpyDeviceToHost, c->stream));
-    CHK(sync(c));
-    for (int64_t i = 0; i < n; ++i) {  // columns 0,1 only; every other column untouched
-        src[i * ld] = xy[2 * i];
-        src[i * ld + 1] = xy[2 * i + 1];
+    CHK(d2h_xy_columns(c, c->stage2.as<double>(), n, src, ld));
+    if (stats) {
+        stats->host_ms[0] = ms(t0, t1);
+        stats->host_ms[1] = ms(t1, t2);
+        stats->host_ms[2] = ms(t2, clk::now());
+        stats->host_ms[3] = 0.0;
     }
     return FICP_OK;
 }
@@ -1096,7 +1121,7 @@ int ficp_select_fit_device(ficp_ctx *c, const double *x, const double *y, int64_
         CHK(sync(c));
         c->sel_levels = ss[1];
         c->sel_radix = ss[2];
-        if (ss[0]) return fail(FICP_EHIP, "fraction selection raised error flag %u", ss[0]);
+        if (ss[0]) return fail(FICP_EHIP, "%s", sel_err_text(ss[0]).c_str());
     }
     return FICP_OK;
 }
@@ -1397,8 +1422,8 @@ int ficp_dist_end(ficp_ctx *c, ficp_stats *st) {
     const IterState &h = c->h_rep->st;
     if (!h.done) return fail(FICP_EHIP, "distributed ICP loop did not finish");
     if (c->h_rep->misc[1] & 2u)
-        return fail(FICP_EHIP, "a rank's selection candidates exceeded the pack capacity");
-    if (c->h_rep->misc[1]) return fail(FICP_EHIP, "fraction selection raised error flag %u", c->h_rep->misc[1]);
+        return fail(FICP_EHIP, "ERR_CAP: a rank's selection candidates exceeded the pack capacity");
+    if (c->h_rep->misc[1]) return fail(FICP_EHIP, "%s", sel_err_text(c->h_rep->misc[1]).c_str());
     if (st) {
         st->n_nn_calls = h.n_nn;
         st->n_nn_reused = h.n_reuse;
@@ -1410,6 +1435,7 @@ int ficp_dist_end(ficp_ctx *c, ficp_stats *st) {
         st->frmsd_last[1] = h.frmsd_last[1];
         memcpy(st->T_total, h.Ttot, sizeof st->T_total);
         st->gpu_ms = 0.0;
+        for (double &hm : st->host_ms) hm = 0.0;
         const int nc = std::min(std::min(h.n_nn, st->max_trace), kDistTrace);
         if (nc > 0 && st->trace_k) {
             HIPCHK(hipMemcpyAsync(st->trace_k, c->tr_k.p, (size_t)nc * 8, hipMemcpyDeviceToHost,

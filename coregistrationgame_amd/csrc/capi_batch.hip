@@ -316,14 +316,7 @@ int ficp_run_batch(ficp_ctx *c, int32_t nplots, const int64_t *src_off, double *
     CHK(b.stage.ensure(n * 16));
     HIPCHK(launch_interleave_xy(b.sx.as<double>(), b.sy.as<double>(), n, b.stage.as<double>(),
                                 c->stream));
-    std::vector<double> xy((size_t)n * 2);
-    HIPCHK(hipMemcpyAsync(xy.data(), b.stage.p, n * 16, hipMemcpyDeviceToHost, c->stream));
-    CHK(sync(c));
-    for (int64_t i = 0; i < n; ++i) {  // columns 0,1 only
-        src[i * lds] = xy[2 * i];
-        src[i * lds + 1] = xy[2 * i + 1];
-    }
-    return FICP_OK;
+    return d2h_xy_columns(c, b.stage.as<double>(), n, src, lds);
 }
 
 int ficp_run_batch_device(ficp_ctx *c, int32_t nplots, const int64_t *src_off, double *x,

@@ -9,9 +9,12 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <string.h>
+
 #include <algorithm>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace ficp_capi {
@@ -76,6 +79,38 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging (capacity-cached like DevBuf).  A D2H copy into pageable memory ran
+// at ~8 GB/s on the box (24 MB in 3 ms, tools/host_probe.py); into pinned memory at the
+// link rate, so results come back through this buffer.  (H2D from pageable memory already
+// ran at the pinned rate, 24 MB in 0.44 ms, and is left direct.)
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return FICP_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(FICP_ENOMEM, "hipHostMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        cap = want;
+        return FICP_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T *as() const {
+        return (T *)p;
+    }
+};
+
 enum ProfClass { P_NN = 1, P_SORT = 2, P_FRAC = 4, P_FIT = 8, P_GRID = 16, P_MISC = 32 };
 
 struct ProfRec {
@@ -104,6 +139,7 @@ struct ficp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int nn_mode = 0;
+    int fault = 0;  // test-only fault injection mask (ficp_set_fault)
 
     // target (CHM layer)
     bool has_target = false;
@@ -160,6 +196,8 @@ struct ficp_ctx {
     LoopCtl dist_lc{};
     DevBuf gorig;                      // caller index (row0 + local) of each work-order row
     DevBuf drange;                     // int64 range words of the local rows (top bit flipped)
+
+    PinBuf pin;  // pinned staging of results on their way to the caller's (pageable) arrays
 };
 
 namespace ficp_capi {
@@ -256,6 +294,58 @@ inline int upload_rows(ficp_ctx *c, const double *rows, int64_t n, int64_t ld, i
                                c1.as<double>(), c2 ? c2->as<double>() : nullptr, c->stream));
     return FICP_OK;
 }
+// f(i0, i1) over [0, n) on up to 8 host threads (large host-side copies of results)
+template <typename F>
+inline void host_parallel(int64_t n, F f) {
+    const int64_t per_min = 1 << 17;
+    const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, n / per_min));
+    if (nt <= 1) {
+        f((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t per = (n + nt - 1) / nt;
+    for (int t = 1; t < nt; ++t) {
+        const int64_t a = std::min(n, t * per), b = std::min(n, a + per);
+        th.emplace_back([=]() { f(a, b); });
+    }
+    f(0, std::min(n, per));
+    for (auto &x : th) x.join();
+}
+
+// device bytes -> the caller's host memory through the pinned staging buffer
+inline int d2h_staged(ficp_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!bytes) return FICP_OK;
+    CHK(c->pin.ensure(bytes));
+    HIPCHK(hipMemcpyAsync(c->pin.p, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    const char *s = c->pin.as<const char>();
+    char *d = (char *)dst;
+    host_parallel((int64_t)bytes, [&](int64_t a, int64_t b) { memcpy(d + a, s + a, (size_t)(b - a)); });
+    return FICP_OK;
+}
+
+// interleaved device XY (n x 2) -> columns 0 and 1 of the caller's (n x ld) rows; every
+// other column is left untouched (ficp.py:114-118)
+inline int d2h_xy_columns(ficp_ctx *c, const double *xy_dev, int64_t n, double *dst, int64_t ld) {
+    if (n <= 0) return FICP_OK;
+    CHK(c->pin.ensure((size_t)n * 16));
+    HIPCHK(hipMemcpyAsync(c->pin.p, xy_dev, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
+    CHK(sync(c));
+    const double *xy = c->pin.as<const double>();
+    host_parallel(n, [&](int64_t a, int64_t b) {
+        if (ld == 2) {
+            memcpy(dst + 2 * a, xy + 2 * a, (size_t)(b - a) * 16);
+            return;
+        }
+        for (int64_t i = a; i < b; ++i) {
+            dst[i * ld] = xy[2 * i];
+            dst[i * ld + 1] = xy[2 * i + 1];
+        }
+    });
+    return FICP_OK;
+}
+
 // Wait for a flag that a kernel stores (system scope) into coherent pinned memory; -1 =
 // not yet written.  Ends with an error when the stream fails or drains without it.
 int poll_flag(ficp_ctx *c, int *flag, int &v);

@@ -349,7 +349,8 @@ struct ReportSeg {
 hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg &c, int *flag,
                          unsigned long long *t_end, hipStream_t s);
 // zero the sort timeout flag and stamp the device clock (100 MHz) into *t0 (host)
-hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s);
+hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s,
+                            unsigned *selerr = nullptr);
 
 // grid build (k_grid_nn.hip)
 // bbox of (x, y) -> out4 {xmin, xmax, ymin, ymax}; with ox, also copies x, y (z) there
@@ -486,7 +487,12 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
                          int64_t n, double lam, const double *lam_dev, unsigned long long *range,
                          int64_t range_parts, void *tmp, IterState *st, const int *skip,
                          const LoopCtl *loop, int *host_flag, hipStream_t s,
-                         const FitSrc *fit = nullptr);
+                         const FitSrc *fit = nullptr, int fault = 0);
+// the selection's sticky error word inside its workspace (k_run_start resets it per run)
+unsigned *sel_err_word(void *tmp, int64_t n);
+// test-only fault injection (ficp_set_fault): block 0 of k_sel_bounds_gather publishes a
+// wrong token, so every gather block times out (ERR_SPIN)
+constexpr int FICP_FAULT_SPIN = 1;
 
 // selection + fit + apply (k_select_fit.hip)
 int64_t frac_tmp_bytes(int64_t n);

@@ -60,16 +60,19 @@ __global__ __launch_bounds__(256) void k_trace_idx(const IterState *st, const in
 // run start: zero the sort's timeout flag and stamp the device clock (100 MHz) into
 // coherent host memory; the report kernel stamps the end (ficp_stats::gpu_ms without
 // event records, each of which left ~5 us of idle queue)
-__global__ void k_run_start(uint32_t *tflag, unsigned long long *t0) {
+__global__ void k_run_start(uint32_t *tflag, unsigned long long *t0, unsigned *selerr) {
     if (threadIdx.x == 0) {
         __hip_atomic_exchange(tflag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the selection's sticky error bits are per run (a failed run leaves no poison)
+        if (selerr) __hip_atomic_exchange(selerr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s) {
-    hipLaunchKernelGGL(k_run_start, dim3(1), dim3(64), 0, s, tflag, t0);
+hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s,
+                            unsigned *selerr) {
+    hipLaunchKernelGGL(k_run_start, dim3(1), dim3(64), 0, s, tflag, t0, selerr);
     return hipGetLastError();
 }
 

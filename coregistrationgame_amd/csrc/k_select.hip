@@ -956,14 +956,28 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
     const BMap bm = w.ctl->map;  // k_sel_hist's (an earlier launch)
     const int lane = threadIdx.x & 63;
     const int64_t base = (int64_t)blk * (GT * GI) + threadIdx.x;
-    // all loads first (no load waits behind the append's atomic)
+    // all loads first (no load waits behind the append's atomic).  With the fused fit the
+    // rows' pairs load here too, before the bounds wait: which rows lie below the
+    // candidates is known only after it, and loaded behind it the pairs cost ~7 us
     u64 kk[GI];
     double rr[GI];
+    double fxs[GI], fys[GI], fxt[GI], fyt[GI];
 #pragma unroll
     for (int q = 0; q < GI; ++q) {
         const int64_t i = base + (int64_t)q * GT;
         kk[q] = i < n ? key[i] : 0ULL;
         rr[q] = i < n ? r[i] : 0.0;
+    }
+    if (fs.on) {
+#pragma unroll
+        for (int q = 0; q < GI; ++q) {
+            const int64_t i = base + (int64_t)q * GT;
+            const bool ok = i < n;
+            fxs[q] = ok ? fs.sx[i] : 0.0;
+            fys[q] = ok ? fs.sy[i] : 0.0;
+            fxt[q] = ok ? fs.cx[i] : 0.0;
+            fyt[q] = ok ? fs.cy[i] : 0.0;
+        }
     }
     if (sk) return;
     int b0, b1;
@@ -975,17 +989,22 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
             // (2^20 polls, >= ~30 ms), raise ERR_SPIN (the host fails the run), no hang
             unsigned it = 0;
             u64 v;
+            bool late = false;
             while (((v = __hip_atomic_load(&w.ctl->bpub, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT)) >> 32) != gen) {
                 if (++it == (1u << 20)) {
                     __hip_atomic_fetch_or(&w.ctl->err, ERR_SPIN, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
+                    late = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            s_b[0] = (int)((v >> 16) & 0xffffu);
-            s_b[1] = (int)(v & 0xffffu);
+            // a timed-out block takes an empty range: no row below, no candidate, so it
+            // appends nothing at a ccount block 0 may not have reset yet (the run fails
+            // with ERR_SPIN; k_sel_final ends the device loop)
+            s_b[0] = late ? 0 : (int)((v >> 16) & 0xffffu);
+            s_b[1] = late ? -1 : (int)(v & 0xffffu);
         }
         __syncthreads();
         b0 = s_b[0];
@@ -1040,6 +1059,8 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
             if ((inm >> q) & 1u) {
                 const int64_t i = base + (int64_t)q * GT;
                 const unsigned p = pos + (unsigned)__popcll(masks[q] & lt);
+                if ((int64_t)p >= n) continue;  // the buffers hold n candidates (never hit
+                                                // unless ccount was stale: ERR_SPIN)
                 w.ka[p] = kk[q];
                 w.oa[p] = orig ? orig[i] : (uint32_t)i;
                 w.ra[p] = rr[q];
@@ -1052,21 +1073,8 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (fs.on) {
 #pragma unroll
-        for (int q0 = 0; q0 < GI; q0 += 4) {
-            double xs[4], ys[4], xt[4], yt[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t i = base + (int64_t)(q0 + u) * GT;
-                const bool on = (bel >> (q0 + u)) & 1u;
-                xs[u] = on ? fs.sx[i] : 0.0;
-                ys[u] = on ? fs.sy[i] : 0.0;
-                xt[u] = on ? fs.cx[i] : 0.0;
-                yt[u] = on ? fs.cy[i] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if ((bel >> (q0 + u)) & 1u) fit_add(c, xs[u], ys[u], xt[u], yt[u], fs.px, fs.py);
-        }
+        for (int q = 0; q < GI; ++q)
+            if ((bel >> q) & 1u) fit_add(c, fxs[q], fys[q], fxt[q], fyt[q], fs.px, fs.py);
     }
     // fixed tree: wave butterfly, then the waves in order
 #pragma unroll
@@ -1109,14 +1117,15 @@ __global__ __launch_bounds__(GT) void k_sel_bounds_gather(const u64 *key, const 
                                                           const double *r, int64_t n, SelWS w,
                                                           double lam, const double *lam_dev,
                                                           const int *skip, int fixb, FitSrc fs,
-                                                          unsigned gen) {
+                                                          unsigned gen, unsigned pub_gen) {
     if (blockIdx.x == 0) {
         const unsigned bb = bounds_body(w, n, lam, lam_dev, skip, fixb);
         if (bb != kBoundsSkipped && threadIdx.x == 0) {
             // thread 0 reset ccount (atomic) inside bounds_body: drain it before the flag,
-            // so no gather block's append can precede the reset
+            // so no gather block's append can precede the reset.  (pub_gen == gen except
+            // under the test-only fault injection FICP_FAULT_SPIN, ficp_set_fault)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&w.ctl->bpub, ((u64)gen << 32) | bb, __ATOMIC_RELAXED,
+            __hip_atomic_store(&w.ctl->bpub, ((u64)pub_gen << 32) | bb, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
@@ -1214,6 +1223,7 @@ constexpr int X_T = X_B + 256 * 4;
 constexpr int X_END = X_T + 256 * 4;
 constexpr int SMEM = L_END > R_END ? (L_END > X_END ? L_END : X_END) : (R_END > X_END ? R_END : X_END);
 static_assert(SMEM <= 150 * 1024, "final kernel LDS");
+static_assert(HT * 56 <= SMEM, "final_small's LDS (keys, r, orig, pos, fused-fit pairs)");
 
 // (a) c <= CAPT candidates: bucket sort in LDS, exact prefix sums, first minimum.  RL:
 // r is staged in LDS too (c <= CAP); otherwise (c <= CAP2) r is read from global memory
@@ -1379,15 +1389,26 @@ __device__ void final_small(const Cand &src, unsigned c, const FinalIn &in, unsi
     double *lr = (double *)(sm + HT * 8);
     uint32_t *lo = (uint32_t *)(sm + HT * 16);
     uint16_t *pos = (uint16_t *)(sm + HT * 20);
+    double *lf = (double *)(sm + HT * 24);  // fused fit: the candidate's pair [4][HT]
     const unsigned t = threadIdx.x;
     u64 k = 0;
     uint32_t o = 0;
     if (t < c) {
         k = src.k[t];
         o = src.o[t];
+        const double rv = src.r[t];
+        if (in.fs.on) {
+            // the pair of every candidate loads now (overlapping the ranking below); the
+            // sums then run over LDS in sorted order (deterministic), not after the argmin
+            const uint32_t w = src.p[t];
+            lf[t] = in.fs.sx[w];
+            lf[HT + t] = in.fs.sy[w];
+            lf[2 * HT + t] = in.fs.cx[w];
+            lf[3 * HT + t] = in.fs.cy[w];
+        }
         lk[t] = k;
         lo[t] = o;
-        lr[t] = src.r[t];
+        lr[t] = rv;
     }
     __syncthreads();
     if (t < c) {
@@ -1412,7 +1433,10 @@ __device__ void final_small(const Cand &src, unsigned c, const FinalIn &in, unsi
     blk_argmin(bf, bk, scr);
     if (in.fs.on && bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
         double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if ((long long)t < bk - in.K0) fit_row(cf, in.fs, src.p[pos[t]]);
+        if ((long long)t < bk - in.K0) {
+            const unsigned e = pos[t];
+            fit_add(cf, lf[e], lf[HT + e], lf[2 * HT + e], lf[3 * HT + e], in.fs.px, in.fs.py);
+        }
         blk_sum8_add(cf, in.fsum, scr);
     }
     if (t == 0) {
@@ -1852,6 +1876,8 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     const double lamv = lam_dev ? *lam_dev : lam;
     unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned errv = __hip_atomic_fetch_or(&w.ctl->err, 0u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
     const long long kbase = w.ctl->kbase;
     const double Ub = w.ctl->U;
     if (sk) {
@@ -1924,6 +1950,12 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     SELPROF(5);
     if (t == 0) {
         if (fuse_loop) loop_step(&s_st, lc);
+        // a sticky selection error (ERR_SPIN, ERR_CAP): this call's result is invalid, so
+        // the device loop ends here and the host reports the flag (no further calls)
+        if (fuse_loop && errv) {
+            s_st.phase = PH_DONE;
+            loop_set_flags(s_st);
+        }
         // fused fit: T of the next loop body from this selection (k_fit_sums' work)
         if (fs.on && !s_st.no_fit && s_st.k > 0)
             fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
@@ -2021,6 +2053,8 @@ __global__ __launch_bounds__(HT) void k_sel_unpack(SelWS w, const long long *all
 
 int64_t sel_tmp_bytes(int64_t n) { return carve_bytes(n, nullptr, nullptr); }
 
+unsigned *sel_err_word(void *tmp, int64_t n) { return &carve(tmp, n).ctl->err; }
+
 int sel_hist_words() { return 2 * NB; }
 
 hipError_t launch_select_dist_hist(const unsigned long long *key, const double *r, int64_t n,
@@ -2080,7 +2114,8 @@ hipError_t launch_select_stats(void *tmp, int64_t n, unsigned *out3, hipStream_t
 hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, const double *r,
                          int64_t n, double lam, const double *lam_dev, unsigned long long *range,
                          int64_t range_parts, void *tmp, IterState *st, const int *skip,
-                         const LoopCtl *loop, int *host_flag, hipStream_t s, const FitSrc *fit) {
+                         const LoopCtl *loop, int *host_flag, hipStream_t s, const FitSrc *fit,
+                         int fault) {
     if (n <= 0) return hipSuccess;
     const SelWS w = carve(tmp, n);
     const HistPack hp = hist_pack(n);
@@ -2094,8 +2129,9 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     static std::atomic<unsigned> s_gen{0};  // launch tokens, unique per process
     unsigned gen = ++s_gen;
     if (gen == 0) gen = ++s_gen;  // 0 means "no flag"
+    const unsigned pub = (fault & FICP_FAULT_SPIN) ? (gen ^ 0x40000000u) : gen;
     hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n, w, lam,
-                       lam_dev, skip, hp.fixb, fs, gen);
+                       lam_dev, skip, hp.fixb, fs, gen, pub);
     LoopCtl lc{};
     if (loop) lc = *loop;
     hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, gb, n, lam, lam_dev, st, skip, lc,

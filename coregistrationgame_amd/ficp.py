@@ -19,6 +19,8 @@ There is no CPU fallback: without the library or a GPU the methods raise.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
 from . import _lib
@@ -46,8 +48,10 @@ class FractionalICP:
         Extra keyword-only options of this engine: ``device`` (GPU ordinal; default
         $FICP_DEVICE, $LOCAL_RANK or 0) and ``nn_mode`` ("auto", "brute", "grid").
         """
+        t0 = time.perf_counter()
         self.source = np.array(source, dtype=float)
         self.target = np.array(target, dtype=float)
+        self._ctor_ms = 1e3 * (time.perf_counter() - t0)  # host-path accounting (last_stats)
 
         if self.source.ndim != 2 or self.target.ndim != 2:
             raise ValueError("source and target must be 2D arrays (N, D).")
@@ -60,18 +64,16 @@ class FractionalICP:
         self.device = device
         self.nn_mode = {"auto": _lib.NN_AUTO, "brute": _lib.NN_BRUTE, "grid": _lib.NN_GRID}[nn_mode]
         self.last_stats = None
-        self._ctx = None
 
     # ----------------- engine context -----------------
-    def _context(self) -> _lib.Context:
-        if self._ctx is None:
-            self._ctx = _lib.Context(self.device, self.nn_mode)
-        return self._ctx
+    def _borrow(self):
+        """A pooled library context for one call (_lib.borrowed): the instance holds no
+        device state between calls, so a new instance per Join (app.py:658) costs no
+        context creation or device allocation."""
+        return _lib.borrowed(self.device, self.nn_mode)
 
     def close(self):
-        if self._ctx is not None:
-            self._ctx.close()
-            self._ctx = None
+        """Kept for callers that release explicitly; the instance holds nothing."""
 
     # ----------------- helpers (ficp.py:47-51) -----------------
     def _xy(self, pts):
@@ -89,7 +91,8 @@ class FractionalICP:
         b = self._xyz_or_xy(np.asarray(corresponding_targets, dtype=float))
         if a.shape != b.shape:
             raise ValueError(f"operands could not be broadcast together with shapes {a.shape} {b.shape}")
-        return self._context().frmsd(a, b, num_elements, self.match_dims, fraction, self.lambda_val)
+        with self._borrow() as ctx:
+            return ctx.frmsd(a, b, num_elements, self.match_dims, fraction, self.lambda_val)
 
     def get_n_first_elements(self, num_elements, distances):
         """argsort(distances)[:num_elements] -- ficp.py:62-63.
@@ -100,7 +103,8 @@ class FractionalICP:
         d = np.asarray(distances, dtype=float).ravel()
         if d.size == 0:
             return np.zeros(0, dtype=np.intp)
-        return self._context().argsort(d)[:num_elements].astype(np.intp, copy=False)
+        with self._borrow() as ctx:
+            return ctx.argsort(d)[:num_elements].astype(np.intp, copy=False)
 
     def find_correspondences(self, source, target):
         """Exact 1-NN of every source row in the target -- ficp.py:65-71.
@@ -111,9 +115,10 @@ class FractionalICP:
             empty_corr = np.empty((0, target.shape[1]))
             return empty_corr, np.array([])
         md = self.match_dims
-        ctx = self._context()
-        ctx.set_target(np.asarray(target, dtype=float)[:, :md], md)
-        idx, dist = ctx.nn(np.asarray(source, dtype=float)[:, :md])
+        with self._borrow() as ctx:
+            # rows go over with their leading dimension; the library reads md columns
+            ctx.set_target(np.asarray(target, dtype=float), md)
+            idx, dist = ctx.nn(np.asarray(source, dtype=float))
         return target[idx], dist
 
     def find_optimal_fraction(self, corresponding_targets, distances):
@@ -129,8 +134,8 @@ class FractionalICP:
         md = self.match_dims
         src = self._xyz_or_xy(self.source[:n])
         corr = self._xyz_or_xy(np.asarray(corresponding_targets, dtype=float)[:n])
-        frac, k = self._context().optimal_fraction(src, corr, d, N, md, self.lambda_val)
-        return frac, k
+        with self._borrow() as ctx:
+            return ctx.optimal_fraction(src, corr, d, N, md, self.lambda_val)
 
     # ----------------- rigid 2D transform -----------------
     def compute_optimal_transform_2d(self, source_subset, target_subset):
@@ -144,27 +149,44 @@ class FractionalICP:
             T = np.eye(3)
             T[:2, 2] = np.nan
             return T
-        return self._context().fit_rigid2d(X, Y, self.allow_reflection)
+        with self._borrow() as ctx:
+            return ctx.fit_rigid2d(X, Y, self.allow_reflection)
 
     def apply_transform_2d_xy_only(self, points, T):
         """Apply a 2D rigid transform to XY only -- ficp.py:112-119."""
         out = points.copy()
         if len(points) == 0:
             return out
-        xy_t = self._context().apply_xy(np.asarray(points, dtype=float)[:, :2], np.asarray(T, dtype=float))
+        with self._borrow() as ctx:
+            xy_t = ctx.apply_xy(np.asarray(points, dtype=float), np.asarray(T, dtype=float))
         out[:, :2] = xy_t
         return out
 
     # ----------------- ICP loop -----------------
     def _stages(self, lambdas, trace=False, trace_idx=False):
-        src = np.array(self.source, dtype=np.float64, order="C", copy=True)
-        if len(src) == 0 or len(self.target) == 0:
+        if len(self.source) == 0 or len(self.target) == 0:
             self.last_stats = dict(n_nn_calls=0, n_fits=0, iters=(0, 0))
             return self.source
-        ctx = self._context()
-        ctx.set_target(self._xyz_or_xy(self.target), self.match_dims)
-        self.last_stats = ctx.run(src, lambdas, self.threshold, self.max_iterations, self.allow_reflection,
-                                  trace=trace, trace_idx=trace_idx)
+        # the run moves a fresh array (ficp.py:114,135 replace self.source; the array the
+        # constructor made is never written), columns 0-1 only
+        t0 = time.perf_counter()
+        src = np.array(self.source, dtype=np.float64, order="C", copy=True)
+        t1 = time.perf_counter()
+        with self._borrow() as ctx:
+            t2 = time.perf_counter()
+            # the CHM rows go over with their leading dimension (no column-slice copy)
+            ctx.set_target(np.ascontiguousarray(self.target, dtype=np.float64), self.match_dims)
+            t3 = time.perf_counter()
+            st = ctx.run(src, lambdas, self.threshold, self.max_iterations, self.allow_reflection,
+                         trace=trace, trace_idx=trace_idx)
+            t4 = time.perf_counter()
+        t5 = time.perf_counter()
+        # where the call's host time went (ms): the constructor's copies, this copy, the
+        # pool, the CHM upload + grid inputs, the library run (its own phases in
+        # st["lib_host_ms"], the device loop in st["gpu_ms"]) and the release
+        st["host_ms"] = dict(ctor_copies=self._ctor_ms, copy_source=1e3 * (t1 - t0), borrow=1e3 * (t2 - t1),
+                             set_target=1e3 * (t3 - t2), run=1e3 * (t4 - t3), release=1e3 * (t5 - t4))
+        self.last_stats = st
         self.source = src
         return self.source
 

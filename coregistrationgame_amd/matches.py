@@ -44,13 +44,10 @@ def remove_matches_arrays(plot, chm, min_dist_percent=15, *, device=None) -> np.
     # chm_plot.py:236-244 tests np.isnan only: an infinite height keeps the 3-D search
     use_3d = bool(not np.isnan(plot[:, 2]).any() and not np.isnan(chm[:, 2]).any())
     md = 3 if use_3d else 2
-    ctx = _lib.Context(device, _lib.NN_GRID)
-    try:
+    with _lib.borrowed(device, _lib.NN_GRID) as ctx:
         ctx.set_target(np.ascontiguousarray(chm[:, :md]), md)
         return ctx.remove_matches(np.ascontiguousarray(plot[:, :md]),
                                   thresholds(plot[:, 2], use_3d, min_dist_percent))
-    finally:
-        ctx.close()
 
 
 def _height(t) -> float:

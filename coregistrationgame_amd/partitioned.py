@@ -118,8 +118,12 @@ def merge_local(d2s, idxs):
 class PartitionedFICP:
     # source mode: candidates one rank may contribute per NN call: at least CAPD, and 1/64
     # of the rank's largest row range (a stage's first call, on the uniform bucket map, can
-    # leave ~1e-3 of the rows as candidates: 8M rows on one rank overflowed 8192).  More
-    # than that raises FicpError (ERR_CAP); split the rows over more shards.
+    # leave ~1e-3 of the rows as candidates: 8M rows on one rank overflowed 8192).  A call
+    # whose candidates exceed that on any rank (flat FRMSD curves near lambda = 1, tied
+    # distances) is not an error: every rank sees the same merged overflow bit, the device
+    # loop stops at that call on every rank, and the run starts over with packs that hold
+    # every row of a rank (capd = the largest row range), where the final selection's
+    # refinement levels / chunked scan take any candidate count (exact, as one GPU).
     CAPD = 8192
     CAPD_FRAC = 64
 
@@ -194,7 +198,7 @@ class PartitionedFICP:
         else:
             hw = _lib.dist_hist_words()
             n_max = max(c for _, c in parts)
-            self.capd = max(self.CAPD, -(-n_max // self.CAPD_FRAC))
+            self.capd = min(n_max, max(self.CAPD, -(-n_max // self.CAPD_FRAC)))
             res.update(sums=[torch.zeros(8, dtype=f64, device=dev) for _ in mine],
                        range2=[torch.zeros(2, dtype=i64, device=dev) for _ in mine],
                        hist=[torch.zeros(hw, dtype=i64, device=dev) for _ in mine],
@@ -263,6 +267,20 @@ class PartitionedFICP:
         return out
 
     def _run_on_stream(self, res, lambda0):
+        try:
+            return self._run_once(res, lambda0)
+        except _lib.FicpError as e:
+            if self.mode != "source" or "ERR_CAP" not in str(e) or self.capd >= res["n_max"]:
+                raise
+        # a rank's candidates overflowed its pack: every rank stopped at the same call (the
+        # overflow bit is merged); start over with packs that can hold every row
+        import torch
+        self.capd = res["n_max"]
+        res["pack"] = [torch.zeros(4 + 3 * self.capd, dtype=torch.int64, device=res["dev"]) for _ in res["mine"]]
+        self.n_cap_restarts = getattr(self, "n_cap_restarts", 0) + 1
+        return self._run_once(res, lambda0)
+
+    def _run_once(self, res, lambda0):
         n, md = len(self.source), self.match_dims
         world, W, ctxs, mine = res["world"], res["W"], res["ctxs"], res["mine"]
         src, tgt = res["src"], res["tgt"]

@@ -83,11 +83,8 @@ def get_transform(plot, *, device=None):
     src = _object_rows([[t.tree_id, t.x, t.y, t.height] for t in plot.trees])[:, 1:3].astype(float)
     tgt = _object_rows([[t.tree_id, t.currentx, t.currenty, t.height] for t in plot.trees])[:, 1:3].astype(float)
     flipped = bool(getattr(plot, "flipped", False))
-    ctx = _lib.Context(device)
-    try:  # trees.py:267-278: reflection kept only for a flipped plot
+    with _lib.borrowed(device) as ctx:  # trees.py:267-278: reflection kept only for a flipped plot
         T = ctx.fit_rigid2d(src, tgt, allow_reflection=flipped)
-    finally:
-        ctx.close()
     return T[:2, :2].copy(), T[:2, 2].copy(), getattr(plot, "flipped", False)
 
 

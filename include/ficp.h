@@ -58,6 +58,9 @@ typedef struct ficp_stats {
     double *trace_lambda;    /* [max_trace]      lambda in force                      */
     double *trace_T;         /* [max_trace * 9]  fits, in order                       */
     int32_t *trace_idx;      /* [max_trace * n]  NN target index per call             */
+    double host_ms[4];       /* out: host wall time of ficp_run's phases: [0] source
+                                upload, [1] device loop (enqueue + waits, incl. gpu_ms),
+                                [2] result download + column write-back, [3] 0         */
 } ficp_stats;
 
 /* --- library / context ------------------------------------------------- */
@@ -68,6 +71,10 @@ int ficp_create(int device, ficp_ctx **out);
 void ficp_destroy(ficp_ctx *ctx);
 /* NN algorithm: 0 = auto, 1 = brute force (LDS-tiled), 2 = uniform grid. */
 int ficp_set_nn_mode(ficp_ctx *ctx, int32_t mode);
+/* Test-only fault injection (no reference counterpart): mask 1 makes the selection's
+   bounds hand-off never arrive, so the run must fail with the ERR_SPIN flag (4) instead of
+   hanging or writing out of bounds.  0 = off (the default). */
+int ficp_set_fault(ficp_ctx *ctx, int32_t mask);
 /* Kernel timing with HIP events on the context stream: mask bit per kernel class
    (1 = nn, 2 = sort, 4 = scan/fraction, 8 = fit, 16 = grid build); 0 = off. */
 int ficp_profile_enable(ficp_ctx *ctx, int32_t mask);

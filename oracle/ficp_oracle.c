@@ -324,11 +324,13 @@ EXPORT int orc_optimal_fraction(const double *src, int64_t lds, const double *co
 }
 
 /* ficp.py:54-60 */
+/* ficp.py:54-60: the squared differences of ALL `rows` rows given, divided by k
+   (num_elements, which callers may pass different from the row count) */
 EXPORT double orc_frmsd(double fraction, int64_t k, const double *src, int64_t lds,
-                        const double *corr, int64_t ldc, int md, double lam) {
+                        const double *corr, int64_t ldc, int64_t rows, int md, double lam) {
     if (k == 0) return INFINITY;
     double S = 0.0;
-    for (int64_t i = 0; i < k; ++i)
+    for (int64_t i = 0; i < rows; ++i)
         for (int t = 0; t < md; ++t) {
             double df = src[i * lds + t] - corr[i * ldc + t];
             S = S + df * df;

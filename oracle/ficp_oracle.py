@@ -57,7 +57,7 @@ def lib():
         L.orc_sort_order.argtypes = [_dp, _i64, _ip64]
         L.orc_optimal_fraction.argtypes = [_dp, _i64, _dp, _i64, _dp, _i64, _i64, C.c_int, C.c_double,
                                            C.c_int, _dp, _ip64, _dp]
-        L.orc_frmsd.argtypes = [C.c_double, _i64, _dp, _i64, _dp, _i64, C.c_int, C.c_double]
+        L.orc_frmsd.argtypes = [C.c_double, _i64, _dp, _i64, _dp, _i64, _i64, C.c_int, C.c_double]
         L.orc_frmsd.restype = C.c_double
         L.orc_fit_rigid2d.argtypes = [_dp, _i64, _dp, _i64, _i64, C.c_int, _dp]
         L.orc_apply_xy.argtypes = [_dp, _i64, _i64, _dp]
@@ -151,7 +151,9 @@ def optimal_fraction(src, corr, d, N, md, lam, literal=False):
 
 def frmsd(fraction, k, src, corr, md, lam):
     src, corr = _c64(src), _c64(corr)
-    return lib().orc_frmsd(fraction, k, _p(src), src.shape[1], _p(corr), corr.shape[1], md, lam)
+    if len(src) != len(corr):
+        raise ValueError("operands could not be broadcast together")
+    return lib().orc_frmsd(fraction, k, _p(src), src.shape[1], _p(corr), corr.shape[1], len(src), md, lam)
 
 
 def fit_rigid2d(src, tgt, allow_reflection=False):

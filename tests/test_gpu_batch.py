@@ -153,6 +153,26 @@ def test_partitioned_matches_single(shards, mode, oracle):
     assert part.lambda_val == 0.95
 
 
+@pytest.mark.parametrize("lam", [3.0, 0.95, 1.3])
+def test_source_mode_pack_overflow_is_exact(lam, oracle):
+    """Source mode when a rank's candidates overflow its pack (ERR_CAP in round 2): flat
+    FRMSD curves (lambda near 1) with packs of 16 rows force it on the first call; the run
+    restarts with full packs and gives the unsplit run (k per call, XY within 1e-6)."""
+    from coregistrationgame_amd import FractionalICP, synth
+    from coregistrationgame_amd.partitioned import PartitionedFICP
+    p = synth.make_plot(30_000, 30_000, 0.6, seed=91, md=3)
+    part = PartitionedFICP(p.source, p.target, lambda_val=lam, local_shards=8, mode="source")
+    part.CAPD, part.CAPD_FRAC = 16, 1 << 30  # packs of 16 candidates: overflow at once
+    out = part.run()
+    assert getattr(part, "n_cap_restarts", 0) == 1
+    icp = FractionalICP(p.source, p.target, lambda_val=lam)
+    single = icp.run(trace=True)
+    np.testing.assert_allclose(out[:, :2], single[:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(np.array(part.last_stats["k"]), icp.last_stats["k"])
+    ofinal, otr = oracle.run(p.source, p.target, lam0=lam, nthreads=8)
+    np.testing.assert_allclose(out[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+
+
 @pytest.mark.parametrize("mode", ["target", "source"])
 def test_partitioned_2d_and_tiny_shards(mode):
     """2-D layers and more shards than stems (target: empty shards) or a few rows per

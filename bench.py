@@ -484,15 +484,16 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
     return out
 
 
-def bench_batch(args, rank, world, local, D, steps, warmup, with_cpu):
+def bench_batch(args, rank, world, local, D, steps, warmup, with_cpu, share_of=0):
     """C4: the batch is dealt over ranks (shard.deal_plots); each rank runs its plots in
-    one ficp_run_batch_device per step; no collective on the data path."""
+    one ficp_run_batch_device per step; no collective on the data path.  share_of = N > 0
+    (one process): run only the plots rank 0 gets when the batch is dealt over N ranks."""
     from coregistrationgame_amd import shard
     n, m, f, seed0, md, thr, max_it, desc = WORKLOADS["batch"]
     nplots = args.plots or BATCH_PLOTS
-    deal = shard.deal_plots(np.full(nplots, float(n) * m), world)
-    mine = deal[rank]
-    plots = [synth.make_plot(n, m, f, seed0 + int(p), md=md) for p in mine]
+    deal = shard.deal_plots(np.full(nplots, float(n) * m), share_of or world)
+    mine = deal[0 if share_of else rank]
+    plots = [_batch_plot(n, m, f, seed0 + int(p), md) for p in mine]
     ctx = _lib.Context(local)
     so = np.zeros(len(plots) + 1, np.int64)
     to = np.zeros(len(plots) + 1, np.int64)
@@ -583,6 +584,36 @@ def bench_batch(args, rank, world, local, D, steps, warmup, with_cpu):
             out["cpu_baseline"] = cpu_baseline_batch(plots, threads)
         else:
             out["cpu_baseline"] = None
+    return out
+
+
+_PLOTS = {}
+
+
+def _batch_plot(n, m, f, seed, md):
+    """C4 plots are generated once per process (the shares reuse the full batch's)."""
+    key = (n, m, f, seed, md)
+    if key not in _PLOTS:
+        _PLOTS[key] = synth.make_plot(n, m, f, seed, md=md)
+    return _PLOTS[key]
+
+
+def batch_shares(args, local, full):
+    """The per-rank shares of the north star's 1/2/4/8-GPU batch line, on this one GPU: the
+    plots rank 0 gets when the 1024 plots are dealt over N = 2, 4, 8 ranks (512, 256, 128
+    plots), each timed alone.  A rank of an N-GPU job runs exactly that share with no
+    data-path collective, so share rate x N is the job's rate before the one all-gather of
+    the per-plot records (shard.gather_plot_stats) and any host-side contention."""
+    out = {"1024": {"plots": full["config"]["plots_per_rank"], "plot_iterations_per_s": full["value"],
+                    "ms_per_step": full["ms_per_step"], "kernel_ms": full["kernel_ms"]}}
+    per_gpu_full = full["value"]
+    for N in (2, 4, 8):
+        b = bench_batch(args, 0, 1, local, None, max(5, args.steps), 2, False, share_of=N)
+        out[str(BATCH_PLOTS // N)] = {
+            "share_of_n_gpus": N, "plots": b["config"]["plots_per_rank"],
+            "plot_iterations_per_s": b["value"], "ms_per_step": b["ms_per_step"],
+            "kernel_ms": b["kernel_ms"], "vs_1024_per_gpu": b["value"] / per_gpu_full,
+            "implied_job_rate": b["value"] * N}
     return out
 
 
@@ -725,6 +756,7 @@ def main():
                                                   "iterations_per_step", "nn_calls_per_step",
                                                   "correspondences_per_s", "roofline", "iteration_roofline",
                                                   "kernel_ms")}
+                out["batch_shares"] = batch_shares(args, local, b)
     if out is not None:
         out["ranks_seen"] = ranks_seen
         print(json.dumps(out), flush=True)

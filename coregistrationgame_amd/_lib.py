@@ -50,7 +50,7 @@ class Stats(C.Structure):
         ("k_last", C.c_int64), ("frmsd_last", C.c_double * 2), ("T_total", C.c_double * 9),
         ("gpu_ms", C.c_double), ("max_trace", C.c_int32), ("n_nn_reused", C.c_int32),
         ("trace_k", _ip64), ("trace_frmsd", _dp), ("trace_lambda", _dp), ("trace_T", _dp),
-        ("trace_idx", _ip32), ("host_ms", C.c_double * 4),
+        ("trace_idx", _ip32), ("host_ms", C.c_double * 4), ("path", C.c_int32), ("max_trace_idx", C.c_int32),
     ]
 
 
@@ -515,9 +515,11 @@ def dist_hist_words() -> int:
 def _make_stats(n, trace, trace_idx, max_trace):
     st = Stats()
     keep = {}
+    idx_calls = max_trace
     if trace_idx and n > 0:
-        # the per-call idx trace is max_trace x n int32 on both sides: keep it <= ~1 GB
-        max_trace = max(64, min(max_trace, int(1e9) // (4 * n)))
+        # the per-call idx trace is calls x n int32 on both sides: keep it <= ~1 GB; only the
+        # idx trace is shortened (the k / FRMSD / T traces keep max_trace calls)
+        idx_calls = max(1, min(max_trace, int(1e9) // (4 * n)))
     if trace:
         st.max_trace = max_trace
         keep["k"] = np.zeros(max_trace, np.int64)
@@ -527,7 +529,8 @@ def _make_stats(n, trace, trace_idx, max_trace):
         st.trace_k, st.trace_frmsd = _p(keep["k"], _ip64), _p(keep["frmsd"])
         st.trace_lambda, st.trace_T = _p(keep["lam"]), _p(keep["T"])
         if trace_idx:
-            keep["idx"] = np.zeros((max_trace, n), np.int32)
+            st.max_trace_idx = idx_calls
+            keep["idx"] = np.zeros((idx_calls, n), np.int32)
             st.trace_idx = _p(keep["idx"], _ip32)
     return st, keep
 
@@ -538,7 +541,8 @@ def _stats_dict(st, keep, n):
     out = dict(n_nn_calls=nc, n_nn_reused=st.n_nn_reused, n_fits=nf, iters=(st.iters[0], st.iters[1]), k_last=st.k_last,
                frmsd_last=(st.frmsd_last[0], st.frmsd_last[1]),
                T_total=np.array(st.T_total[:]).reshape(3, 3), gpu_ms=st.gpu_ms,
-               lib_host_ms=dict(upload=st.host_ms[0], loop=st.host_ms[1], result=st.host_ms[2]))
+               lib_host_ms=dict(upload=st.host_ms[0], loop=st.host_ms[1], result=st.host_ms[2]),
+               path=("small" if st.path == 1 else "loop"))
     if keep:
         m = st.max_trace
         out["k"] = keep["k"][:min(nc, m)].copy()
@@ -546,5 +550,6 @@ def _stats_dict(st, keep, n):
         out["lam"] = keep["lam"][:min(nc, m)].copy()
         out["T"] = keep["T"][:min(nf, m) * 9].reshape(-1, 3, 3).copy()
         if "idx" in keep:
-            out["idx"] = keep["idx"][:min(nc, m)].copy()
+            out["idx"] = keep["idx"][:min(nc, st.max_trace_idx)].copy()
+            out["idx_truncated"] = nc > st.max_trace_idx
     return out

@@ -342,6 +342,117 @@ int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const doub
     return FICP_OK;
 }
 
+// A small plot's whole run in one workgroup (k_small.hip): the Join button's size
+// (app.py:630-661).  One launch, then the state and traces come back as in run_core.
+// rows (device, n x ld, nullable): the trees as uploaded (else the SoA sx, sy, sz); with
+// host_xy the kernel reports straight into coherent pinned memory (the XY, the state, the
+// clock stamps and a flag the host polls): one launch and one poll per run()
+int run_small(ficp_ctx *c, const double *rows, int64_t ld, double *sx, double *sy,
+              const double *sz, int64_t n, int32_t nstages, const double *lambdas,
+              double threshold, int32_t max_iter, int32_t allow_refl, ficp_stats *st,
+              double **host_xy) {
+    CHK(c->state_dev.ensure(sizeof(IterState)));
+    LoopCtl lc{};
+    lc.nstages = nstages;
+    lc.max_iter = max_iter;
+    lc.threshold = threshold;
+    for (int e = 0; e < kLamIn; ++e) lc.lam_in[e] = e < nstages ? lambdas[e] : 0.0;
+    if (nstages > kLamIn) {
+        CHK(c->lams.ensure((size_t)nstages * 8));
+        HIPCHK(hipMemcpyAsync(c->lams.p, lambdas, (size_t)nstages * 8, hipMemcpyHostToDevice,
+                              c->stream));
+        lc.lams = c->lams.as<double>();
+    }
+    const int mt = (st && st->max_trace > 0) ? st->max_trace : 0;
+    int32_t *tidx = nullptr;
+    if (mt > 0) {
+        lc.max_trace = mt;
+        CHK(c->tr_k.ensure((size_t)mt * 8));
+        CHK(c->tr_f.ensure((size_t)mt * 8));
+        CHK(c->tr_l.ensure((size_t)mt * 8));
+        CHK(c->tr_T.ensure((size_t)mt * 72));
+        lc.tk = c->tr_k.as<long long>();
+        lc.tf = c->tr_f.as<double>();
+        lc.tl = c->tr_l.as<double>();
+        lc.tT = c->tr_T.as<double>();
+        if (st->trace_idx) {
+            lc.max_trace_idx = st->max_trace_idx > 0 ? std::min(st->max_trace_idx, mt) : mt;
+            CHK(c->tr_idx.ensure((size_t)lc.max_trace_idx * (size_t)n * 4));
+            tidx = c->tr_idx.as<int32_t>();
+        }
+    }
+    SmallArgs a{};
+    a.rows = rows;
+    a.ld = ld;
+    a.sx = sx;
+    a.sy = sy;
+    a.sz = c->md == 3 ? sz : nullptr;
+    a.n = (int)n;
+    a.tx = c->tx.as<double>();
+    a.ty = c->ty.as<double>();
+    a.tz = c->md == 3 ? c->tz.as<double>() : nullptr;
+    a.m = (int)c->m;
+    a.allow_refl = allow_refl;
+    a.st = c->state_dev.as<IterState>();
+    a.tidx = tidx;
+    if (host_xy) {
+        CHK(c->pin_xy.ensure((size_t)n * 16));
+        a.host_xy = c->pin_xy.as<double>();
+        a.host_st = &c->h_rep->st;
+        a.host_t = c->h_rep->t;
+        a.host_flag = &c->h_rep->flag;
+        __atomic_store_n(&c->h_rep->flag, -1, __ATOMIC_RELAXED);
+        HIPCHK(launch_small_run(a, c->md, lc, c->stream));
+        int v = 0;
+        CHK(poll_flag(c, &c->h_rep->flag, v));
+        *host_xy = c->pin_xy.as<double>();
+    } else {
+        CHK(c->sel_stats.ensure(16));
+        HIPCHK(launch_run_start(c->sel_stats.as<uint32_t>(), &c->h_rep->t[0], c->stream));
+        HIPCHK(launch_small_run(a, c->md, lc, c->stream));
+        CHK(report_wait(c, ReportSeg{c->state_dev.p, &c->h_rep->st, (int)(sizeof(IterState) / 4)},
+                        ReportSeg{}, ReportSeg{}, &c->h_rep->t[1]));
+    }
+    const IterState &h = c->h_rep->st;
+    if (!h.done) return fail(FICP_EHIP, "small-plot ICP kernel did not finish");
+    c->runs_small += 1;
+    if (!st) return FICP_OK;
+    st->path = 1;
+    st->n_nn_calls = h.n_nn;
+    st->n_nn_reused = h.n_reuse;
+    st->n_fits = h.n_fit;
+    st->iters[0] = h.iters[0];
+    st->iters[1] = h.iters[1];
+    st->k_last = h.k_last;
+    st->frmsd_last[0] = h.frmsd_last[0];
+    st->frmsd_last[1] = h.frmsd_last[1];
+    memcpy(st->T_total, h.Ttot, sizeof st->T_total);
+    const int nc = std::min(h.n_nn, mt), nf = std::min(h.n_fit, mt);
+    if (nc > 0 || nf > 0) {
+        if (nc > 0 && st->trace_k)
+            HIPCHK(hipMemcpyAsync(st->trace_k, c->tr_k.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        if (nc > 0 && st->trace_frmsd)
+            HIPCHK(hipMemcpyAsync(st->trace_frmsd, c->tr_f.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        if (nc > 0 && st->trace_lambda)
+            HIPCHK(hipMemcpyAsync(st->trace_lambda, c->tr_l.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        if (nc > 0 && tidx)
+            HIPCHK(hipMemcpyAsync(st->trace_idx, tidx, (size_t)std::min(nc, lc.max_trace_idx) * (size_t)n * 4,
+                                  hipMemcpyDeviceToHost, c->stream));
+        if (nf > 0 && st->trace_T)
+            HIPCHK(hipMemcpyAsync(st->trace_T, c->tr_T.p, (size_t)nf * 72, hipMemcpyDeviceToHost, c->stream));
+        CHK(sync(c));
+    }
+    st->gpu_ms = (double)(c->h_rep->t[1] - c->h_rep->t[0]) * 1e-5;  // 100 MHz ticks
+    return FICP_OK;
+}
+
+// the one-workgroup path takes the run (auto NN mode, FICP_SMALL != 0)
+bool use_small(ficp_ctx *c, int64_t n) {
+    if (c->nn_mode != 0 || !small_run_fits(n, c->m)) return false;
+    const char *e = getenv("FICP_SMALL");
+    return !(e && atoi(e) == 0);
+}
+
 // the device-resident ICP: stages of ficp.py:122-147
 int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, int32_t nstages,
              const double *lambdas, double threshold, int32_t max_iter, int32_t allow_refl,
@@ -356,9 +467,13 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         for (int e = 0; e < 9; ++e) st->T_total[e] = (e % 4 == 0) ? 1.0 : 0.0;
         st->gpu_ms = 0.0;
         for (double &h : st->host_ms) h = 0.0;
+        st->path = 0;
     }
     if (n == 0 || c->m == 0) return FICP_OK;  // ficp.py:66-68 + 125-126: nothing moves
     if (n > 0x3fffffff) return fail(FICP_EINVAL, "n too large (max 2^30 - 1)");
+    if (use_small(c, n))
+        return run_small(c, nullptr, 0, sx, sy, sz, n, nstages, lambdas, threshold, max_iter,
+                         allow_refl, st, nullptr);
     CHK(ensure_work(c, n));
     CHK(ensure_bbox(c));
     uint32_t *tflag = sort_timeout_flag(c->sort_tmp.p, n);
@@ -408,10 +523,11 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         lc.tl = c->tr_l.as<double>();
         lc.tT = c->tr_T.as<double>();
         if (st->trace_idx) {
-            if ((double)mt * (double)n * 4.0 > 8e9)
-                return fail(FICP_EINVAL, "trace_idx of %d calls x %lld rows is too large", mt,
-                            (long long)n);
-            CHK(c->tr_idx.ensure((size_t)mt * (size_t)n * 4));
+            lc.max_trace_idx = st->max_trace_idx > 0 ? std::min(st->max_trace_idx, mt) : mt;
+            if ((double)lc.max_trace_idx * (double)n * 4.0 > 8e9)
+                return fail(FICP_EINVAL, "trace_idx of %d calls x %lld rows is too large",
+                            lc.max_trace_idx, (long long)n);
+            CHK(c->tr_idx.ensure((size_t)lc.max_trace_idx * (size_t)n * 4));
             tidx = c->tr_idx.as<int32_t>();
         }
     }
@@ -459,7 +575,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         }
         if (!fused) {
             if (tidx)
-                HIPCHK(launch_trace_idx(dst, c->idx.as<int32_t>(), worig, n, tidx, mt, c->stream));
+                HIPCHK(launch_trace_idx(dst, c->idx.as<int32_t>(), worig, n, tidx, lc.max_trace_idx,
+                                        c->stream));
             HIPCHK(launch_loop_update(dst, lc, c->stream));
             HIPCHK(hipMemcpyAsync(&c->h_flags[slot], &dst->done, 4, hipMemcpyDeviceToHost,
                                   c->stream));
@@ -534,7 +651,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
                 HIPCHK(hipMemcpyAsync(st->trace_lambda, c->tr_l.p, nc * 8, hipMemcpyDeviceToHost,
                                       c->stream));
             if (nc > 0 && tidx)
-                HIPCHK(hipMemcpyAsync(st->trace_idx, tidx, (size_t)nc * (size_t)n * 4,
+                HIPCHK(hipMemcpyAsync(st->trace_idx, tidx,
+                                      (size_t)std::min(nc, lc.max_trace_idx) * (size_t)n * 4,
                                       hipMemcpyDeviceToHost, c->stream));
             if (nf > 0 && st->trace_T)
                 HIPCHK(hipMemcpyAsync(st->trace_T, c->tr_T.p, (size_t)nf * 72, hipMemcpyDeviceToHost,
@@ -671,6 +789,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp, &c->bs_tmp2};
     for (DevBuf *b : bufs) b->release();
     c->pin.release();
+    c->pin_xy.release();
     batch_release(c->batch);
     c->batch = nullptr;
     for (auto &r : c->recs) {
@@ -930,6 +1049,27 @@ int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
     const auto t0 = clk::now();
+    if (use_small(c, n) && n <= 0x3fffffff) {
+        // the Join button's size: one H2D of the rows, one launch that reports straight
+        // into pinned memory, one poll (k_small.hip)
+        CHK(c->stage.ensure((size_t)n * ld * 8));
+        HIPCHK(hipMemcpyAsync(c->stage.p, src, (size_t)n * ld * 8, hipMemcpyHostToDevice, c->stream));
+        const auto t1 = clk::now();
+        double *xy = nullptr;
+        CHK(run_small(c, c->stage.as<double>(), ld, nullptr, nullptr, nullptr, n, nstages, lambdas,
+                      threshold, max_iterations, allow_reflection, stats, &xy));
+        const auto t2 = clk::now();
+        for (int64_t i = 0; i < n; ++i) {  // columns 0, 1 only (ficp.py:114-118)
+            src[i * ld] = xy[2 * i];
+            src[i * ld + 1] = xy[2 * i + 1];
+        }
+        if (stats) {
+            stats->host_ms[0] = ms(t0, t1);
+            stats->host_ms[1] = ms(t1, t2);
+            stats->host_ms[2] = ms(t2, clk::now());
+        }
+        return FICP_OK;
+    }
     CHK(upload_rows(c, src, n, ld, c->md, c->sx, c->sy, &c->sz));
     const auto t1 = clk::now();
     CHK(run_core(c, c->sx.as<double>(), c->sy.as<double>(),
@@ -1245,6 +1385,9 @@ int ficp_dist_begin(ficp_ctx *c, int32_t mode, double *x, double *y, const doubl
     CHK(c->tr_k.ensure((size_t)kDistTrace * 8));
     lc.max_trace = kDistTrace;
     lc.tk = c->tr_k.as<long long>();
+    // the target mode's shard NN never skips a call (its index offset is added per call),
+    // so n_nn_reused stays 0 there
+    lc.no_reuse_count = mode == 1;
     c->dist_lc = lc;
     HIPCHK(launch_loop_init(c->state_dev.as<IterState>(), lc, c->stream));
     c->dist_mode = mode;
@@ -1436,6 +1579,7 @@ int ficp_dist_end(ficp_ctx *c, ficp_stats *st) {
         memcpy(st->T_total, h.Ttot, sizeof st->T_total);
         st->gpu_ms = 0.0;
         for (double &hm : st->host_ms) hm = 0.0;
+        st->path = 0;
         const int nc = std::min(std::min(h.n_nn, st->max_trace), kDistTrace);
         if (nc > 0 && st->trace_k) {
             HIPCHK(hipMemcpyAsync(st->trace_k, c->tr_k.p, (size_t)nc * 8, hipMemcpyDeviceToHost,

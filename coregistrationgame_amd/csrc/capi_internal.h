@@ -86,13 +86,14 @@ struct DevBuf {
 struct PinBuf {
     void *p = nullptr;
     size_t cap = 0;
+    unsigned flags = hipHostMallocDefault;  // hipHostMallocCoherent: kernels store into it
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return FICP_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
         const size_t want = std::max<size_t>(bytes, 4096);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, want, flags);
         if (e != hipSuccess) {
             p = nullptr;
             return fail(FICP_ENOMEM, "hipHostMalloc(%zu) failed: %s", want, hipGetErrorString(e));
@@ -140,6 +141,7 @@ struct ficp_ctx {
     hipStream_t stream = nullptr;
     int nn_mode = 0;
     int fault = 0;  // test-only fault injection mask (ficp_set_fault)
+    int64_t runs_small = 0;  // runs taken by the one-workgroup path (k_small.hip)
 
     // target (CHM layer)
     bool has_target = false;
@@ -198,6 +200,7 @@ struct ficp_ctx {
     DevBuf drange;                     // int64 range words of the local rows (top bit flipped)
 
     PinBuf pin;  // pinned staging of results on their way to the caller's (pageable) arrays
+    PinBuf pin_xy{nullptr, 0, hipHostMallocCoherent};  // k_small_run's XY, stored by the kernel
 };
 
 namespace ficp_capi {

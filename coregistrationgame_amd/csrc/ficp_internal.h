@@ -71,6 +71,22 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
     return x * q + (x < r ? x : r) + (b >> 3);
 }
 
+// squared distance in md dims in the reference's order, no contraction (cKDTree-identical
+// bits): ((0 + dx*dx) + dy*dy) + dz*dz
+template <int MD>
+__device__ __forceinline__ double sq_dist(double qx, double qy, double qz, double px, double py,
+                                          double pz) {
+    double dx = qx - px;
+    double dy = qy - py;
+    double s = dx * dx;  // == 0 + dx*dx exactly
+    s = s + dy * dy;
+    if (MD == 3) {
+        double dz = qz - pz;
+        s = s + dz * dz;
+    }
+    return s;
+}
+
 struct alignas(32) TPt {
     double x, y, z;
     long long idx;
@@ -261,6 +277,9 @@ struct LoopCtl {
     int max_iter;
     double threshold;
     int max_trace;         // capacity of the trace buffers (NN calls), 0 = no trace
+    int max_trace_idx;     // calls whose NN index is traced (<= max_trace; its buffer is n per call)
+    int no_reuse_count;    // the NN step of this loop never honours nn_reuse (dist target mode):
+                           // n_reuse stays 0
     int pad;
     long long *tk;         // [max_trace] k per call
     double *tf;            // [max_trace] FRMSD per call
@@ -298,7 +317,7 @@ __device__ __forceinline__ void loop_end_stage(IterState &s, const LoopCtl &c) {
 __device__ __forceinline__ void loop_step(IterState *st, const LoopCtl &c) {
     IterState &s = *st;
     if (s.done) return;
-    s.n_reuse += s.nn_reuse;
+    if (!c.no_reuse_count) s.n_reuse += s.nn_reuse;
     const int call = s.n_nn++;
     s.k_last = s.k;
     if (call < c.max_trace) {
@@ -338,6 +357,33 @@ __device__ __forceinline__ void loop_step(IterState *st, const LoopCtl &c) {
     }
     loop_set_flags(s);
 }
+
+// ------------------------------------------- one small plot in one workgroup (k_small.hip)
+// The Join button's size (app.py:630-661: 5-44 trees vs ~260 CHM stems): the whole run()
+// in one launch, the CHM layer in LDS, one tree per thread.
+constexpr int kSmallMaxN = 1024;            // trees (one per thread)
+constexpr int kSmallMaxM = 4096;            // CHM stems staged in LDS (96 KB at md 3)
+constexpr int64_t kSmallMaxPairs = 1 << 18; // brute-force pairs per NN call (~10 us in one CU)
+struct SmallArgs {
+    const double *rows;         // trees as the caller's (n x ld) rows on the device (nullable:
+    int64_t ld;                 //   then the SoA columns below are read)
+    double *sx, *sy;            // trees (caller order), SoA; moved in place (nullable with rows)
+    const double *sz;
+    int n;
+    const double *tx, *ty, *tz; // CHM layer (original order)
+    int m;
+    int allow_refl;
+    IterState *st;              // out: the final loop state (stats, T_total), device
+    int32_t *tidx;              // out (nullable): NN index per call [max_trace][n]
+    // pinned host report (nullable): the final XY interleaved, the state, the device clock
+    // at start and end, then *host_flag = 1 (system scope) -- no copy or report launch
+    double *host_xy;
+    IterState *host_st;
+    unsigned long long *host_t; // [2]
+    int *host_flag;
+};
+bool small_run_fits(int64_t n, int64_t m);
+hipError_t launch_small_run(const SmallArgs &a, int md, const LoopCtl &lc, hipStream_t s);
 
 // ----------------------------------------------------------------- launchers
 // device -> coherent pinned host copies + a completion flag the host polls (k_loop.hip)

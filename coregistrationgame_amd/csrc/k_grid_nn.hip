@@ -38,19 +38,6 @@ __device__ __forceinline__ int cell_coord(double v, double v0, double inv_h, int
     return (int)f;
 }
 
-template <int MD>
-__device__ __forceinline__ double sq_dist(double qx, double qy, double qz, double px, double py,
-                                          double pz) {
-    double dx = qx - px;
-    double dy = qy - py;
-    double s = dx * dx;  // == 0 + dx*dx exactly
-    s = s + dy * dy;
-    if (MD == 3) {
-        double dz = qz - pz;
-        s = s + dz * dz;
-    }
-    return s;
-}
 
 // The cell-sorted stems are read through a buffer descriptor: 32-bit per-lane byte
 // offsets, no 64-bit address arithmetic per candidate (cdna_hip_programming.md T8).

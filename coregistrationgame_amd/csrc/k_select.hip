@@ -37,6 +37,7 @@
 #include "frmsd_bounds.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1383,7 +1384,16 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
 // block scan of r in sorted order, FRMSD of every position, first minimum.  Fewer
 // barriers than the binned sort of lds_sort_scan, whose fixed phases dominated at this c.
 constexpr int SMALL_C = 160;  // above it the binned sort ranks faster (390: 5.8 vs 3.4 us)
-__device__ void final_small(const Cand &src, unsigned c, const FinalIn &in, unsigned char *sm,
+// Pre: thread t < c holds candidate t (pk, po, pr; with the fused fit also its pair in
+// pf[4]), loaded in k_sel_final's prologue beside the state and S_base parts (they were a
+// second dependent round trip after the candidate count).
+struct CandPre {
+    u64 k;
+    uint32_t o;
+    double r;
+    double f[4];
+};
+__device__ void final_small(const CandPre &pre, unsigned c, const FinalIn &in, unsigned char *sm,
                             Scr &scr, IterState *st) {
     u64 *lk = (u64 *)sm;
     double *lr = (double *)(sm + HT * 8);
@@ -1394,21 +1404,17 @@ __device__ void final_small(const Cand &src, unsigned c, const FinalIn &in, unsi
     u64 k = 0;
     uint32_t o = 0;
     if (t < c) {
-        k = src.k[t];
-        o = src.o[t];
-        const double rv = src.r[t];
-        if (in.fs.on) {
-            // the pair of every candidate loads now (overlapping the ranking below); the
-            // sums then run over LDS in sorted order (deterministic), not after the argmin
-            const uint32_t w = src.p[t];
-            lf[t] = in.fs.sx[w];
-            lf[HT + t] = in.fs.sy[w];
-            lf[2 * HT + t] = in.fs.cx[w];
-            lf[3 * HT + t] = in.fs.cy[w];
+        k = pre.k;
+        o = pre.o;
+        if (in.fs.on) {  // summed over LDS in sorted order below (deterministic)
+            lf[t] = pre.f[0];
+            lf[HT + t] = pre.f[1];
+            lf[2 * HT + t] = pre.f[2];
+            lf[3 * HT + t] = pre.f[3];
         }
         lk[t] = k;
         lo[t] = o;
-        lr[t] = rv;
+        lr[t] = pre.r;
     }
     __syncthreads();
     if (t < c) {
@@ -1869,9 +1875,10 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
 __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N, double lam,
                                                   const double *lam_dev, IterState *st,
                                                   const int *skip, LoopCtl lc, int fuse_loop,
-                                                  int *host_flag, FitSrc fs) {
+                                                  int *host_flag, FitSrc fs, int64_t cap) {
     // the independent loads (skip flag, lambda, the candidate count and the bounds'
-    // outputs) issue together, before the first wait
+    // outputs, and the first SMALL_C candidate slots whatever the count) issue together,
+    // before the first wait
     const int sk = skip ? *skip : 0;
     const double lamv = lam_dev ? *lam_dev : lam;
     unsigned c = __hip_atomic_fetch_add(&w.ctl->ccount, 0u, __ATOMIC_RELAXED,
@@ -1880,6 +1887,15 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
                                                 __HIP_MEMORY_SCOPE_AGENT);
     const long long kbase = w.ctl->kbase;
     const double Ub = w.ctl->U;
+    CandPre pre{};
+    const bool pfc = (int64_t)threadIdx.x < cap && threadIdx.x < (unsigned)SMALL_C;
+    uint32_t prow = 0;
+    if (pfc) {
+        pre.k = w.ka[threadIdx.x];
+        pre.o = w.oa[threadIdx.x];
+        pre.r = w.ra[threadIdx.x];
+        if (fs.on) prow = w.pa[threadIdx.x];
+    }
     if (sk) {
         if (host_flag && threadIdx.x == 0)
             __hip_atomic_store(host_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1899,6 +1915,12 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
     if (t < 8) s_fit[t] = 0.0;
+    if (fs.on && pfc && t < c) {  // the candidate's pair (its row is known now)
+        pre.f[0] = fs.sx[prow];
+        pre.f[1] = fs.sy[prow];
+        pre.f[2] = fs.cx[prow];
+        pre.f[3] = fs.cy[prow];
+    }
     double a = 0.0;
     for (int p = t; p < nparts; p += HT) a = a + w.parts[p];  // fixed order per thread
     FinalIn in;
@@ -1934,8 +1956,23 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
             __syncthreads();
         }
         if (t == 0) w.ctl->levels += lev;
-        if (c <= (unsigned)SMALL_C) {
-            final_small(src, c, in, sm, scr, &s_st);
+        if (c <= (unsigned)SMALL_C && lev == 0) {
+            final_small(pre, c, in, sm, scr, &s_st);
+        } else if (c <= (unsigned)SMALL_C) {  // after refinement: the candidates moved
+            CandPre q{};
+            if (t < c) {
+                q.k = src.k[t];
+                q.o = src.o[t];
+                q.r = src.r[t];
+                if (fs.on) {
+                    const uint32_t wr = src.p[t];
+                    q.f[0] = fs.sx[wr];
+                    q.f[1] = fs.sy[wr];
+                    q.f[2] = fs.cx[wr];
+                    q.f[3] = fs.cy[wr];
+                }
+            }
+            final_small(q, c, in, sm, scr, &s_st);
         } else if (c <= (unsigned)CAP) {
             final_lds<CAP, true>(src, c, in, sm, scr, &s_st);
         } else if (c <= (unsigned)CAP2) {
@@ -2097,7 +2134,7 @@ hipError_t launch_select_dist_final(const long long *packs, int world, int capd,
     LoopCtl lc{};
     if (loop) lc = *loop;
     hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, world, n_total, lam, lam_dev, st,
-                       skip, lc, loop ? 1 : 0, host_flag, FitSrc{});
+                       skip, lc, loop ? 1 : 0, host_flag, FitSrc{}, std::max<int64_t>(n_ws, 1));
     return hipGetLastError();
 }
 
@@ -2129,13 +2166,23 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     static std::atomic<unsigned> s_gen{0};  // launch tokens, unique per process
     unsigned gen = ++s_gen;
     if (gen == 0) gen = ++s_gen;  // 0 means "no flag"
-    const unsigned pub = (fault & FICP_FAULT_SPIN) ? (gen ^ 0x40000000u) : gen;
-    hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n, w, lam,
-                       lam_dev, skip, hp.fixb, fs, gen, pub);
+    // FICP_SEL_SPLIT=1: the bounds and the gather as two launches (no in-launch hand-off:
+    // the one-launch form relies on block 0 being dispatched before the polling blocks,
+    // which HIP does not promise; the split form trades its +1.4 % for no such assumption)
+    const char *sp = getenv("FICP_SEL_SPLIT");
+    const bool split = sp && atoi(sp) != 0;
+    if (split) {
+        hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip, hp.fixb);
+        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs);
+    } else {
+        const unsigned pub = (fault & FICP_FAULT_SPIN) ? (gen ^ 0x40000000u) : gen;
+        hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n, w,
+                           lam, lam_dev, skip, hp.fixb, fs, gen, pub);
+    }
     LoopCtl lc{};
     if (loop) lc = *loop;
     hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, gb, n, lam, lam_dev, st, skip, lc,
-                       loop ? 1 : 0, host_flag, fs);
+                       loop ? 1 : 0, host_flag, fs, std::max<int64_t>(n, 1));
     return hipGetLastError();
 }
 

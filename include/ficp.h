@@ -61,6 +61,10 @@ typedef struct ficp_stats {
     double host_ms[4];       /* out: host wall time of ficp_run's phases: [0] source
                                 upload, [1] device loop (enqueue + waits, incl. gpu_ms),
                                 [2] result download + column write-back, [3] 0         */
+    int32_t path;            /* out: 0 = the multi-kernel device loop, 1 = the whole run in
+                                one workgroup (small plots, auto NN mode: k_small.hip)   */
+    int32_t max_trace_idx;   /* in : calls whose NN index goes to trace_idx (0: max_trace);
+                                trace_idx then holds min(this, max_trace) * n entries    */
 } ficp_stats;
 
 /* --- library / context ------------------------------------------------- */

@@ -82,5 +82,5 @@ def test_no_cpu_fallback_without_gpu():
 
 def test_stats_struct_layout():
     """ctypes mirror of struct ficp_stats has the C layout (offsets of the trace pointers)."""
-    assert ctypes.sizeof(_lib.Stats) == 4 * 4 + 8 + 16 + 72 + 8 + 8 + 5 * 8 + 4 * 8
+    assert ctypes.sizeof(_lib.Stats) == 4 * 4 + 8 + 16 + 72 + 8 + 8 + 5 * 8 + 4 * 8 + 8
     assert _lib.Stats.host_ms.offset == 4 * 4 + 8 + 16 + 72 + 8 + 8 + 5 * 8

@@ -153,24 +153,27 @@ def test_partitioned_matches_single(shards, mode, oracle):
     assert part.lambda_val == 0.95
 
 
-@pytest.mark.parametrize("lam", [3.0, 0.95, 1.3])
-def test_source_mode_pack_overflow_is_exact(lam, oracle):
-    """Source mode when a rank's candidates overflow its pack (ERR_CAP in round 2): flat
-    FRMSD curves (lambda near 1) with packs of 16 rows force it on the first call; the run
-    restarts with full packs and gives the unsplit run (k per call, XY within 1e-6)."""
+def test_source_mode_pack_overflow_is_exact(oracle):
+    """Source mode when a rank's candidates overflow its pack (ERR_CAP in round 2): packs
+    of one candidate overflow as soon as a rank holds two (flat FRMSD curves near lambda =
+    1 hold many); the run restarts with full packs and gives the unsplit run (k per call,
+    XY within 1e-6) and the oracle's."""
     from coregistrationgame_amd import FractionalICP, synth
     from coregistrationgame_amd.partitioned import PartitionedFICP
     p = synth.make_plot(30_000, 30_000, 0.6, seed=91, md=3)
-    part = PartitionedFICP(p.source, p.target, lambda_val=lam, local_shards=8, mode="source")
-    part.CAPD, part.CAPD_FRAC = 16, 1 << 30  # packs of 16 candidates: overflow at once
-    out = part.run()
-    assert getattr(part, "n_cap_restarts", 0) == 1
-    icp = FractionalICP(p.source, p.target, lambda_val=lam)
-    single = icp.run(trace=True)
-    np.testing.assert_allclose(out[:, :2], single[:, :2], atol=1e-6, rtol=0)
-    np.testing.assert_array_equal(np.array(part.last_stats["k"]), icp.last_stats["k"])
-    ofinal, otr = oracle.run(p.source, p.target, lam0=lam, nthreads=8)
-    np.testing.assert_allclose(out[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+    restarts = 0
+    for lam in (3.0, 0.95, 1.3):
+        part = PartitionedFICP(p.source, p.target, lambda_val=lam, local_shards=8, mode="source")
+        part.CAPD, part.CAPD_FRAC = 1, 1 << 30  # packs of one candidate
+        out = part.run()
+        restarts += getattr(part, "n_cap_restarts", 0)
+        icp = FractionalICP(p.source, p.target, lambda_val=lam)
+        single = icp.run(trace=True)
+        np.testing.assert_allclose(out[:, :2], single[:, :2], atol=1e-6, rtol=0)
+        np.testing.assert_array_equal(np.array(part.last_stats["k"]), icp.last_stats["k"])
+        ofinal, otr = oracle.run(p.source, p.target, lam0=lam, nthreads=8)
+        np.testing.assert_allclose(out[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+    assert restarts >= 2, restarts
 
 
 @pytest.mark.parametrize("mode", ["target", "source"])

@@ -246,15 +246,22 @@ def test_apply_golden_bit_exact():
 
 
 # ------------------------------------------------------------------ whole runs
-@pytest.mark.parametrize("nn_mode", ["auto", "grid"])
+@pytest.mark.parametrize("nn_mode", ["auto", "grid", "auto_loop"])
 @pytest.mark.parametrize("name", RUN_FIXTURES)
-def test_run_trace(name, nn_mode):
-    from coregistrationgame_amd import FractionalICP
+def test_run_trace(name, nn_mode, monkeypatch):
+    """Every golden run trace: "auto" takes the one-workgroup path (k_small.hip) where the
+    plot fits it, "auto_loop" the multi-kernel loop at the same size (FICP_SMALL=0),
+    "grid" the grid NN."""
+    from coregistrationgame_amd import FractionalICP, _lib
     r = load_run(name)
+    if nn_mode == "auto_loop":
+        monkeypatch.setenv("FICP_SMALL", "0")
     icp = FractionalICP(r["src"], r["tgt"], threshold=float(r["kwargs_threshold"]),
-                        max_iterations=int(r["kwargs_max_iterations"]), nn_mode=nn_mode)
+                        max_iterations=int(r["kwargs_max_iterations"]), nn_mode=nn_mode.split("_")[0])
     final = icp.run(trace=True, trace_idx=True)
     tr = icp.last_stats
+    fits = len(r["src"]) <= 1024 and len(r["tgt"]) <= 4096 and len(r["src"]) * len(r["tgt"]) <= 1 << 18
+    assert tr["path"] == ("small" if nn_mode == "auto" and fits else "loop")
     np.testing.assert_allclose(final[:, :2], r["final"][:, :2], atol=1e-6, rtol=0)
     np.testing.assert_array_equal(bits(final[:, 2:]), bits(r["final"][:, 2:]))
     assert icp.lambda_val == float(r["lambda_final"])
@@ -269,6 +276,37 @@ def test_run_trace(name, nn_mode):
     else:
         nf = min(first, len(r["T"]))
         assert_T_close(tr["T"][:nf], r["T"][:nf], r["src"], msg=name)
+
+
+def test_small_run_vs_oracle(oracle):
+    """The one-workgroup run (k_small.hip) on plots of every size it takes -- 1 tree, 1
+    stem, the Join button's 5-44 trees vs ~260 stems, 1024 trees, 4096 stems, md 2 and 3,
+    geo-referenced, fixed iteration counts -- against the oracle run: k and NN index of
+    every pinned call, XY within 1e-6, Z untouched."""
+    from coregistrationgame_amd import FractionalICP, synth
+    rng = np.random.default_rng(404)
+    # (a plot whose selection maps onto one CHM stem has a zero cross-covariance: its rotation
+    # is rounding noise in the reference, unpinnable -- test_batch_vs_oracle_mixed)
+    shapes = [(1, 1), (1, 50), (7, 20), (5, 259), (44, 259), (20, 259), (300, 800), (1024, 256),
+              (64, 4096), (500, 500), (1000, 200), (130, 2000)]
+    for q, (n, m) in enumerate(shapes):
+        md = 3 if q % 3 else 2
+        p = synth.make_plot(n, m, float(rng.uniform(0.5, 0.9)), seed=4000 + q, md=md)
+        kw = dict(threshold=float("-inf"), max_iterations=7) if q % 4 == 1 else {}
+        icp = FractionalICP(p.source, p.target, **kw)
+        final = icp.run(trace=True, trace_idx=True)
+        st = icp.last_stats
+        assert st["path"] == "small", (n, m)
+        ofinal, otr = oracle.run(p.source, p.target, trace_idx=True,
+                                 threshold=kw.get("threshold", 1e-6), max_iterations=kw.get("max_iterations", 1000))
+        scale = 1.0 + np.abs(p.source[:, :2]).max()
+        first = pinned_prefix(otr["gap"], otr["frmsd"], scale)
+        np.testing.assert_array_equal(st["k"][:first], otr["k"][:first], err_msg=str((n, m)))
+        np.testing.assert_array_equal(st["idx"][:first], otr["idx"][:first], err_msg=str((n, m)))
+        if first == len(otr["k"]):
+            assert st["n_nn_calls"] == otr["n_calls"], (n, m)
+        np.testing.assert_allclose(final[:, :2], ofinal[:, :2], atol=1e-6, rtol=0, err_msg=str((n, m)))
+        np.testing.assert_array_equal(bits(final[:, 2:]), bits(p.source[:, 2:]))
 
 
 def test_real_stand10():
@@ -305,7 +343,7 @@ def test_run_vs_oracle_100k(oracle):
 # and the grid density (points per cell: more per cell, more cells per disk scan)
 KNOBS = [{}, {"FICP_FUSE_FIT": "1"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
          {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "1"},
-         {"FICP_GRID_PER_CELL": "4"}]
+         {"FICP_GRID_PER_CELL": "4"}, {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_SPLIT": "1", "FICP_FUSE_FIT": "1"}]
 
 
 @pytest.mark.parametrize("knobs,md", [(k, 3) for k in KNOBS] + [({}, 2), ({"FICP_GRID_ATOMIC": "1"}, 2)],

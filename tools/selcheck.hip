@@ -158,7 +158,8 @@ int main(int argc, char **argv) {
             CK(hipEventRecord(ev[2], 0));
             hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, 0, dkey, dorig, dr,
                                n, w, lam, (const double *)nullptr, (const int *)nullptr,
-                               hist_pack(n).fixb, FitSrc{}, ++gen);
+                               hist_pack(n).fixb, FitSrc{}, gen + 1, gen + 1);
+            ++gen;
         } else {
             hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, 0, w, n, lam,
                                (const double *)nullptr, (const int *)nullptr, hist_pack(n).fixb);
@@ -170,7 +171,7 @@ int main(int argc, char **argv) {
         LoopCtl lc{};
         hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, 0, w, gb, n, lam,
                            (const double *)nullptr, st, (const int *)nullptr, lc, 0, (int *)nullptr,
-                           FitSrc{});
+                           FitSrc{}, (int64_t)std::max<int64_t>(n, 1));
         CK(hipEventRecord(ev[4], 0));
         CK(hipEventSynchronize(ev[4]));
         for (int q = 0; q < 4; ++q) {

@@ -534,7 +534,12 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     HIPCHK(launch_loop_init(dst, lc, c->stream));
     const FitSrc fsrc{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->pivot_x, c->pivot_y, 1,
                       allow_refl};
-    const bool fuse_fit = getenv("FICP_FUSE_FIT") && atoi(getenv("FICP_FUSE_FIT")) != 0;
+    // the rigid fit fused into the selection (gather: the rows below the candidates, their
+    // pairs loaded before the bounds wait; final: the selected candidates, prefetched in its
+    // prologue) instead of a k_fit_sums pass: +1.5-2.5 % at C3 (tools/ab_bench.sh, 2 x 40
+    // steps: 8,067 / 8,140 vs 7,965 / 7,933 it/s).  FICP_FUSE_FIT=0: the separate pass.
+    const char *ff = getenv("FICP_FUSE_FIT");
+    const bool fuse_fit = !(ff && atoi(ff) == 0);
     // Iterations are enqueued `la` ahead of the one whose done flag the host reads, so
     // the device never waits for the host; the iterations enqueued past the end are
     // no-ops (every kernel tests the flags k_loop_update set).  la = 1 with the fused
@@ -790,6 +795,8 @@ void ficp_destroy(ficp_ctx *c) {
     for (DevBuf *b : bufs) b->release();
     c->pin.release();
     c->pin_xy.release();
+    c->pin_up.release();
+    if (c->up_ev) (void)hipEventDestroy(c->up_ev);
     batch_release(c->batch);
     c->batch = nullptr;
     for (auto &r : c->recs) {
@@ -865,6 +872,20 @@ int ficp_set_target(ficp_ctx *c, const double *tgt, int64_t m, int64_t ld, int32
     if (m < 0 || (m > 0 && (!tgt || ld < md))) return fail(FICP_EINVAL, "bad target shape");
     if (m > 0x7fffffff) return fail(FICP_EINVAL, "target too large");
     reset_target(c, m, md);
+    const size_t bytes = (size_t)m * (size_t)ld * 8;
+    if (m > 0 && bytes <= kBounceBytes) {
+        // a small layer (the Join button's ~260 stems) goes through a pinned bounce buffer:
+        // the caller's array is free as soon as this returns and the upload runs stream-
+        // ordered before the next run, with no host round trip (the previous upload from
+        // the bounce buffer is waited for first; it is long done by then)
+        CHK(c->pin_up.ensure(kBounceBytes));
+        if (c->up_ev) HIPCHK(hipEventSynchronize(c->up_ev));
+        else HIPCHK(hipEventCreateWithFlags(&c->up_ev, hipEventDisableTiming));
+        memcpy(c->pin_up.p, tgt, bytes);
+        CHK(upload_rows(c, c->pin_up.as<double>(), m, ld, md, c->tx, c->ty, &c->tz));
+        HIPCHK(hipEventRecord(c->up_ev, c->stream));
+        return FICP_OK;
+    }
     CHK(upload_rows(c, tgt, m, ld, md, c->tx, c->ty, &c->tz));
     return sync(c);
 }

@@ -201,7 +201,10 @@ struct ficp_ctx {
 
     PinBuf pin;  // pinned staging of results on their way to the caller's (pageable) arrays
     PinBuf pin_xy{nullptr, 0, hipHostMallocCoherent};  // k_small_run's XY, stored by the kernel
+    PinBuf pin_up;             // bounce buffer of small target uploads (ficp_set_target)
+    hipEvent_t up_ev = nullptr;  // the last upload from pin_up
 };
+constexpr size_t kBounceBytes = 1 << 20;  // ficp_set_target layers up to 1 MB bounce (no sync)
 
 namespace ficp_capi {
 

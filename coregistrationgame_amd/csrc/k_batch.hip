@@ -16,6 +16,7 @@
 #include "frmsd_bounds.h"
 
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -168,39 +169,43 @@ __device__ __forceinline__ T wave_incl_scan(T x) {
     return x;
 }
 
+template <int NW>
 struct SelRed {
-    double d[SWV];
-    u64 a[SWV], b[SWV];
-    unsigned c[SWV];
-    long long l[SWV];
+    double d[NW];
+    u64 a[NW], b[NW];
+    unsigned c[NW];
+    long long l[NW];
 };
 
 // block sum of a double in a fixed order (deterministic, same value on every thread)
-__device__ __forceinline__ double blk_sum_d(double x, SelRed &r) {
+template <int NW>
+__device__ __forceinline__ double blk_sum_d(double x, SelRed<NW> &r) {
     x = wave_sum_d(x);
     if ((threadIdx.x & 63) == 0) r.d[threadIdx.x >> 6] = x;
     __syncthreads();
     double t = r.d[0];
 #pragma unroll
-    for (int w = 1; w < SWV; ++w) t = t + r.d[w];
+    for (int w = 1; w < NW; ++w) t = t + r.d[w];
     __syncthreads();
     return t;
 }
 
-__device__ __forceinline__ double blk_min_d(double x, SelRed &r) {
+template <int NW>
+__device__ __forceinline__ double blk_min_d(double x, SelRed<NW> &r) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, 64));
     if ((threadIdx.x & 63) == 0) r.d[threadIdx.x >> 6] = x;
     __syncthreads();
     double t = r.d[0];
 #pragma unroll
-    for (int w = 1; w < SWV; ++w) t = fmin(t, r.d[w]);
+    for (int w = 1; w < NW; ++w) t = fmin(t, r.d[w]);
     __syncthreads();
     return t;
 }
 
 // {max a, max b, sum c} over the block
-__device__ __forceinline__ void blk_max2_sum(u64 &a, u64 &b, unsigned &c, SelRed &r) {
+template <int NW>
+__device__ __forceinline__ void blk_max2_sum(u64 &a, u64 &b, unsigned &c, SelRed<NW> &r) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const u64 xa = __shfl_xor(a, o, 64), xb = __shfl_xor(b, o, 64);
@@ -218,7 +223,7 @@ __device__ __forceinline__ void blk_max2_sum(u64 &a, u64 &b, unsigned &c, SelRed
     b = r.b[0];
     c = r.c[0];
 #pragma unroll
-    for (int w = 1; w < SWV; ++w) {
+    for (int w = 1; w < NW; ++w) {
         a = r.a[w] > a ? r.a[w] : a;
         b = r.b[w] > b ? r.b[w] : b;
         c += r.c[w];
@@ -227,7 +232,8 @@ __device__ __forceinline__ void blk_max2_sum(u64 &a, u64 &b, unsigned &c, SelRed
 }
 
 // {min lo, max hi} over the block
-__device__ __forceinline__ void blk_minmax_ll(long long &lo, long long &hi, SelRed &r) {
+template <int NW>
+__device__ __forceinline__ void blk_minmax_ll(long long &lo, long long &hi, SelRed<NW> &r) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         lo = min(lo, (long long)__shfl_xor(lo, o, 64));
@@ -241,7 +247,7 @@ __device__ __forceinline__ void blk_minmax_ll(long long &lo, long long &hi, SelR
     lo = r.l[0];
     hi = (long long)r.a[0];
 #pragma unroll
-    for (int w = 1; w < SWV; ++w) {
+    for (int w = 1; w < NW; ++w) {
         lo = min(lo, r.l[w]);
         hi = max(hi, (long long)r.a[w]);
     }
@@ -249,7 +255,8 @@ __device__ __forceinline__ void blk_minmax_ll(long long &lo, long long &hi, SelR
 }
 
 // exclusive scan over the block (thread order) of a count and a sum; fixed schedule
-__device__ __forceinline__ void blk_excl_scan2(unsigned &c, double &x, SelRed &r) {
+template <int NW>
+__device__ __forceinline__ void blk_excl_scan2(unsigned &c, double &x, SelRed<NW> &r) {
     const unsigned ci = wave_incl_scan(c);
     const double xi = wave_incl_scan(x);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -276,7 +283,8 @@ __device__ __forceinline__ void blk_excl_scan2(unsigned &c, double &x, SelRed &r
 }
 
 // exclusive scan of a double over the block + the block total; fixed schedule
-__device__ __forceinline__ double blk_excl_scan_d(double x, double &total, SelRed &r) {
+template <int NW>
+__device__ __forceinline__ double blk_excl_scan_d(double x, double &total, SelRed<NW> &r) {
     const double xi = wave_incl_scan(x);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double xe = __shfl_up(xi, 1, 64);
@@ -285,7 +293,7 @@ __device__ __forceinline__ double blk_excl_scan_d(double x, double &total, SelRe
     __syncthreads();
     double xp = 0.0, tot = 0.0;
 #pragma unroll
-    for (int v = 0; v < SWV; ++v) {
+    for (int v = 0; v < NW; ++v) {
         if (v < w) xp = xp + r.d[v];
         tot = tot + r.d[v];
     }
@@ -294,7 +302,8 @@ __device__ __forceinline__ double blk_excl_scan_d(double x, double &total, SelRe
     return xp + xe;
 }
 
-__device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed &r) {
+template <int NW>
+__device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed<NW> &r) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const double of = __shfl_xor(f, o, 64);
@@ -312,7 +321,7 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed &r) {
     f = r.d[0];
     k = r.l[0];
 #pragma unroll
-    for (int w = 1; w < SWV; ++w)
+    for (int w = 1; w < NW; ++w)
         if (better(r.d[w], r.l[w], f, k)) {
             f = r.d[w];
             k = r.l[w];
@@ -350,16 +359,23 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed &r) {
 #else
 #define BSEL_WPE
 #endif
-template <bool CACHED>
-__global__ __launch_bounds__(ST) BSEL_WPE void k_batch_select(const u64 *__restrict__ key,
+// KST threads (512; 1024 when the plots are fewer than the CUs: half the rows per thread
+// on the same per-plot latency chain), KRPT rows per thread kept in registers
+template <bool CACHED, int KST, int KRPT, bool KRC = (bool)FICP_BSEL_RCACHE>
+__global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__restrict__ key,
                                                      const double *__restrict__ r,
                                                      const int64_t *__restrict__ so,
                                                      const double *__restrict__ lams,
                                                      PlotState *__restrict__ st,
                                                      BatchSelScratch ws) {
+    constexpr int ST = KST;                // (these hide the namespace-scope defaults)
+    constexpr int RPT = KRPT;
+    constexpr bool BSEL_RCACHE = KRC;
+    constexpr int SPER = SB / ST;          // buckets per thread in the scans
+    constexpr int BMAXACT = ST / SPER;     // active bound chunks evaluated one bucket per lane
     __shared__ unsigned s_cnt[SB];  // counts, then exclusive bucket starts
     __shared__ double s_sum[SB];    // sums, then per-bucket fill counters (as unsigned)
-    __shared__ SelRed red;
+    __shared__ SelRed<ST / 64> red;
     __shared__ long long s_k[2];
     __shared__ u64 l_wk[WCAP], l_sk[WCAP];       // a small window's rows (phases 4-6)
     __shared__ double l_wr[WCAP], l_sr[WCAP];
@@ -916,12 +932,19 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
                                int nplots, int64_t max_rows, const double *lambdas,
                                PlotState *st, BatchSelScratch ws, hipStream_t s) {
     if (nplots <= 0) return hipSuccess;
-    if (max_rows <= (int64_t)ST * RPT)
-        hipLaunchKernelGGL(k_batch_select<true>, dim3(nplots), dim3(ST), 0, s, key, r, so, lambdas, st,
-                           ws);
+    // fewer plots than CUs: 1024-thread workgroups, 10 cached rows per thread (C4's 10k-tree
+    // plots); FICP_BSEL_WIDE=0/1 forces the choice (A/B)
+    const char *wv = getenv("FICP_BSEL_WIDE");
+    const bool wide = wv ? atoi(wv) != 0 : nplots < 256;
+    if (wide && max_rows <= (int64_t)1024 * 10)
+        hipLaunchKernelGGL((k_batch_select<true, 1024, 10, false>), dim3(nplots), dim3(1024), 0, s, key,
+                           r, so, lambdas, st, ws);
+    else if (max_rows <= (int64_t)ST * RPT)
+        hipLaunchKernelGGL((k_batch_select<true, ST, RPT>), dim3(nplots), dim3(ST), 0, s, key, r, so,
+                           lambdas, st, ws);
     else
-        hipLaunchKernelGGL(k_batch_select<false>, dim3(nplots), dim3(ST), 0, s, key, r, so, lambdas,
-                           st, ws);
+        hipLaunchKernelGGL((k_batch_select<false, ST, RPT>), dim3(nplots), dim3(ST), 0, s, key, r, so,
+                           lambdas, st, ws);
     return hipGetLastError();
 }
 

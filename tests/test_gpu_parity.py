@@ -341,9 +341,9 @@ def test_run_vs_oracle_100k(oracle):
 # left): the fused fit, the two fallback paths the bucket sort takes for
 # layers it cannot plan (global-atomic grid build, 64-bit radix work order), forced here,
 # and the grid density (points per cell: more per cell, more cells per disk scan)
-KNOBS = [{}, {"FICP_FUSE_FIT": "1"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
-         {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "1"},
-         {"FICP_GRID_PER_CELL": "4"}, {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_SPLIT": "1", "FICP_FUSE_FIT": "1"}]
+KNOBS = [{}, {"FICP_FUSE_FIT": "0"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
+         {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "0"},
+         {"FICP_GRID_PER_CELL": "4"}, {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_SPLIT": "1", "FICP_FUSE_FIT": "0"}]
 
 
 @pytest.mark.parametrize("knobs,md", [(k, 3) for k in KNOBS] + [({}, 2), ({"FICP_GRID_ATOMIC": "1"}, 2)],
@@ -351,7 +351,8 @@ KNOBS = [{}, {"FICP_FUSE_FIT": "1"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADI
                          if isinstance(v, dict) else f"md{v}")
 def test_run_untraced_vs_oracle_100k(oracle, knobs, md, monkeypatch):
     """The production loop (no traces: the selection's last kernel runs the loop step; with
-    FICP_FUSE_FIT=1 it also runs the rigid fit; half-step lookahead, certified NN reuse)
+    by default it also runs the rigid fit, FICP_FUSE_FIT=0 a separate pass; half-step
+    lookahead, certified NN reuse)
     against the pinned oracle at 100k, 3-D and 2-D matching, under every kernel switch."""
     from coregistrationgame_amd import FractionalICP, synth
     for k, v in knobs.items():

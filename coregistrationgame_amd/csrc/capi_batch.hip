@@ -32,8 +32,13 @@ struct BatchBufs {
     DevBuf fpart, fctr;                    // batch fit: per-chunk sums, per-plot arrivals
     unsigned fctr_init_gen = 0;            // fctr allocation whose counters are zeroed
     int *h_flag = nullptr;                 // coherent pinned ring: plots still running
+    PinBuf up;                             // pinned staging of the small per-run uploads
+    PinBuf rep{nullptr, 0, hipHostMallocCoherent};  // report kernel target: states + flag
+    hipStream_t s2 = nullptr;              // the second sub-batch's stream (few plots)
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 constexpr int kBatchRing = 4;
+constexpr int kMaxSub = 2;  // sub-batches on their own streams (h_flag holds kMaxSub rings)
 
 void batch_release(BatchBufs *b) {
     if (!b) return;
@@ -45,6 +50,11 @@ void batch_release(BatchBufs *b) {
                       &b->tx,       &b->ty,      &b->tz,       &b->stage, &b->bp,
                       &b->dz2,      &b->bs_tmp,  &b->fpart,   &b->fctr};
     for (DevBuf *d : bufs) d->release();
+    b->up.release();
+    b->rep.release();
+    if (b->s2) (void)hipStreamDestroy(b->s2);
+    if (b->fork) (void)hipEventDestroy(b->fork);
+    if (b->join) (void)hipEventDestroy(b->join);
     if (b->h_flag) (void)hipHostFree(b->h_flag);
     delete b;
 }
@@ -71,9 +81,19 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
                       std::vector<PlotGrid> &grids) {
     CHK(b.bb.ensure((size_t)nplots * 4 * 8));
     HIPCHK(launch_batch_bbox(tx, ty, b.to.as<int64_t>(), nplots, b.bb.as<double>(), c->stream));
-    std::vector<double> bb((size_t)nplots * 4);
-    HIPCHK(hipMemcpyAsync(bb.data(), b.bb.p, bb.size() * 8, hipMemcpyDeviceToHost, c->stream));
-    CHK(sync(c));
+    // the bboxes through the report kernel into coherent pinned memory and a polled flag
+    // (a pageable D2H copy + stream sync cost more idle device)
+    const size_t bbytes = (size_t)nplots * 4 * 8;
+    CHK(b.rep.ensure(std::max<size_t>(bbytes, (size_t)nplots * sizeof(PlotState)) + 64));
+    int *bflag = (int *)(b.rep.as<char>() + bbytes + 32);
+    __atomic_store_n(bflag, -1, __ATOMIC_RELAXED);
+    HIPCHK(launch_report(ReportSeg{b.bb.p, b.rep.p, (int)(bbytes / 4)}, ReportSeg{}, ReportSeg{},
+                         bflag, nullptr, c->stream));
+    {
+        int v = 0;
+        CHK(poll_flag(c, bflag, v));
+    }
+    const double *bb = b.rep.as<const double>();
     grids.assign(nplots, PlotGrid{});
     int64_t ncells = 0;
     for (int32_t p = 0; p < nplots; ++p) {
@@ -153,21 +173,27 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
     const int64_t n = so_h[nplots], m = to_h[nplots];
     BatchBufs &b = *batch_of(c);
     if (!b.h_flag)
-        HIPCHK(hipHostMalloc((void **)&b.h_flag, kBatchRing * sizeof(int), hipHostMallocCoherent));
+        HIPCHK(hipHostMalloc((void **)&b.h_flag, kMaxSub * kBatchRing * sizeof(int),
+                             hipHostMallocCoherent));
     CHK(b.so.ensure((size_t)(nplots + 1) * 8));
     CHK(b.to.ensure((size_t)(nplots + 1) * 8));
     CHK(b.st.ensure((size_t)nplots * sizeof(PlotState)));
     CHK(b.lams.ensure((size_t)std::max(nstages, 1) * 8));
-    HIPCHK(hipMemcpyAsync(b.so.p, so_h, (size_t)(nplots + 1) * 8, hipMemcpyHostToDevice,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(b.to.p, to_h, (size_t)(nplots + 1) * 8, hipMemcpyHostToDevice,
-                          c->stream));
-    if (nstages > 0)
-        HIPCHK(hipMemcpyAsync(b.lams.p, lambdas, (size_t)nstages * 8, hipMemcpyHostToDevice,
-                              c->stream));
+    {
+        // offsets and lambdas through pinned staging (three pageable copies were three
+        // host-blocking calls); the previous run of this context has finished with it
+        const size_t off = (size_t)(nplots + 1) * 8, nl = (size_t)std::max(nstages, 0) * 8;
+        CHK(b.up.ensure(2 * off + nl + 64));
+        char *u = b.up.as<char>();
+        memcpy(u, so_h, off);
+        memcpy(u + off, to_h, off);
+        if (nl) memcpy(u + 2 * off, lambdas, nl);
+        HIPCHK(hipMemcpyAsync(b.so.p, u, off, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(b.to.p, u + off, off, hipMemcpyHostToDevice, c->stream));
+        if (nl) HIPCHK(hipMemcpyAsync(b.lams.p, u + 2 * off, nl, hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(launch_batch_init(b.so.as<int64_t>(), b.to.as<int64_t>(), nplots, nstages,
                              b.st.as<PlotState>(), c->stream));
-    HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (n > 0 && m > 0 && nstages > 0) {
         std::vector<PlotGrid> grids;
         {
@@ -223,49 +249,118 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         }
         // every plot makes at most nstages * (max_iter + 1) NN calls
         const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1) + 1;
-        auto enqueue = [&](int64_t bit) -> int {
-            int *flag = &b.h_flag[bit % kBatchRing];
+        // Few plots (a rank's share of a multi-GPU batch: 128 plots at N = 8): two sub-
+        // batches, each on its own stream, so one half's latency-bound selection (one
+        // workgroup per plot, half the CUs idle) and fit run beside the other half's NN.
+        // The plots are independent (app.py:658-660), so the split changes no result.
+        // FICP_BATCH_STREAMS=1|2 forces the count.
+        int nsub = (nplots >= 64 && nplots <= 384) ? 2 : 1;
+        if (const char *e = getenv("FICP_BATCH_STREAMS")) nsub = std::max(1, std::min(kMaxSub, atoi(e)));
+        if (nsub > 1) {
+            if (!b.s2) HIPCHK(hipStreamCreateWithFlags(&b.s2, hipStreamNonBlocking));
+            if (!b.fork) HIPCHK(hipEventCreateWithFlags(&b.fork, hipEventDisableTiming));
+            if (!b.join) HIPCHK(hipEventCreateWithFlags(&b.join, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(b.fork, c->stream));  // the grids, states and offsets are ready
+            HIPCHK(hipStreamWaitEvent(b.s2, b.fork, 0));
+        }
+        struct Sub {
+            int p0, np;
+            int64_t r0, nr;
+            hipStream_t s;
+            int *ring;
+            bool finished;
+        };
+        Sub subs[kMaxSub];
+        for (int q = 0; q < nsub; ++q) {
+            Sub &u = subs[q];
+            u.p0 = (int)((int64_t)nplots * q / nsub);
+            u.np = (int)((int64_t)nplots * (q + 1) / nsub) - u.p0;
+            u.r0 = so_h[u.p0];
+            u.nr = so_h[u.p0 + u.np] - u.r0;
+            u.s = q == 0 ? c->stream : b.s2;
+            u.ring = b.h_flag + q * kBatchRing;
+            u.finished = u.np == 0;
+        }
+        const size_t fch = (size_t)batch_fit_chunks(max_rows) * 8;  // fit partial doubles per plot
+        auto enqueue = [&](Sub &u, int64_t bit) -> int {
+            int *flag = &u.ring[bit % kBatchRing];
             __atomic_store_n(flag, -1, __ATOMIC_RELEASE);
+            const bool prof = u.s == c->stream;  // kernel timing covers the first sub-batch
+            PlotState *su = st + u.p0;
+            const int64_t *sou = b.so.as<int64_t>() + u.p0;
+            const PlotGrid *gu = b.grids.as<PlotGrid>() + u.p0;
             {
-                ProfScope ps(c, P_FIT, "batch_fit");
+                ProfScope ps(c, prof ? P_FIT : 0, "batch_fit");
                 HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
-                                        b.key.as<unsigned long long>(), b.so.as<int64_t>(),
-                                        b.grids.as<PlotGrid>(), nplots, max_rows, allow_refl, st,
-                                        b.fpart.as<double>(), b.fctr.as<unsigned>(), c->stream));
+                                        b.key.as<unsigned long long>(), sou, gu, u.np, max_rows,
+                                        allow_refl, su, b.fpart.as<double>() + (size_t)u.p0 * fch,
+                                        b.fctr.as<unsigned>() + u.p0, u.s));
             }
-            a.warm_c = bit > 0 ? 1 : 0;
+            NNArgs au = a;  // this sub-batch's trees: the per-tree arrays from its first row
+            au.warm_c = bit > 0 ? 1 : 0;
+            au.sx = sx + u.r0;
+            au.sy = sy + u.r0;
+            au.sz = a.sz ? a.sz + u.r0 : nullptr;
+            au.n = u.nr;
+            au.r = a.r + u.r0;
+            au.key = a.key + u.r0;
+            au.cx = a.cx + u.r0;
+            au.cy = a.cy + u.r0;
+            au.out_bp = a.out_bp + u.r0;
+            au.gap = a.gap + u.r0;
+            au.dz2 = a.dz2 ? a.dz2 + u.r0 : nullptr;
             {
-                ProfScope ps(c, P_NN, "nn_grid_batch");
-                HIPCHK(launch_nn_grid_batch(a, b.plot_of.as<int32_t>(), b.grids.as<PlotGrid>(),
+                ProfScope ps(c, prof ? P_NN : 0, "nn_grid_batch");
+                HIPCHK(launch_nn_grid_batch(au, b.plot_of.as<int32_t>() + u.r0, b.grids.as<PlotGrid>(),
                                             b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
-                                            md, c->stream));
+                                            md, u.s));
             }
             {
-                ProfScope ps(c, P_FRAC, "batch_select");
-                HIPCHK(launch_batch_select(b.key.as<unsigned long long>(), b.r.as<double>(),
-                                           b.so.as<int64_t>(), nplots, max_rows,
-                                           b.lams.as<double>(), st, ws, c->stream));
+                ProfScope ps(c, prof ? P_FRAC : 0, "batch_select");
+                HIPCHK(launch_batch_select(b.key.as<unsigned long long>(), b.r.as<double>(), sou, u.np,
+                                           max_rows, b.lams.as<double>(), su, ws, u.s));
             }
-            HIPCHK(launch_batch_update(nplots, nstages, threshold, max_iter, st, flag, c->stream));
+            HIPCHK(launch_batch_update(u.np, nstages, threshold, max_iter, su, flag, u.s));
             return FICP_OK;
         };
-        bool finished = false;
-        CHK(enqueue(0));
-        for (int64_t w = 0; w < cap && !finished; ++w) {
-            if (w + 1 < cap) CHK(enqueue(w + 1));  // one batch iteration ahead
-            int live = 0;
-            CHK(poll_flag(c, &b.h_flag[w % kBatchRing], live));
-            finished = live == 0;
+        for (int q = 0; q < nsub; ++q)
+            if (!subs[q].finished) CHK(enqueue(subs[q], 0));
+        for (int64_t w = 0; w < cap; ++w) {
+            bool all = true;
+            for (int q = 0; q < nsub; ++q)  // one batch iteration ahead, per sub-batch
+                if (!subs[q].finished && w + 1 < cap) CHK(enqueue(subs[q], w + 1));
+            for (int q = 0; q < nsub; ++q) {
+                Sub &u = subs[q];
+                if (u.finished) continue;
+                int live = 0;
+                CHK(poll_flag(c, &u.ring[w % kBatchRing], live));
+                u.finished = live == 0;
+                all = all && u.finished;
+            }
+            if (all) break;
         }
-        if (!finished) return fail(FICP_EHIP, "batch did not converge within its bound");
+        for (int q = 0; q < nsub; ++q)
+            if (!subs[q].finished) return fail(FICP_EHIP, "batch did not converge within its bound");
+        if (nsub > 1) {
+            HIPCHK(hipEventRecord(b.join, b.s2));
+            HIPCHK(hipStreamWaitEvent(c->stream, b.join, 0));
+        }
 
     }
-    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    // one report kernel copies the plot states into coherent pinned memory and raises a
+    // flag the host polls (a pageable D2H copy + stream sync left ~40 us of idle device)
+    const size_t sbytes = (size_t)nplots * sizeof(PlotState);
+    CHK(b.rep.ensure(sbytes + 64));
+    int *rflag = (int *)(b.rep.as<char>() + sbytes + 32);
+    __atomic_store_n(rflag, -1, __ATOMIC_RELAXED);
+    HIPCHK(launch_report(ReportSeg{b.st.p, b.rep.p, per_plot ? (int)(sbytes / 4) : 0}, ReportSeg{},
+                         ReportSeg{}, rflag, nullptr, c->stream));
+    {
+        int v = 0;
+        CHK(poll_flag(c, rflag, v));
+    }
     if (per_plot) {
-        std::vector<PlotState> hs((size_t)nplots);
-        HIPCHK(hipMemcpyAsync(hs.data(), b.st.p, hs.size() * sizeof(PlotState),
-                              hipMemcpyDeviceToHost, c->stream));
-        CHK(sync(c));
+        const PlotState *hs = b.rep.as<const PlotState>();
         for (int32_t p = 0; p < nplots; ++p) {
             const PlotState &s = hs[p];
             ficp_plot_stats &o = per_plot[p];
@@ -278,7 +373,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             o.iters[1] = s.iters1;
         }
     }
-    return sync(c);
+    return FICP_OK;  // the report's flag follows every kernel of the run on the stream
 }
 
 int check_batch_args(int32_t nplots, int32_t md, int32_t nstages, const double *lambdas) {

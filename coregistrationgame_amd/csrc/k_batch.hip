@@ -932,14 +932,9 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
                                int nplots, int64_t max_rows, const double *lambdas,
                                PlotState *st, BatchSelScratch ws, hipStream_t s) {
     if (nplots <= 0) return hipSuccess;
-    // fewer plots than CUs: 1024-thread workgroups, 10 cached rows per thread (C4's 10k-tree
-    // plots); FICP_BSEL_WIDE=0/1 forces the choice (A/B)
-    const char *wv = getenv("FICP_BSEL_WIDE");
-    const bool wide = wv ? atoi(wv) != 0 : nplots < 256;
-    if (wide && max_rows <= (int64_t)1024 * 10)
-        hipLaunchKernelGGL((k_batch_select<true, 1024, 10, false>), dim3(nplots), dim3(1024), 0, s, key,
-                           r, so, lambdas, st, ws);
-    else if (max_rows <= (int64_t)ST * RPT)
+    // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
+    // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers)
+    if (max_rows <= (int64_t)ST * RPT)
         hipLaunchKernelGGL((k_batch_select<true, ST, RPT>), dim3(nplots), dim3(ST), 0, s, key, r, so,
                            lambdas, st, ws);
     else

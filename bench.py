@@ -113,20 +113,28 @@ def launch(n: int, argv: list[str]) -> int:
 
 # ----------------------------------------------------------------------------- helpers
 class DevArray:
-    """A device buffer owned through libficp (no torch types at the boundary)."""
+    """A device buffer owned through libficp (no torch types at the boundary): one column,
+    or k columns of n rows stored one after another (host shape (k, n))."""
 
     def __init__(self, ctx: _lib.Context, host: np.ndarray):
         host = np.ascontiguousarray(host, dtype=np.float64)
-        self.ctx, self.n = ctx, host.size
+        self.ctx = ctx
+        self.n = host.shape[-1]
+        self.k = host.size // max(self.n, 1)
         p = _lib.C.c_void_p()
-        _lib._check(_lib.lib().ficp_dev_alloc(ctx.h, host.nbytes, _lib.C.byref(p)))
+        _lib._check(_lib.lib().ficp_dev_alloc(ctx.h, max(host.nbytes, 8), _lib.C.byref(p)))
         self.ptr = p.value
         _lib._check(_lib.lib().ficp_memcpy_h2d(ctx.h, _lib.C.c_void_p(self.ptr), host.ctypes.data_as(_lib.C.c_void_p),
                                                host.nbytes))
 
-    def copy_from(self, other: "DevArray"):
+    def col(self, j: int) -> int:
+        return self.ptr + 8 * self.n * j
+
+    def copy_from(self, other: "DevArray", cols: int | None = None):
+        """The first `cols` columns (all by default) of other, in one device copy."""
+        c = self.k if cols is None else cols
         _lib._check(_lib.lib().ficp_memcpy_d2d(self.ctx.h, _lib.C.c_void_p(self.ptr), _lib.C.c_void_p(other.ptr),
-                                               8 * self.n))
+                                               8 * self.n * c))
 
     def free(self):
         _lib.lib().ficp_dev_free(self.ctx.h, _lib.C.c_void_p(self.ptr))
@@ -391,17 +399,15 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
     n, m, f, seed0, md, thr, max_it, desc = WORKLOADS[wl]
     plot = synth.make_plot(n, m, f, seed0 + rank, md=md)
     ctx = _lib.Context(local, {"auto": 0, "brute": 1, "grid": 2}[args.nn_mode])
-    cols = [plot.source[:, j] for j in range(md)]
-    src0 = [DevArray(ctx, c) for c in cols]          # pristine source, resident
-    src = [DevArray(ctx, c) for c in cols]           # working copy (x, y move)
-    tgt = [DevArray(ctx, plot.target[:, j]) for j in range(md)]
+    src0 = DevArray(ctx, plot.source.T)   # pristine source columns, resident
+    src = DevArray(ctx, plot.source.T)    # working copy (x, y move)
+    tgt = DevArray(ctx, plot.target.T)
     lam = [3.0, 0.95 if md == 3 else 1.3]
 
     def step():
-        src[0].copy_from(src0[0])
-        src[1].copy_from(src0[1])
-        ctx.set_target_device(tgt[0].ptr, tgt[1].ptr, tgt[2].ptr if md == 3 else 0, m, md)
-        return ctx.run_device(src[0].ptr, src[1].ptr, src[2].ptr if md == 3 else 0, n, lam, thr, max_it)
+        src.copy_from(src0, cols=2)  # x, y restored in one copy
+        ctx.set_target_device(tgt.col(0), tgt.col(1), tgt.col(2) if md == 3 else 0, m, md)
+        return ctx.run_device(src.col(0), src.col(1), src.col(2) if md == 3 else 0, n, lam, thr, max_it)
 
     def barrier():
         ctx.synchronize()
@@ -468,7 +474,7 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
                                    "unit": "GB/s", "peak": HBM_PEAK_GBS,
                                    "frac": ib * fits_all / dt_max / 1e9 / HBM_PEAK_GBS},
         }
-    for a in src0 + src + tgt:
+    for a in (src0, src, tgt):
         a.free()
     ctx.close()
     if rank == 0 and world == 1 and with_cpu:
@@ -501,16 +507,15 @@ def bench_batch(args, rank, world, local, D, steps, warmup, with_cpu, share_of=0
     to[1:] = np.cumsum([len(pl.target) for pl in plots])
     S = np.concatenate([pl.source for pl in plots])
     T = np.concatenate([pl.target for pl in plots])
-    src0 = [DevArray(ctx, S[:, j]) for j in range(md)]
-    src = [DevArray(ctx, S[:, j]) for j in range(md)]
-    tgt = [DevArray(ctx, T[:, j]) for j in range(md)]
+    src0 = DevArray(ctx, S.T)
+    src = DevArray(ctx, S.T)
+    tgt = DevArray(ctx, T.T)
     lam = [3.0, 0.95 if md == 3 else 1.3]
 
     def step():
-        src[0].copy_from(src0[0])
-        src[1].copy_from(src0[1])
-        return ctx.run_batch_device(so, src[0].ptr, src[1].ptr, src[2].ptr if md == 3 else 0, to,
-                                    tgt[0].ptr, tgt[1].ptr, tgt[2].ptr if md == 3 else 0, md, lam, thr, max_it)
+        src.copy_from(src0, cols=2)
+        return ctx.run_batch_device(so, src.col(0), src.col(1), src.col(2) if md == 3 else 0, to,
+                                    tgt.col(0), tgt.col(1), tgt.col(2) if md == 3 else 0, md, lam, thr, max_it)
 
     def barrier():
         ctx.synchronize()
@@ -575,7 +580,7 @@ def bench_batch(args, rank, world, local, D, steps, warmup, with_cpu, share_of=0
                                    "frac": ib * fits_all / dt_max / 1e9 / HBM_PEAK_GBS,
                                    "note": "per plot-iteration, SURVEY.md §8(d) bytes at 10k x 10k"},
         }
-    for a in src0 + src + tgt:
+    for a in (src0, src, tgt):
         a.free()
     ctx.close()
     if out is not None:

@@ -220,7 +220,7 @@ unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long lo
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
             bool want_keys, int warm = 0, const int *skip = nullptr,
             const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true,
-            const int *reuse = nullptr) {
+            const int *reuse = nullptr, bool store_key = true) {
     NNArgs a{};
     a.sx = sx;
     a.sy = sy;
@@ -233,7 +233,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.idx = want_idx ? c->idx.as<int32_t>() : nullptr;  // the run loop reads idx only for traces
     a.dist = want_keys ? nullptr : c->dist.as<double>();
     a.r = c->r.as<double>();
-    a.key = want_keys ? c->key.as<unsigned long long>() : nullptr;
+    a.key = (want_keys && store_key) ? c->key.as<unsigned long long>() : nullptr;
     a.val = nullptr;
     a.cx = want_keys ? c->ccx.as<double>() : nullptr;
     a.cy = want_keys ? c->ccy.as<double>() : nullptr;
@@ -477,25 +477,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     CHK(ensure_work(c, n));
     CHK(ensure_bbox(c));
     uint32_t *tflag = sort_timeout_flag(c->sort_tmp.p, n);
-    HIPCHK(launch_run_start(tflag, &c->h_rep->t[0], c->stream, sel_err_word(c->sel_tmp.p, n)));
-    double *wx = sx, *wy = sy;
-    const double *wz = sz;
-    const uint32_t *worig = nullptr;
-    if (use_grid(c, n)) {
-        // the grid build and the work order: one bucket sort of two jobs (four launches)
-        BSJob gj{}, wj{};
-        CHK(ensure_grid(c, &gj));
-        CHK(build_work_order(c, sx, sy, sz, n, &wj));
-        if (gj.n > 0 || wj.n > 0)
-            HIPCHK(launch_bsort2(gj.n > 0 ? gj : wj, gj.n > 0 ? wj : BSJob{}, c->stream));
-        wx = c->wx.as<double>();
-        wy = c->wy.as<double>();
-        wz = sz ? c->wz.as<double>() : nullptr;
-        worig = c->worig.as<uint32_t>();
-    }
     IterState *dst = c->state_dev.as<IterState>();
-    FitIn fa{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
-             nullptr, worig, n, c->pivot_x, c->pivot_y, dst};
     // loop parameters and traces live on the device (k_loop.hip)
     LoopCtl lc{};
     lc.nstages = nstages;
@@ -531,7 +513,25 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             tidx = c->tr_idx.as<int32_t>();
         }
     }
-    HIPCHK(launch_loop_init(dst, lc, c->stream));
+    HIPCHK(launch_run_start(tflag, &c->h_rep->t[0], c->stream, sel_err_word(c->sel_tmp.p, n), dst,
+                            &lc));
+    double *wx = sx, *wy = sy;
+    const double *wz = sz;
+    const uint32_t *worig = nullptr;
+    if (use_grid(c, n)) {
+        // the grid build and the work order: one bucket sort of two jobs (four launches)
+        BSJob gj{}, wj{};
+        CHK(ensure_grid(c, &gj));
+        CHK(build_work_order(c, sx, sy, sz, n, &wj));
+        if (gj.n > 0 || wj.n > 0)
+            HIPCHK(launch_bsort2(gj.n > 0 ? gj : wj, gj.n > 0 ? wj : BSJob{}, c->stream));
+        wx = c->wx.as<double>();
+        wy = c->wy.as<double>();
+        wz = sz ? c->wz.as<double>() : nullptr;
+        worig = c->worig.as<uint32_t>();
+    }
+    FitIn fa{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->key.as<unsigned long long>(),
+             nullptr, worig, n, c->pivot_x, c->pivot_y, dst};
     const FitSrc fsrc{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->pivot_x, c->pivot_y, 1,
                       allow_refl};
     // the rigid fit fused into the selection (gather: the rows below the candidates, their
@@ -551,10 +551,13 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     int64_t j = 0;
     bool finished = nstages <= 0;
     // selection path without traces: the selection's last kernel also runs the loop step
-    // and stores the done flag straight into the pinned ring.  FICP_FUSE_FIT=1 also moves
-    // the rigid fit into gather + final (no k_fit_sums pass): measured slower at C3
-    // (gather +7 us, final +8.5 us vs the 12 us pass), so off by default.
+    // and stores the done flag straight into the pinned ring (and, fuse_fit, the rigid fit
+    // of the next iteration: gather + final, no k_fit_sums pass).
     const bool fused = !tidx;
+    // with the fused loop and fit every consumer of the sort key (histogram, gather) derives
+    // it from r (key_of_r): the NN stores 8 B per row less.  FICP_NN_KEYS=1: stored keys.
+    const char *nk = getenv("FICP_NN_KEYS");
+    const bool keys_from_r = fused && fuse_fit && !(nk && atoi(nk) != 0);
     // part A of iteration i: the fit and the NN call; part B: the selection (and, not
     // fused, the loop step and the flag copy)
     auto enq_a = [&](int64_t i) -> int {
@@ -564,7 +567,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         }
         // (a later stage's head reuses the previous call's outputs: dst->nn_reuse)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
-                    false, tidx != nullptr, &dst->nn_reuse));
+                    false, tidx != nullptr, &dst->nn_reuse, !keys_from_r));
         return FICP_OK;
     };
     auto enq_b = [&](int64_t i) -> int {
@@ -572,7 +575,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
         {
             ProfScope ps(c, P_SORT, "select");
-            HIPCHK(launch_select(c->key.as<unsigned long long>(), worig, c->r.as<double>(), n, 0.0,
+            HIPCHK(launch_select(keys_from_r ? nullptr : c->key.as<unsigned long long>(), worig,
+                                 c->r.as<double>(), n, 0.0,
                                  &dst->lam_cur, range_ptr(c), nn_range_parts(n, c->m, use_grid(c, n)),
                                  c->sel_tmp.p, dst, &dst->done, fused ? &lc : nullptr,
                                  fused ? &c->h_flags[slot] : nullptr, c->stream,
@@ -625,11 +629,10 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // state, the sort's timeout flag and the selection's statistics (each separate sync
     // cost ~40 us of idle device at C3)
     if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
-    HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
     c->h_rep->misc[1] = c->h_rep->misc[2] = c->h_rep->misc[3] = 0u;
     CHK(report_wait(c, ReportSeg{c->state_dev.p, &c->h_rep->st, (int)(sizeof(IterState) / 4)},
                     ReportSeg{tflag, &c->h_rep->misc[0], 1},
-                    ReportSeg{c->sel_stats.p, &c->h_rep->misc[1], 3},
+                    ReportSeg{sel_err_word(c->sel_tmp.p, n), &c->h_rep->misc[1], 3},
                     &c->h_rep->t[1]));
     memcpy(c->h_state, &c->h_rep->st, sizeof(IterState));
     memcpy(c->h_misc, c->h_rep->misc, sizeof c->h_rep->misc);
@@ -1277,8 +1280,8 @@ int ficp_select_fit_device(ficp_ctx *c, const double *x, const double *y, int64_
     if (tf) return fail(FICP_EHIP, "residual sort raised error flag %u (results invalid)", tf);
     if (sel) {
         unsigned ss[3] = {0, 0, 0};
-        HIPCHK(launch_select_stats(c->sel_tmp.p, n, c->sel_stats.as<unsigned>(), c->stream));
-        HIPCHK(hipMemcpyAsync(ss, c->sel_stats.p, 12, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(ss, sel_err_word(c->sel_tmp.p, n), 12, hipMemcpyDeviceToHost,
+                              c->stream));
         CHK(sync(c));
         c->sel_levels = ss[1];
         c->sel_radix = ss[2];
@@ -1308,6 +1311,30 @@ int ficp_dev_alloc(ficp_ctx *c, int64_t bytes, void **ptr) {
 int ficp_dev_free(ficp_ctx *c, void *ptr) {
     CHK(check_ctx(c));
     HIPCHK(hipFree(ptr));
+    return FICP_OK;
+}
+
+int ficp_host_alloc(int64_t bytes, void **ptr) {
+    if (!ptr || bytes < 0) return fail(FICP_EINVAL, "bad arguments");
+    *ptr = nullptr;
+    HIPCHK(hipHostMalloc(ptr, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+    return FICP_OK;
+}
+
+int ficp_host_free(void *ptr) {
+    if (ptr) HIPCHK(hipHostFree(ptr));
+    return FICP_OK;
+}
+
+int ficp_host_copy(void *dst, const void *src, int64_t bytes) {
+    if (bytes < 0 || (bytes > 0 && (!dst || !src))) return fail(FICP_EINVAL, "bad arguments");
+    char *d = (char *)dst;
+    const char *s = (const char *)src;
+    // 2 MiB pieces per thread at least: below that the thread start costs more than it saves
+    host_parallel((bytes + 15) / 16, [&](int64_t a, int64_t b) {
+        const int64_t lo = a * 16, hi = std::min<int64_t>(b * 16, bytes);
+        if (hi > lo) memcpy(d + lo, s + lo, (size_t)(hi - lo));
+    });
     return FICP_OK;
 }
 
@@ -1579,10 +1606,10 @@ int ficp_dist_end(ficp_ctx *c, ficp_stats *st) {
     if (mode == 2)
         HIPCHK(launch_scatter_xy(c->worig.as<uint32_t>(), c->wx.as<double>(), c->wy.as<double>(),
                                  c->dist_n, c->dist_x, c->dist_y, c->stream));
-    HIPCHK(launch_select_stats(c->sel_tmp.p, c->dist_nws, c->sel_stats.as<unsigned>(), c->stream));
     c->h_rep->misc[1] = c->h_rep->misc[2] = c->h_rep->misc[3] = 0u;
     CHK(report_wait(c, ReportSeg{c->state_dev.p, &c->h_rep->st, (int)(sizeof(IterState) / 4)},
-                    ReportSeg{c->sel_stats.p, &c->h_rep->misc[1], 3}, ReportSeg{}));
+                    ReportSeg{sel_err_word(c->sel_tmp.p, c->dist_nws), &c->h_rep->misc[1], 3},
+                    ReportSeg{}));
     const IterState &h = c->h_rep->st;
     if (!h.done) return fail(FICP_EHIP, "distributed ICP loop did not finish");
     if (c->h_rep->misc[1] & 2u)

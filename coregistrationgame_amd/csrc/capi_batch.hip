@@ -249,12 +249,13 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         }
         // every plot makes at most nstages * (max_iter + 1) NN calls
         const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1) + 1;
-        // Few plots (a rank's share of a multi-GPU batch: 128 plots at N = 8): two sub-
-        // batches, each on its own stream, so one half's latency-bound selection (one
-        // workgroup per plot, half the CUs idle) and fit run beside the other half's NN.
-        // The plots are independent (app.py:658-660), so the split changes no result.
-        // FICP_BATCH_STREAMS=1|2 forces the count.
-        int nsub = (nplots >= 64 && nplots <= 384) ? 2 : 1;
+        // From 64 plots on: two sub-batches, each on its own stream, so one half's
+        // latency-bound selection (one workgroup per plot) runs beside the other half's
+        // NN.  The plots are independent (app.py:658-660), so the split changes no result.
+        // Measured with the fused step (tools/r3_iter6.sh, plot-it/s): 128 plots 846k vs
+        // 834k, 512 1,082k vs 1,019k, 1024 1,119k vs 1,061k.  FICP_BATCH_STREAMS=1|2
+        // forces the count.
+        int nsub = nplots >= 64 ? 2 : 1;
         if (const char *e = getenv("FICP_BATCH_STREAMS")) nsub = std::max(1, std::min(kMaxSub, atoi(e)));
         if (nsub > 1) {
             if (!b.s2) HIPCHK(hipStreamCreateWithFlags(&b.s2, hipStreamNonBlocking));
@@ -282,6 +283,13 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             u.finished = u.np == 0;
         }
         const size_t fch = (size_t)batch_fit_chunks(max_rows) * 8;  // fit partial doubles per plot
+        // the loop step and the next body's fit run inside the selection (one workgroup per
+        // plot, its rows L2-hot): two launches per batch iteration fewer.  FICP_BATCH_FUSE=0:
+        // the separate k_batch_fit and k_batch_update launches.
+        const char *bf = getenv("FICP_BATCH_FUSE");
+        const bool bfuse = !(bf && atoi(bf) == 0);
+        const BatchStepArgs step{sx, sy, b.ccx.as<double>(), b.ccy.as<double>(), b.grids.as<PlotGrid>(),
+                                 allow_refl, nstages, max_iter, threshold};
         auto enqueue = [&](Sub &u, int64_t bit) -> int {
             int *flag = &u.ring[bit % kBatchRing];
             __atomic_store_n(flag, -1, __ATOMIC_RELEASE);
@@ -289,7 +297,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             PlotState *su = st + u.p0;
             const int64_t *sou = b.so.as<int64_t>() + u.p0;
             const PlotGrid *gu = b.grids.as<PlotGrid>() + u.p0;
-            {
+            if (!bfuse) {
                 ProfScope ps(c, prof ? P_FIT : 0, "batch_fit");
                 HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
                                         b.key.as<unsigned long long>(), sou, gu, u.np, max_rows,
@@ -318,9 +326,11 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             {
                 ProfScope ps(c, prof ? P_FRAC : 0, "batch_select");
                 HIPCHK(launch_batch_select(b.key.as<unsigned long long>(), b.r.as<double>(), sou, u.np,
-                                           max_rows, b.lams.as<double>(), su, ws, u.s));
+                                           max_rows, b.lams.as<double>(), su, ws, u.s,
+                                           bfuse ? &step : nullptr));
             }
-            HIPCHK(launch_batch_update(u.np, nstages, threshold, max_iter, su, flag, u.s));
+            if (bfuse) HIPCHK(launch_batch_live(u.np, su, flag, u.s));
+            else HIPCHK(launch_batch_update(u.np, nstages, threshold, max_iter, su, flag, u.s));
             return FICP_OK;
         };
         for (int q = 0; q < nsub; ++q)

@@ -21,6 +21,12 @@ __device__ __forceinline__ unsigned long long ordkey(double v) {
     return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
 }
 
+// the sort key of a row from its squared distance r: ordkey(sqrt(r)), bit for bit what the
+// NN kernels store (write_out / cert_try).  The selection recomputes it from r when the NN
+// did not store keys (C3 fused loop: 8 B per row less written by the NN and read by the
+// histogram and the gather).
+__device__ __forceinline__ unsigned long long key_of_r(double r) { return ordkey(sqrt(r)); }
+
 // wave-wide max of two u64 (all 64 lanes must be active)
 __device__ __forceinline__ void wave_range_reduce(unsigned long long &a, unsigned long long &b) {
 #pragma unroll
@@ -217,8 +223,16 @@ struct FitSrc {
 // pivot) over the k selected rows: sum s'x, s'y, t'x, t'y, s'x t'x, s'x t'y, s'y t'x,
 // s'y t'y.  Closed-form 2-D Kabsch (ficp.py:89-110); writes T, the
 // centroids and H into *st.
+// the closed-form solve alone: T (row-major 3x3) from the 8 sums, centroids and H out
+__device__ inline void fit_solve_T(const double c[8], double k, double px, double py,
+                                   int allow_refl, double *T, double *cent4 = nullptr,
+                                   double *H4 = nullptr);
 __device__ inline void fit_solve(const double c[8], double k, double px, double py,
                                  int allow_refl, IterState *st) {
+    fit_solve_T(c, k, px, py, allow_refl, st->T, &st->csx, st->H);
+}
+__device__ inline void fit_solve_T(const double c[8], double k, double px, double py,
+                                   int allow_refl, double *T, double *cent4, double *H4) {
     // centroids of the pivot-shifted pairs, then H = sum s't'^T - k cs' ct'^T
     const double csx = c[0] / k, csy = c[1] / k, ctx = c[2] / k, cty = c[3] / k;
     double H[4];
@@ -253,20 +267,23 @@ __device__ inline void fit_solve(const double c[8], double k, double px, double 
     // centroids in world coordinates, t = ct - cs @ R^T (ficp.py:105)
     const double wsx = csx + px, wsy = csy + py;
     const double wtx = ctx + px, wty = cty + py;
-    st->T[0] = R00;
-    st->T[1] = R01;
-    st->T[2] = wtx - (wsx * R00 + wsy * R01);
-    st->T[3] = R10;
-    st->T[4] = R11;
-    st->T[5] = wty - (wsx * R10 + wsy * R11);
-    st->T[6] = 0.0;
-    st->T[7] = 0.0;
-    st->T[8] = 1.0;
-    st->csx = csx;
-    st->csy = csy;
-    st->ctx = ctx;
-    st->cty = cty;
-    for (int e = 0; e < 4; ++e) st->H[e] = H[e];
+    T[0] = R00;
+    T[1] = R01;
+    T[2] = wtx - (wsx * R00 + wsy * R01);
+    T[3] = R10;
+    T[4] = R11;
+    T[5] = wty - (wsx * R10 + wsy * R11);
+    T[6] = 0.0;
+    T[7] = 0.0;
+    T[8] = 1.0;
+    if (cent4) {  // IterState: csx, csy, ctx, cty are consecutive
+        cent4[0] = csx;
+        cent4[1] = csy;
+        cent4[2] = ctx;
+        cent4[3] = cty;
+    }
+    if (H4)
+        for (int e = 0; e < 4; ++e) H4[e] = H[e];
 }
 
 // Loop parameters and optional trace buffers of the device-resident loop.
@@ -394,9 +411,11 @@ struct ReportSeg {
 };
 hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg &c, int *flag,
                          unsigned long long *t_end, hipStream_t s);
-// zero the sort timeout flag and stamp the device clock (100 MHz) into *t0 (host)
+// zero the sort timeout flag and stamp the device clock (100 MHz) into *t0 (host); with lc,
+// also initialise the loop state *st (the work of launch_loop_init, one launch less)
 hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s,
-                            unsigned *selerr = nullptr);
+                            unsigned *selerr = nullptr, IterState *st = nullptr,
+                            const LoopCtl *lc = nullptr);
 
 // grid build (k_grid_nn.hip)
 // bbox of (x, y) -> out4 {xmin, xmax, ymin, ymax}; with ox, also copies x, y (z) there
@@ -524,7 +543,6 @@ hipError_t launch_keys_from_doubles(const double *d, int64_t n, unsigned long lo
 int64_t sel_tmp_bytes(int64_t n);
 hipError_t launch_select_init(void *tmp, int64_t n, hipStream_t s);
 // out3 (device): {sticky error bits, refinement levels run, radix fallbacks}
-hipError_t launch_select_stats(void *tmp, int64_t n, unsigned *out3, hipStream_t s);
 // range_parts > 0: range holds the producer's unreduced parts (block_range_store); the
 // histogram kernel reduces them (no launch_range_reduce needed) and stores range[0..1].
 // loop (nullable): the last kernel also runs the k_loop_update step; host_flag (nullable,
@@ -534,7 +552,8 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
                          int64_t range_parts, void *tmp, IterState *st, const int *skip,
                          const LoopCtl *loop, int *host_flag, hipStream_t s,
                          const FitSrc *fit = nullptr, int fault = 0);
-// the selection's sticky error word inside its workspace (k_run_start resets it per run)
+// the selection's sticky error word inside its workspace (k_run_start resets it per run),
+// followed by its statistics words levels and radix (the report reads all three)
 unsigned *sel_err_word(void *tmp, int64_t n);
 // test-only fault injection (ficp_set_fault): block 0 of k_sel_bounds_gather publishes a
 // wrong token, so every gather block times out (ERR_SPIN)
@@ -679,9 +698,19 @@ struct BatchSelScratch {
     uint32_t *wrow, *srow;
     double *wr, *sr;
 };
+// the loop step and the next body's rigid fit inside the selection (nullable: the separate
+// k_batch_fit and k_batch_update launches)
+struct BatchStepArgs {
+    const double *sx, *sy, *cx, *cy;
+    const PlotGrid *grids;
+    int allow_refl, nstages, max_iter;
+    double threshold;
+};
+hipError_t launch_batch_live(int nplots, const PlotState *st, int *flag, hipStream_t s);
 hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,
                                int nplots, int64_t max_rows, const double *lambdas,
-                               PlotState *st, BatchSelScratch ws, hipStream_t s);
+                               PlotState *st, BatchSelScratch ws, hipStream_t s,
+                               const BatchStepArgs *step = nullptr);
 // *flag (coherent pinned host memory) <- number of plots still running
 hipError_t launch_batch_update(int nplots, int nstages, double threshold, int max_iter,
                                PlotState *st, int *flag, hipStream_t s);

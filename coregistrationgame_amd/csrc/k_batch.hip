@@ -136,18 +136,14 @@ __global__ void k_batch_init(const int64_t *so, const int64_t *to, int nplots, i
 #ifndef FICP_BSEL_RCACHE
 #define FICP_BSEL_RCACHE 1  // r kept in registers too (0: re-read from L2 in its two passes)
 #endif
-constexpr bool BSEL_RCACHE = FICP_BSEL_RCACHE;
 #ifndef FICP_BSEL_RPT
 #define FICP_BSEL_RPT 32
 #endif
 constexpr int ST = FICP_BSEL_ST; // threads
-constexpr int SWV = ST / 64;
 constexpr int SB = 2048;         // buckets
 constexpr int SB_LOG = 11;
-constexpr int SPER = SB / ST;    // buckets per thread in the scans
 constexpr int RPT = FICP_BSEL_RPT;  // rows per thread kept in registers (plots <= ST * RPT rows)
 constexpr int SRP = 4;           // window rows per thread per scan chunk
-constexpr int BMAXACT = ST / SPER;  // active bound chunks evaluated one bucket per lane
 constexpr int WCAP = 1024;          // candidate windows up to this many rows stay in LDS
 
 typedef unsigned long long u64;
@@ -329,6 +325,141 @@ __device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed<NW> &
     __syncthreads();
 }
 
+__device__ __forceinline__ void end_stage(PlotState &s, int nstages) {
+    if (s.stage == 0) s.iters0 = s.it;
+    else if (s.stage == 1) s.iters1 = s.it;
+    if (s.stage + 1 < nstages) {
+        s.stage += 1;  // ficp.py:152: lambda switches, stage 2 starts with a head NN call
+        s.phase = PH_HEAD;
+        s.it = 0;
+    } else {
+        s.phase = PH_DONE;
+    }
+}
+
+// one workgroup, one thread per plot (strided): the convergence logic of ficp.py:125-145
+// per plot; the number of plots still running is stored (system scope, release) into
+// *flag in coherent pinned host memory, which the host polls while the next batch
+// iteration already runs
+constexpr int UT = 1024;
+__device__ __forceinline__ void step_plot(PlotState &s, int nstages, double threshold,
+                                          int max_iter) {
+    if (s.phase != PH_DONE) {
+        s.n_nn += 1;
+        if (s.phase == PH_HEAD) {
+            if (s.k == 0) {
+                end_stage(s, nstages);
+            } else {
+                s.cur = s.frmsd;
+                s.phase = PH_LOOP;
+                s.it = 0;
+                if (max_iter <= 0) end_stage(s, nstages);
+            }
+        } else {  // a loop body just ran: fit -> apply -> NN -> fraction
+            s.n_fit += 1;
+            double R[9];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j)
+                    R[3 * i + j] = s.T[3 * i] * s.Ttot[j] + s.T[3 * i + 1] * s.Ttot[3 + j] +
+                                   s.T[3 * i + 2] * s.Ttot[6 + j];
+            for (int e = 0; e < 9; ++e) s.Ttot[e] = R[e];
+            const double nw = s.frmsd;
+            if (s.cur - nw <= threshold) {  // ficp.py:142
+                end_stage(s, nstages);
+            } else {
+                s.cur = nw;
+                s.it += 1;
+                if (s.it >= max_iter) end_stage(s, nstages);
+            }
+        }
+        s.apply = 0;
+    }
+}
+
+__device__ __forceinline__ bool update_plot(PlotState *st, int p, int nstages, double threshold,
+                                            int max_iter) {
+    PlotState s = st[p];
+    if (s.phase != PH_DONE) {
+        step_plot(s, nstages, threshold, max_iter);
+        st[p] = s;
+    }
+    return s.phase != PH_DONE;
+}
+
+
+// The batch iteration's tail in the plot's selection workgroup (BatchStep::fuse): thread
+// 0 takes the loop step of ficp.py:125-145 (k_batch_update's update_plot) with this call's
+// k and FRMSD, and when a loop body follows, the workgroup fits it on this call's selection
+// (ficp.py:133-134: k_batch_fit's 8 pivot-shifted sums of the rows (key, row) <= (tkey,
+// trow), here per thread in row order, then a wave butterfly and the waves in order), so
+// the next NN call applies T with no fit launch in between.
+struct BatchStep {
+    const double *sx, *sy, *cx, *cy;
+    const PlotGrid *grids;
+    int fuse, allow_refl, nstages, max_iter;
+    double threshold;
+};
+
+template <int NW>
+__device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, double frmsd,
+                              u64 tkey, long long trow, int64_t b, int64_t e, const u64 *key,
+                              const BatchStep &bs, double *s8, int *s_flag) {
+    const int t = threadIdx.x;
+    constexpr int NT = NW * 64;
+    if (t == 0) {
+        PlotState s = st[p];
+        s.k = k;
+        s.frac = frac;
+        s.frmsd = frmsd;
+        if (k > 0) {
+            s.tkey = tkey;
+            s.trow = trow;
+        }
+        step_plot(s, bs.nstages, bs.threshold, bs.max_iter);
+        s_flag[0] = s.phase == PH_LOOP && s.k > 0;  // a loop body (fit -> apply -> NN) follows
+        st[p] = s;
+    }
+    __syncthreads();
+    if (!s_flag[0]) return;
+    const PlotGrid g = bs.grids[p];
+    double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    constexpr int FU = 8;  // rows in flight per thread (every load before its predicate)
+    for (int64_t i0 = b + t; i0 < e; i0 += (int64_t)FU * NT) {
+        u64 kv[FU];
+        double xs[FU], ys[FU], xt[FU], yt[FU];
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const int64_t i = i0 + (int64_t)u * NT;
+            const bool in = i < e;
+            kv[u] = in ? key[i] : ~0ULL;
+            xs[u] = in ? bs.sx[i] : 0.0;
+            ys[u] = in ? bs.sy[i] : 0.0;
+            xt[u] = in ? bs.cx[i] : 0.0;
+            yt[u] = in ? bs.cy[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const int64_t i = i0 + (int64_t)u * NT;
+            if (i < e && (kv[u] < tkey || (kv[u] == tkey && i <= trow))) fit_add(c, xs[u], ys[u], xt[u], yt[u], g.px, g.py);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) c[q] = wave_sum_d(c[q]);
+    if ((t & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s8[8 * (t >> 6) + q] = c[q];
+    __syncthreads();
+    if (t != 0) return;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        double v = s8[q];
+        for (int w = 1; w < NW; ++w) v = v + s8[8 * w + q];
+        c[q] = v;
+    }
+    fit_solve_T(c, (double)k, g.px, g.py, bs.allow_refl, st[p].T);
+    st[p].apply = 1;
+}
+
 // every row of the plot with its key and r: CACHED keeps them in registers (RPT per
 // thread, rows past the plot hold r = inf), otherwise they are re-read per pass
 #define SEL_ROWS(BODY)                                                              \
@@ -367,7 +498,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
                                                      const int64_t *__restrict__ so,
                                                      const double *__restrict__ lams,
                                                      PlotState *__restrict__ st,
-                                                     BatchSelScratch ws) {
+                                                     BatchSelScratch ws, BatchStep bs) {
     constexpr int ST = KST;                // (these hide the namespace-scope defaults)
     constexpr int RPT = KRPT;
     constexpr bool BSEL_RCACHE = KRC;
@@ -376,6 +507,8 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     __shared__ unsigned s_cnt[SB];  // counts, then exclusive bucket starts
     __shared__ double s_sum[SB];    // sums, then per-bucket fill counters (as unsigned)
     __shared__ SelRed<ST / 64> red;
+    __shared__ double s_fit8[8 * (ST / 64)];
+    __shared__ int s_fitflag[1];
     __shared__ long long s_k[2];
     __shared__ u64 l_wk[WCAP], l_sk[WCAP];       // a small window's rows (phases 4-6)
     __shared__ double l_wr[WCAP], l_sr[WCAP];
@@ -417,7 +550,9 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     })
     blk_max2_sum(amin, kmax, nfin, red);
     if (nfin == 0) {  // every distance inf / NaN: the reference keeps (0.0, 0)
-        if (t == 0) {
+        if (bs.fuse) {
+            plot_step_fit<ST / 64>(st, p, 0, 0.0, INFINITY, 0, 0, b, e, key, bs, s_fit8, s_fitflag);
+        } else if (t == 0) {
             st[p].k = 0;
             st[p].frac = 0.0;
             st[p].frmsd = INFINITY;
@@ -645,6 +780,14 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
                bt_[6] - bt_[5], bt_[7] - bt_[6], bt_[8] - bt_[2], bt_[9] - bt_[8], bt_[10] - bt_[9],
                bt_[11] - bt_[10], bt_[3] - bt_[11]);
 #endif
+    if (bs.fuse) {
+        const bool none = bk == 0x7fffffffffffffffLL;  // every FRMSD NaN: (0.0, 0)
+        plot_step_fit<ST / 64>(st, p, none ? 0 : bk, none ? 0.0 : (double)bk / (double)N,
+                               none ? INFINITY : bf, none ? 0ULL : sk[bk - K0 - 1],
+                               none ? 0LL : (long long)srw[bk - K0 - 1], b, e, key, bs, s_fit8,
+                               s_fitflag);
+        return;
+    }
     if (t == 0) {
         if (bk == 0x7fffffffffffffffLL) {  // every FRMSD NaN: the reference keeps (0.0, 0)
             st[p].k = 0;
@@ -795,66 +938,29 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
     st[p].apply = 1;
 }
 
-__device__ __forceinline__ void end_stage(PlotState &s, int nstages) {
-    if (s.stage == 0) s.iters0 = s.it;
-    else if (s.stage == 1) s.iters1 = s.it;
-    if (s.stage + 1 < nstages) {
-        s.stage += 1;  // ficp.py:152: lambda switches, stage 2 starts with a head NN call
-        s.phase = PH_HEAD;
-        s.it = 0;
-    } else {
-        s.phase = PH_DONE;
-    }
-}
-
-// one workgroup, one thread per plot (strided): the convergence logic of ficp.py:125-145
-// per plot; the number of plots still running is stored (system scope, release) into
-// *flag in coherent pinned host memory, which the host polls while the next batch
-// iteration already runs
-constexpr int UT = 1024;
-__device__ __forceinline__ bool update_plot(PlotState *st, int p, int nstages, double threshold,
-                                            int max_iter) {
-    PlotState s = st[p];
-    if (s.phase != PH_DONE) {
-        s.n_nn += 1;
-        if (s.phase == PH_HEAD) {
-            if (s.k == 0) {
-                end_stage(s, nstages);
-            } else {
-                s.cur = s.frmsd;
-                s.phase = PH_LOOP;
-                s.it = 0;
-                if (max_iter <= 0) end_stage(s, nstages);
-            }
-        } else {  // a loop body just ran: fit -> apply -> NN -> fraction
-            s.n_fit += 1;
-            double R[9];
-            for (int i = 0; i < 3; ++i)
-                for (int j = 0; j < 3; ++j)
-                    R[3 * i + j] = s.T[3 * i] * s.Ttot[j] + s.T[3 * i + 1] * s.Ttot[3 + j] +
-                                   s.T[3 * i + 2] * s.Ttot[6 + j];
-            for (int e = 0; e < 9; ++e) s.Ttot[e] = R[e];
-            const double nw = s.frmsd;
-            if (s.cur - nw <= threshold) {  // ficp.py:142
-                end_stage(s, nstages);
-            } else {
-                s.cur = nw;
-                s.it += 1;
-                if (s.it >= max_iter) end_stage(s, nstages);
-            }
-        }
-        s.apply = 0;
-        st[p] = s;
-    }
-    return s.phase != PH_DONE;
-}
-
 __global__ __launch_bounds__(UT) void k_batch_update(int nplots, int nstages, double threshold,
                                                      int max_iter, PlotState *st, int *flag) {
     __shared__ int s_live[UT / 64];
     int live = 0;
     for (int p = threadIdx.x; p < nplots; p += UT)
         live += update_plot(st, p, nstages, threshold, max_iter) ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o, 64);
+    if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = live;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < UT / 64; ++w) tot += s_live[w];
+        __threadfence_system();
+        __hip_atomic_store(flag, tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// the number of plots still running (the selection took the loop step: BatchStep::fuse)
+__global__ __launch_bounds__(UT) void k_batch_live(int nplots, const PlotState *st, int *flag) {
+    __shared__ int s_live[UT / 64];
+    int live = 0;
+    for (int p = threadIdx.x; p < nplots; p += UT) live += st[p].phase != PH_DONE ? 1 : 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o, 64);
     if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = live;
@@ -928,18 +1034,37 @@ hipError_t launch_batch_fit_ctr_zero(unsigned *ctr, int n, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_batch_live(int nplots, const PlotState *st, int *flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_batch_live, dim3(1), dim3(UT), 0, s, nplots, st, flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,
                                int nplots, int64_t max_rows, const double *lambdas,
-                               PlotState *st, BatchSelScratch ws, hipStream_t s) {
+                               PlotState *st, BatchSelScratch ws, hipStream_t s,
+                               const BatchStepArgs *step) {
     if (nplots <= 0) return hipSuccess;
+    BatchStep bs{};
+    if (step) {
+        bs.sx = step->sx;
+        bs.sy = step->sy;
+        bs.cx = step->cx;
+        bs.cy = step->cy;
+        bs.grids = step->grids;
+        bs.fuse = 1;
+        bs.allow_refl = step->allow_refl;
+        bs.nstages = step->nstages;
+        bs.max_iter = step->max_iter;
+        bs.threshold = step->threshold;
+    }
     // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
     // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers)
     if (max_rows <= (int64_t)ST * RPT)
         hipLaunchKernelGGL((k_batch_select<true, ST, RPT>), dim3(nplots), dim3(ST), 0, s, key, r, so,
-                           lambdas, st, ws);
+                           lambdas, st, ws, bs);
     else
         hipLaunchKernelGGL((k_batch_select<false, ST, RPT>), dim3(nplots), dim3(ST), 0, s, key, r, so,
-                           lambdas, st, ws);
+                           lambdas, st, ws, bs);
     return hipGetLastError();
 }
 

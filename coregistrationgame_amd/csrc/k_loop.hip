@@ -15,8 +15,7 @@ namespace ficp {
 
 namespace {
 
-__global__ void k_loop_init(IterState *st, LoopCtl c) {
-    if (threadIdx.x != 0) return;
+__device__ void loop_init(IterState *st, const LoopCtl &c) {
     IterState &s = *st;
     for (int e = 0; e < 9; ++e) s.Ttot[e] = (e % 4 == 0) ? 1.0 : 0.0;
     s.cur = INFINITY;
@@ -30,6 +29,10 @@ __global__ void k_loop_init(IterState *st, LoopCtl c) {
     s.phase = c.nstages > 0 ? PH_HEAD : PH_DONE;
     s.lam_cur = c.nstages > 0 ? lam_of(c, 0) : 0.0;
     loop_set_flags(s);
+}
+
+__global__ void k_loop_init(IterState *st, LoopCtl c) {
+    if (threadIdx.x == 0) loop_init(st, c);
 }
 
 __global__ void k_loop_update(IterState *st, LoopCtl c) {
@@ -59,9 +62,12 @@ __global__ __launch_bounds__(256) void k_trace_idx(const IterState *st, const in
 // device each at C3, profiles/r1sel trace).
 // run start: zero the sort's timeout flag and stamp the device clock (100 MHz) into
 // coherent host memory; the report kernel stamps the end (ficp_stats::gpu_ms without
-// event records, each of which left ~5 us of idle queue)
-__global__ void k_run_start(uint32_t *tflag, unsigned long long *t0, unsigned *selerr) {
+// event records, each of which left ~5 us of idle queue); with st, the loop state's
+// initialisation too (one launch less per run)
+__global__ void k_run_start(uint32_t *tflag, unsigned long long *t0, unsigned *selerr,
+                            IterState *st, LoopCtl lc) {
     if (threadIdx.x == 0) {
+        if (st) loop_init(st, lc);
         __hip_atomic_exchange(tflag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the selection's sticky error bits are per run (a failed run leaves no poison)
         if (selerr) __hip_atomic_exchange(selerr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -71,8 +77,10 @@ __global__ void k_run_start(uint32_t *tflag, unsigned long long *t0, unsigned *s
 }
 
 hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s,
-                            unsigned *selerr) {
-    hipLaunchKernelGGL(k_run_start, dim3(1), dim3(64), 0, s, tflag, t0, selerr);
+                            unsigned *selerr, IterState *st, const LoopCtl *lc) {
+    const LoopCtl c = lc ? *lc : LoopCtl{};
+    hipLaunchKernelGGL(k_run_start, dim3(1), dim3(64), 0, s, tflag, t0, selerr, lc ? st : nullptr,
+                       c);
     return hipGetLastError();
 }
 

@@ -37,6 +37,7 @@
 #include "frmsd_bounds.h"
 
 #include <math.h>
+#include <stddef.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -61,9 +62,18 @@ __device__ unsigned long long g_selclk[32];
             g_selclk[i] = clock64();                     \
         }                                                \
     } while (0)
+// the first gather block's own stamps (no barrier: the other blocks are not perturbed)
+#define GPROF(i)                                                        \
+    do {                                                                \
+        if (blk == 0 && threadIdx.x == 0) g_selprof[i] = wall_clock64(); \
+    } while (0)
+__device__ unsigned g_selcalls;
 #else
 #define SELPROF(i) \
     do {           \
+    } while (0)
+#define GPROF(i) \
+    do {         \
     } while (0)
 #endif
 
@@ -115,6 +125,10 @@ struct SelCtl {
     unsigned pad_;
     u64 bpub;              // k_sel_bounds_gather: (launch token << 32) | (b0 << 16) | b1
 };
+// the run's report copies {err, levels, radix} as three words from sel_err_word()
+static_assert(offsetof(SelCtl, levels) == offsetof(SelCtl, err) + 4 &&
+                  offsetof(SelCtl, radix) == offsetof(SelCtl, err) + 8,
+              "SelCtl statistics words must follow err");
 
 struct SelWS {
     unsigned *hcnt;  // [NB] reduced counts (plain stores, k_sel_reduce)
@@ -602,7 +616,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t q = ib + (int64_t)u * HHT;
-        kk[u] = q < i1 ? key[q] : 0ULL;
+        kk[u] = (key && q < i1) ? key[q] : 0ULL;
         rv[u] = q < i1 ? r[q] : 0.0;
     }
     const BPrev pv = bprev_of(st);
@@ -648,14 +662,14 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t q = i + (int64_t)u * HHT;
-                kk[u] = q < i1 ? key[q] : 0ULL;
+                kk[u] = (key && q < i1) ? key[q] : 0ULL;
                 rv[u] = q < i1 ? r[q] : 0.0;
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (i + (int64_t)u * HHT < i1) {
-                const int b = bucket_of(bm, kk[u]);
+                const int b = bucket_of(bm, key ? kk[u] : key_of_r(rv[u]));
                 // r < 2^e for every row of the bucket, from the bucket's upper key bits
                 // (a per-bucket LDS table cost its init and 16 KB: +1 % without it)
                 const int e = bucket_exp(bm, b);
@@ -950,6 +964,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
 __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig, const double *r,
                                             int64_t n, SelWS w, FitSrc fs, int blk,
                                             unsigned gen, const int *skip) {
+    GPROF(26);
     const int sk = skip ? *skip : 0;  // checked after the rows' loads have issued
     __shared__ double s_w[GT / 64];
     __shared__ double s_f[8 * (GT / 64)];
@@ -966,7 +981,7 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
 #pragma unroll
     for (int q = 0; q < GI; ++q) {
         const int64_t i = base + (int64_t)q * GT;
-        kk[q] = i < n ? key[i] : 0ULL;
+        kk[q] = (key && i < n) ? key[i] : 0ULL;
         rr[q] = i < n ? r[i] : 0.0;
     }
     if (fs.on) {
@@ -1014,6 +1029,7 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
         b0 = w.ctl->b0;
         b1 = w.ctl->b1;
     }
+    GPROF(27);
     double acc = 0.0;
     unsigned inm = 0;   // bit q: row q is a candidate
     unsigned bel = 0;   // bit q: row q lies below the candidates (selected)
@@ -1024,6 +1040,7 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
         const int64_t i = base + (int64_t)q * GT;
         bool in = false;
         if (i < n) {
+            if (!key) kk[q] = key_of_r(rr[q]);
             const int b = bucket_of(bm, kk[q]);
             if (b < b0) {
                 acc = acc + rr[q];
@@ -1070,6 +1087,7 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
             pos += (unsigned)__popcll(masks[q]);
         }
     }
+    GPROF(28);
     // fused fit: the 8 sums of the rows below the candidates (all of them are selected)
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (fs.on) {
@@ -1101,6 +1119,7 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
         for (int q = 0; q < GT / 64; ++q) t = t + s_f[8 * q + threadIdx.x];
         w.fparts[8 * blk + threadIdx.x] = t;
     }
+    GPROF(29);
 }
 
 __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_t *orig,
@@ -1416,16 +1435,18 @@ __device__ void final_small(const CandPre &pre, unsigned c, const FinalIn &in, u
         lo[t] = o;
         lr[t] = pre.r;
     }
-    __syncthreads();
+    SELPROF(21);
     if (t < c) {
         unsigned rank = 0;
         for (unsigned j = 0; j < c; ++j) rank += less_ko(lk[j], lo[j], k, o) ? 1u : 0u;
         pos[rank] = (uint16_t)t;
     }
     __syncthreads();
+    SELPROF(22);
     const double v = t < c ? lr[pos[t]] : 0.0;
     double all;
     const double ex = blk_excl_scan_d(v, scr, all);
+    SELPROF(23);
     double bf = INFINITY;
     long long bk = 0x7fffffffffffffffLL;
     if (t < c) {
@@ -1437,6 +1458,7 @@ __device__ void final_small(const CandPre &pre, unsigned c, const FinalIn &in, u
         }
     }
     blk_argmin(bf, bk, scr);
+    SELPROF(24);
     if (in.fs.on && bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
         double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if ((long long)t < bk - in.K0) {
@@ -1445,6 +1467,7 @@ __device__ void final_small(const CandPre &pre, unsigned c, const FinalIn &in, u
         }
         blk_sum8_add(cf, in.fsum, scr);
     }
+    SELPROF(25);
     if (t == 0) {
         u64 tk = 0;
         uint32_t to = 0;
@@ -2002,6 +2025,22 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     if (t == 0 && host_flag)
         __hip_atomic_store(host_flag, s_st.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     SELPROF(6);
+#ifdef SEL_PROF
+    // one line per 13 calls, in 10-ns ticks: bounds phases (block 0 of bounds_gather), the
+    // first gather block (start vs bounds start, wait, append, sums), the final's phases
+    if (t == 0 && (g_selcalls++ % 13u) == 6u) {
+        const unsigned long long *g = g_selprof;
+        printf("SELPROF c=%u bounds %lld %lld %lld %lld %lld %lld | gather +%lld wait %lld app %lld sums %lld"
+               " | gap %lld final pro %lld small %lld %lld %lld %lld %lld post %lld tail %lld\n", c,
+               (long long)(g[9] - g[8]), (long long)(g[10] - g[9]), (long long)(g[11] - g[10]),
+               (long long)(g[12] - g[11]), (long long)(g[13] - g[12]), (long long)(g[14] - g[13]),
+               (long long)(g[26] - g[8]), (long long)(g[27] - g[26]), (long long)(g[28] - g[27]),
+               (long long)(g[29] - g[28]), (long long)(g[0] - g[29]), (long long)(g[1] - g[0]),
+               (long long)(g[21] - g[1]), (long long)(g[22] - g[21]), (long long)(g[23] - g[22]),
+               (long long)(g[24] - g[23]), (long long)(g[25] - g[24]), (long long)(g[5] - g[25]),
+               (long long)(g[6] - g[5]));
+    }
+#endif
 }
 
 __global__ void k_sel_init(SelWS w) {
@@ -2011,14 +2050,6 @@ __global__ void k_sel_init(SelWS w) {
         w.ctl->levels = 0;
         w.ctl->radix = 0;
         __hip_atomic_store(&w.ctl->bpub, (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-__global__ void k_sel_read_stats(SelWS w, unsigned *out) {
-    if (threadIdx.x == 0) {
-        out[0] = __hip_atomic_fetch_or(&w.ctl->err, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        out[1] = w.ctl->levels;
-        out[2] = w.ctl->radix;
     }
 }
 
@@ -2140,11 +2171,6 @@ hipError_t launch_select_dist_final(const long long *packs, int world, int capd,
 
 hipError_t launch_select_init(void *tmp, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(1024), 0, s, carve(tmp, n));
-    return hipGetLastError();
-}
-
-hipError_t launch_select_stats(void *tmp, int64_t n, unsigned *out3, hipStream_t s) {
-    hipLaunchKernelGGL(k_sel_read_stats, dim3(1), dim3(64), 0, s, carve(tmp, n), out3);
     return hipGetLastError();
 }
 

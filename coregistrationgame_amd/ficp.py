@@ -49,8 +49,10 @@ class FractionalICP:
         $FICP_DEVICE, $LOCAL_RANK or 0) and ``nn_mode`` ("auto", "brute", "grid").
         """
         t0 = time.perf_counter()
-        self.source = np.array(source, dtype=float)
-        self.target = np.array(target, dtype=float)
+        # np.array(source, dtype=float) copies (ficp.py:34-35); large layers land in pooled
+        # page-locked blocks (_lib.copy_array): no page faults, unstaged uploads
+        self.source = _lib.copy_array(source)
+        self.target = _lib.copy_array(target)
         self._ctor_ms = 1e3 * (time.perf_counter() - t0)  # host-path accounting (last_stats)
 
         if self.source.ndim != 2 or self.target.ndim != 2:
@@ -170,7 +172,7 @@ class FractionalICP:
         # the run moves a fresh array (ficp.py:114,135 replace self.source; the array the
         # constructor made is never written), columns 0-1 only
         t0 = time.perf_counter()
-        src = np.array(self.source, dtype=np.float64, order="C", copy=True)
+        src = _lib.copy_array(np.ascontiguousarray(self.source, dtype=np.float64))
         t1 = time.perf_counter()
         with self._borrow() as ctx:
             t2 = time.perf_counter()

@@ -233,6 +233,15 @@ int ficp_memcpy_d2h(ficp_ctx *ctx, void *dst, const void *src, int64_t bytes);
 int ficp_memcpy_d2d(ficp_ctx *ctx, void *dst, const void *src, int64_t bytes);
 int ficp_synchronize(ficp_ctx *ctx);
 
+/* --- host memory for the drop-in facade (no context needed) --------------------------
+   Page-locked host memory (hipHostMalloc): the facade keeps its layer copies
+   (ficp.py:34-35 np.array) in pooled blocks of it, so a new instance per Join
+   (app.py:658) neither page-faults fresh memory nor stages its uploads.
+   ficp_host_copy: memcpy split over up to 8 host threads. */
+int ficp_host_alloc(int64_t bytes, void **ptr);
+int ficp_host_free(void *ptr);
+int ficp_host_copy(void *dst, const void *src, int64_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,3 +84,16 @@ def test_stats_struct_layout():
     """ctypes mirror of struct ficp_stats has the C layout (offsets of the trace pointers)."""
     assert ctypes.sizeof(_lib.Stats) == 4 * 4 + 8 + 16 + 72 + 8 + 8 + 5 * 8 + 4 * 8 + 8
     assert _lib.Stats.host_ms.offset == 4 * 4 + 8 + 16 + 72 + 8 + 8 + 5 * 8
+
+
+def test_copy_array_is_np_array_semantics():
+    """_lib.copy_array stands in for ficp.py:34-35's np.array(x, dtype=float): a float64
+    copy for every input kind (pooled pinned memory only where a GPU runtime gives it)."""
+    from coregistrationgame_amd import _lib
+    big = np.random.default_rng(0).random((50_000, 3))  # 1.2 MB: the pooled size class
+    for x in (big, big[:, :2], big.astype(np.float32), [[1, 2], [3, 4]], np.arange(6).reshape(3, 2)):
+        y = _lib.copy_array(x)
+        ref = np.array(x, dtype=float)
+        assert y.dtype == np.float64 and y.shape == ref.shape and np.array_equal(y, ref)
+        if isinstance(x, np.ndarray):
+            assert not np.shares_memory(y, x)

@@ -53,13 +53,15 @@ def test_batch_real_stand10():
             assert b.stats[j]["k_last"] == z[f"{pid}/k"][-1], pid
 
 
-@pytest.mark.parametrize("knobs", [{}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_BATCH_STREAMS": "1"}],
-                         ids=["bsort_grid_2streams", "atomic_grid", "one_stream"])
+@pytest.mark.parametrize("knobs", [{}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_BATCH_STREAMS": "1"},
+                                   {"FICP_BATCH_FUSE": "0"}],
+                         ids=["bsort_grid_2streams", "atomic_grid", "one_stream", "fit_update_launches"])
 def test_batch_vs_oracle_mixed(oracle, knobs, monkeypatch):
     """64 synthetic plots of mixed sizes (incl. 1-tree plots, empty layers, md=2 plots)
     vs the oracle run of each plot alone, with the batch grid built by the bucket sort
     (default) and by the global-atomic fallback, as two sub-batches on two streams (the
-    default at 64-384 plots) and as one.  (A plot whose selection can map onto a single
+    default at 64-384 plots) and as one, with the loop step and the fit inside the
+    selection (default) and as their own launches.  (A plot whose selection can map onto a single
     CHM stem has a zero cross-covariance: its rotation is rounding noise in the reference
     and unpinnable, so the CHM layers here have >= 60 stems.)"""
     from coregistrationgame_amd import FractionalICPBatch, synth

@@ -79,3 +79,32 @@ def test_host_ms_tiles_the_call():
     lib = icp.last_stats["lib_host_ms"]
     assert lib["upload"] + lib["loop"] + lib["result"] <= h["run"] * 1.001 + 0.05
     assert icp.last_stats["gpu_ms"] <= lib["loop"] * 1.001 + 0.05
+
+
+def test_pooled_host_arrays_are_private_copies():
+    """The facade's layer copies live in pooled pinned blocks (_lib.copy_array): each is a
+    private copy (ficp.py:34-35 np.array semantics), a block is not recycled while any view
+    of it is alive, and the run's result is the same as from plain numpy memory."""
+    p = synth.make_plot(60_000, 60_000, 0.7, seed=5, md=3)  # 1.4 MB per layer: pooled
+    src_in = np.array(p.source)
+    icp = FractionalICP(src_in, p.target, device=0)
+    assert _lib.is_pooled(icp.source) and _lib.is_pooled(icp.target)
+    src_in[:, 0] += 1000.0  # the caller's later writes do not reach the instance
+    assert np.array_equal(icp.source, p.source)
+    out = icp.run()
+    assert _lib.is_pooled(out)
+    keep = out[:, :2]  # a view: its block stays out of the pool
+    kept = keep.copy()
+    del icp, out
+    for _ in range(3):  # new instances take other blocks, never the viewed one
+        FractionalICP(p.source, p.target, device=0).run()
+    assert np.array_equal(keep, kept)
+    # same answer as an instance whose layers are plain (small-path threshold aside)
+    ctx = _lib.Context(0, _lib.NN_AUTO)
+    try:
+        ctx.set_target(np.array(p.target), 3)
+        ref = np.array(p.source)
+        ctx.run(ref, [3.0, 0.95], 1e-6, 1000, False)
+    finally:
+        ctx.close()
+    assert np.array_equal(kept, ref[:, :2])

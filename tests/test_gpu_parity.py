@@ -343,7 +343,8 @@ def test_run_vs_oracle_100k(oracle):
 # and the grid density (points per cell: more per cell, more cells per disk scan)
 KNOBS = [{}, {"FICP_FUSE_FIT": "0"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
          {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "0"},
-         {"FICP_GRID_PER_CELL": "4"}, {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_SPLIT": "1", "FICP_FUSE_FIT": "0"}]
+         {"FICP_GRID_PER_CELL": "4"}, {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_SPLIT": "1", "FICP_FUSE_FIT": "0"},
+         {"FICP_NN_KEYS": "1"}]
 
 
 @pytest.mark.parametrize("knobs,md", [(k, 3) for k in KNOBS] + [({}, 2), ({"FICP_GRID_ATOMIC": "1"}, 2)],
@@ -352,7 +353,7 @@ KNOBS = [{}, {"FICP_FUSE_FIT": "0"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADI
 def test_run_untraced_vs_oracle_100k(oracle, knobs, md, monkeypatch):
     """The production loop (no traces: the selection's last kernel runs the loop step; with
     by default it also runs the rigid fit, FICP_FUSE_FIT=0 a separate pass; half-step
-    lookahead, certified NN reuse)
+    lookahead, certified NN reuse; the sort keys derived from r unless FICP_NN_KEYS=1)
     against the pinned oracle at 100k, 3-D and 2-D matching, under every kernel switch."""
     from coregistrationgame_amd import FractionalICP, synth
     for k, v in knobs.items():

@@ -525,7 +525,7 @@ HOST_POOL_MAX_IDLE = int(os.environ.get("FICP_HOST_POOL_MB", "1024")) << 20
 _hpool_lock = threading.Lock()
 _hpool: dict[int, list[int]] = {}
 _hpool_idle = 0
-_hpool_ok: bool | None = None
+_hpool_ok: bool | None = False if os.environ.get("FICP_HOST_POOL", "1") == "0" else None  # 0: numpy memory
 
 
 def _host_block(nbytes: int):

@@ -27,6 +27,23 @@ __device__ __forceinline__ unsigned long long ordkey(double v) {
 // histogram and the gather).
 __device__ __forceinline__ unsigned long long key_of_r(double r) { return ordkey(sqrt(r)); }
 
+// floor(r / 2^L) of an r >= 0 (finite): the fixed-point grid of order-free bucket sums
+// (k_select.hip refine, k_batch.hip k_batch_select)
+__device__ __forceinline__ unsigned long long fx_floor(double r, int L) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(r);
+    const int ex = (int)((b >> 52) & 0x7ff);
+    unsigned long long m = b & 0xfffffffffffffULL;
+    int p2;
+    if (ex == 0) {
+        p2 = -1074;
+    } else {
+        m |= 1ULL << 52;
+        p2 = ex - 1075;
+    }
+    const int sft = p2 - L;
+    return sft >= 0 ? m << sft : (sft > -64 ? m >> (-sft) : 0ULL);
+}
+
 // wave-wide max of two u64 (all 64 lanes must be active)
 __device__ __forceinline__ void wave_range_reduce(unsigned long long &a, unsigned long long &b) {
 #pragma unroll

@@ -562,23 +562,33 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     const u64 kmin = ~amin;
     const int nb = fb::bits_of(kmax - kmin);
     const int sh = nb > SB_LOG ? nb - SB_LOG : 0;
+    // bucket sums of r as integers on the grid 2^Lq (floor per row): the same bits in any
+    // atomic order (a double LDS atomic sum was not; its last bits moved the window and so
+    // the split between S_base and the window's scan).  r < 2^e1 for every finite row
+    // (d <= dmax, d = sqrt(r) rounded), so nfin rows fit in 62 bits; a bucket's true sum
+    // lies in [lo, lo + count) units.
+    const double dmax = __longlong_as_double((long long)(kmax & 0x7fffffffffffffffULL));
+    const int e1 = dmax > 0.0 ? 2 * (ilogb(dmax) + 1) : 0;
+    const int Lq = e1 - (62 - fb::bits_of((u64)nfin));
+    u64 *s_fx = reinterpret_cast<u64 *>(s_sum);
     BSEL_T(1);
     // 2. histogram
 #pragma unroll
     for (int j = 0; j < SPER; ++j) {
         s_cnt[t * SPER + j] = 0u;
-        s_sum[t * SPER + j] = 0.0;
+        s_fx[t * SPER + j] = 0ULL;
     }
     if (t == 0) s_nact = 0;
     __syncthreads();
     SEL_ROWS(if (rv < INFINITY) {
         const int bk = (int)((kk - kmin) >> sh);
         atomicAdd(&s_cnt[bk], 1u);
-        atomicAdd(&s_sum[bk], rv);
+        atomicAdd(&s_fx[bk], fx_floor(rv, Lq));
     })
     __syncthreads();
     BSEL_T(2);
-    // 3. bounds over the buckets (thread t owns buckets t*SPER .. t*SPER + SPER - 1)
+    // 3. bounds over the buckets (thread t owns buckets t*SPER .. t*SPER + SPER - 1): the
+    // lower sums P (prefix of the lo values); the upper sum before a bucket is P + C units
     unsigned c[SPER];
     double sm[SPER];
     unsigned tc = 0;
@@ -586,20 +596,22 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
 #pragma unroll
     for (int j = 0; j < SPER; ++j) {
         c[j] = s_cnt[t * SPER + j];
-        sm[j] = s_sum[t * SPER + j];
+        sm[j] = ldexp((double)s_fx[t * SPER + j], Lq);
         tc += c[j];
         ts = ts + sm[j];
     }
     unsigned Cex = tc;
     double Pex = ts;
     blk_excl_scan2(Cex, Pex, red);
+    const double unit = ldexp(1.0, Lq);
     BSEL_T(8);
     // coarse to fine (as k_select.hip k_sel_bounds): U1 = the bound at each thread's chunk
     // end; a chunk whose lower bound (its rows are all >= its first bucket's lo_r) exceeds
     // U1 holds neither the minimising bucket end nor a candidate bucket, so only the few
     // chunks near the minimum evaluate their buckets (every thread evaluating its 4
     // buckets twice was ~40 % of the workgroup's time: 24 fp64 log2 per thread)
-    double U1 = tc ? fb::h_of((long long)Cex + tc, Pex + ts, pe) + fb::kMarg : INFINITY;
+    double U1 = tc ? fb::h_of((long long)Cex + tc, (Pex + ts) + (double)(Cex + tc) * unit, pe) + fb::kMarg
+                   : INFINITY;
     U1 = blk_min_d(U1, red);
     BSEL_T(9);
     // (the extra 1e-9 covers the different rounding of the chunk's and its buckets' sums)
@@ -639,7 +651,8 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
         // end value and its lower bound in one round of independent log2
         double lb = INFINITY;
         if (cq) {
-            U = fb::h_of(C0 + cq, P0 + s_sum[bk], pe) + fb::kMarg;
+            U = fb::h_of(C0 + cq, (P0 + ldexp((double)s_fx[bk], Lq)) + (double)(C0 + cq) * unit, pe) +
+                fb::kMarg;
             lb = fb::block_lb(C0, cq, P0, fb::lo_r(kmin + ((u64)bk << sh)), pe);
         }
         BSEL_T(10);
@@ -657,7 +670,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
                 if (c[j]) {
                     C += c[j];
                     P = P + sm[j];
-                    U = fmin(U, fb::h_of(C, P, pe) + fb::kMarg);
+                    U = fmin(U, fb::h_of(C, P + (double)C * unit, pe) + fb::kMarg);
                 }
             }
         }

@@ -62,6 +62,22 @@ struct Stems {
     __amdgpu_buffer_rsrc_t r;
 };
 
+// FICP_NN_STATS (diagnostic builds only): per-launch counts of candidate evaluations,
+// certified / scanned queries, printed by a one-thread kernel after each NN launch
+#ifdef FICP_NN_STATS
+__device__ unsigned long long g_nnst[8];
+#define NNST(i)                                                                      \
+    do {                                                                             \
+        const unsigned long long m_ = __ballot(1);                                   \
+        if ((threadIdx.x & 63) == (unsigned)__builtin_ctzll(m_))                    \
+            atomicAdd(&g_nnst[i], (unsigned long long)__popcll(m_));                 \
+    } while (0)
+#else
+#define NNST(i) \
+    do {        \
+    } while (0)
+#endif
+
 __device__ __forceinline__ Stems stems_of(const TPt *pts, int64_t m) {
     Stems st;
     st.r = __builtin_amdgcn_make_buffer_rsrc((void *)pts, 0, (int)(m * (int64_t)sizeof(TPt)),
@@ -80,6 +96,7 @@ struct Best {
 template <int MD>
 __device__ __forceinline__ void eval_slot(const Stems &S, int p, double qx, double qy, double qz,
                                           Best &b) {
+    NNST(1);
     const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32, 0, 0);
     const u32x3 hi = load_zid(S.r, p);
     const double2 xy = __builtin_bit_cast(double2, lo);
@@ -457,6 +474,7 @@ struct Best2 {
 template <int MD>
 __device__ __forceinline__ void eval2(const Stems &S, int p, double qx, double qy, double qz,
                                       Best2 &b) {
+    NNST(0);
     const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(S.r, p * 32, 0, 0);
     const u32x3 hi = load_zid(S.r, p);
     const double2 xy = __builtin_bit_cast(double2, lo);
@@ -595,6 +613,7 @@ __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, con
     mv = sqrt(mx * mx + my * my);
     const double G = a.gap[i] - mv - eps;
     if (!(d2w < INFINITY && sqrt(d2w) + eps < G)) return false;
+    NNST(2);
     a.gap[i] = gap_rd(G);
     if (a.idx) a.idx[i] = (int)load_zid(S.r, a.out_bp[i]).z;
     const double d = sqrt(d2w);
@@ -643,6 +662,7 @@ __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, co
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
     const double eps = cert_eps(g, qx, qy);
     Best2 b{INFINITY, 0x7fffffff, -1, INFINITY};
+    NNST(3);
     if (warm) {
         const double d2w = warm_d2<MD>(a, i, qx, qy);
         if (d2w < INFINITY) b.d2 = d2w;  // a stem's exact d2, its slot unknown (-1)
@@ -699,6 +719,7 @@ __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView 
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
     const double mq = query_margin(g, qx, qy);
     const double rc = sqrt(d2w) + pad;
+    if (lg == 0) NNST(4);
     const double cover2 = rc * rc;
     for (int k = -1;; ++k) {  // rows cy-1, cy, cy+1, then cy -+ 2, 3, ... while in cover
         bool any = false;
@@ -766,6 +787,7 @@ template <int MD>
 __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, const Stems &S,
                                          int64_t i, const double *T, unsigned long long &kmin_c,
                                          unsigned long long &kmax) {
+    NNST(5);
     double qx = a.sx[i], qy = a.sy[i];
     if (T) {
         apply_T(T, qx, qy);
@@ -1335,9 +1357,26 @@ hipError_t launch_grid_sort_cells(TPt *pts, const int32_t *cell_start, int64_t n
     return hipGetLastError();
 }
 
+#ifdef FICP_NN_STATS
+__global__ void k_nn_stats_print(const int *skip, const int *reuse) {
+    if (threadIdx.x != 0) return;
+    if ((skip && *skip) || (reuse && *reuse)) return;
+    printf("NNSTATS eval2 %llu evalslot %llu cert %llu scan %llu group %llu plain %llu\n", g_nnst[0],
+           g_nnst[1], g_nnst[2], g_nnst[3], g_nnst[4], g_nnst[5]);
+    for (int q = 0; q < 8; ++q) g_nnst[q] = 0;
+}
+#endif
+
 hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_t s,
                           bool reduce_range, hipEvent_t e0, hipEvent_t e1) {
     if (a.n == 0) return hipSuccess;
+#ifdef FICP_NN_STATS
+    struct Pr {
+        hipStream_t s;
+        const NNArgs &a;
+        ~Pr() { hipLaunchKernelGGL(k_nn_stats_print, dim3(1), dim3(64), 0, s, a.skip, a.reuse); }
+    } pr_{s, a};
+#endif
     dim3 grid(nblk(a.n)), blk(256);
     if (!e0) {
         // plain dispatch without events

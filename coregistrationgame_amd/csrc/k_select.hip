@@ -1435,6 +1435,7 @@ __device__ void final_small(const CandPre &pre, unsigned c, const FinalIn &in, u
         lo[t] = o;
         lr[t] = pre.r;
     }
+    __syncthreads();
     SELPROF(21);
     if (t < c) {
         unsigned rank = 0;
@@ -1603,10 +1604,60 @@ __device__ bool final_chunked(const Cand &src, const Cand &dst, unsigned c, cons
 
 // (b) one refinement level over c > CAP candidates in global memory: returns false when
 // it cannot shrink the set (the caller then sorts it)
+// v * 2^56 truncated toward zero, two's complement in 128 bits (|v| < 2^70: fit terms of
+// coordinates relative to the pivot, products of two of them)
+__device__ __forceinline__ u128 fx56(double v) {
+    const u64 b = (u64)__double_as_longlong(v);
+    const int ex = (int)((b >> 52) & 0x7ff);
+    if (ex == 0) return (u128)0;  // zero or subnormal: below the grid
+    const u64 m = (b & 0xfffffffffffffULL) | (1ULL << 52);
+    const int sft = ex - 1075 + 56;
+    const u128 a = sft >= 0 ? ((u128)m << sft) : (sft > -64 ? (u128)(m >> (-sft)) : (u128)0);
+    return (b >> 63) ? (u128)0 - a : a;
+}
+
+__device__ __forceinline__ double fx56_to_double(u128 s) {
+    const bool neg = (s >> 127) != 0;
+    const u128 a = neg ? (u128)0 - s : s;
+    const double d = ldexp((double)(u64)(a >> 64), 64 - 56) + ldexp((double)(u64)a, -56);
+    return neg ? -d : d;
+}
+
+// The fused fit's 8 sums of rows taken in an order that is not fixed (the candidate pack
+// is filled by atomics): each term is accumulated exactly on the 2^-56 grid, so the sum
+// is the same bits whatever the order; the block total goes into acc8 as a double.
+__device__ void blk_sum_fx8_add(u128 (&a)[8], double *acc8) {
+    __shared__ u64 s_fx[NWAVE * 8 * 2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const u64 hi = __shfl_xor((u64)(a[e] >> 64), o, 64);
+            const u64 lo = __shfl_xor((u64)a[e], o, 64);
+            a[e] = a[e] + (((u128)hi << 64) | lo);
+        }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            s_fx[(w * 8 + e) * 2] = (u64)(a[e] >> 64);
+            s_fx[(w * 8 + e) * 2 + 1] = (u64)a[e];
+        }
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        u128 t = 0;
+        for (int q = 0; q < NWAVE; ++q)
+            t = t + (((u128)s_fx[(q * 8 + threadIdx.x) * 2] << 64) | s_fx[(q * 8 + threadIdx.x) * 2 + 1]);
+        acc8[threadIdx.x] = acc8[threadIdx.x] + fx56_to_double(t);
+    }
+    __syncthreads();
+}
+
 __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned char *sm,
                        Scr &scr) {
     unsigned *rc = (unsigned *)(sm + R_C);
-    double *rs = (double *)(sm + R_S);
+    u64 *rs = (u64 *)(sm + R_S);
     unsigned *rn = (unsigned *)(sm + R_N);
     const int t = threadIdx.x;
     u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
@@ -1622,7 +1673,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     }
     for (int b = t; b < NS; b += HT) {
         rc[b] = 0u;
-        rs[b] = 0.0;
+        rs[b] = 0ULL;
     }
     if (t == 0) *rn = 0u;
     blk_minmax2_u64(kmn, kmx, omn, omx, scr);
@@ -1632,46 +1683,57 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     const int vb = bits_of(cmp(kmx, (uint32_t)omx));
     if (vb == 0) return false;
     const int sh = vb > NS_LOG ? vb - NS_LOG : 0;
+    // sub-bin sums of r as integers on the grid 2^Lq (floor per row), r < 2^(e+1): the
+    // sums are the same whatever order the atomics run in (a double atomic sum was not,
+    // and its last bits moved the bounds and so the split between the exact integer sum
+    // below and the sorted scan: k flipped on flat FRMSD curves).  [lo, lo + cnt) units
+    // bracket each sub-bin's true sum.
+    const int e = rmax > 0.0 ? ilogb(rmax) : 0;
+    const int Lq = e + 1 - (62 - bits_of((u64)c));
     for (unsigned i = t; i < c; i += HT) {
         const int b = (int)(cmp(src.k[i], src.o[i]) >> sh);
         atomicAdd(&rc[b], 1u);
-        atomicAdd(&rs[b], src.r[i]);
+        atomicAdd(&rs[b], fx_floor(src.r[i], Lq));
     }
     __syncthreads();
     constexpr int PB = NS / HT;  // 4 sub-bins per thread
     unsigned cn[PB];
-    double sv[PB];
+    double slo[PB], shi[PB];
     long long ct = 0;
-    double stt = 0.0;
+    double stl = 0.0, sth = 0.0;
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
         cn[j] = rc[t * PB + j];
-        sv[j] = rs[t * PB + j];
+        const u64 f = rs[t * PB + j];
+        slo[j] = ldexp((double)f, Lq);
+        shi[j] = ldexp((double)(f + cn[j]), Lq);
         ct += cn[j];
-        stt = stt + sv[j];
+        stl = stl + slo[j];
+        sth = sth + shi[j];
     }
     long long ctot;
     double stot;
     const long long Cex = blk_excl_scan_ll(ct, scr, ctot);
-    const double Pex = blk_excl_scan_d(stt, scr, stot);
+    const double Plex = blk_excl_scan_d(stl, scr, stot);
+    const double Phex = blk_excl_scan_d(sth, scr, stot);
     const double p = 2.0 * in.lam + 1.0;
     double U = in.U;
-    {
+    {  // upper bound of h at each sub-bin end: the upper sums
         long long C = in.K0 + Cex;
-        double P = in.S0 + Pex;
+        double P = in.S0 + Phex;
 #pragma unroll
         for (int j = 0; j < PB; ++j)
             if (cn[j]) {
                 C += cn[j];
-                P = P + sv[j];
+                P = P + shi[j];
                 U = fmin(U, h_of(C, P, p) + kMarg);
             }
     }
     U = blk_min_d(U, scr);
     long long bmin = 0x7fffffffLL, bmax = -1, nfirst = 0x7fffffffLL, nlast = -1;
-    {
+    {  // lower bound inside each sub-bin: the lower sums
         long long C = in.K0 + Cex;
-        double P = in.S0 + Pex;
+        double P = in.S0 + Plex;
 #pragma unroll
         for (int j = 0; j < PB; ++j) {
             const int b = t * PB + j;
@@ -1684,7 +1746,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
                     bmax = max(bmax, (long long)b);
                 }
                 C += cn[j];
-                P = P + sv[j];
+                P = P + slo[j];
             }
         }
     }
@@ -1693,12 +1755,12 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     nfirst = blk_min_ll(nfirst, scr);
     nlast = blk_max_ll(nlast, scr);
     if (bmax < 0 || (bmin == nfirst && bmax == nlast)) return false;
-    // rows that drop below the new range: exact integer sum on the grid 2^(e - 96)
-    const int e = rmax > 0.0 ? ilogb(rmax) : 0;
+    // rows that drop below the new range: exact integer sum on the grid 2^(e - 96); their
+    // fused-fit terms exactly on the 2^-56 grid (the pack's order is not fixed)
     const int L = e - 96;
     u128 acc = 0;
     long long below = 0;
-    double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u128 cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (unsigned i = t; i < c; i += HT) {
         const u64 k = src.k[i];
         const uint32_t o = src.o[i];
@@ -1706,7 +1768,14 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
         const int b = (int)(cmp(k, o) >> sh);
         if (b < bmin) {
             below += 1;
-            if (in.fs.on) fit_row(cf, in.fs, src.p[i]);
+            if (in.fs.on) {
+                const uint32_t wr = src.p[i];
+                double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                fit_add(v, in.fs.sx[wr], in.fs.sy[wr], in.fs.cx[wr], in.fs.cy[wr], in.fs.px,
+                        in.fs.py);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) cf[q] = cf[q] + fx56(v[q]);
+            }
             const u64 bitsr = (u64)__double_as_longlong(rv);
             const int ex = (int)((bitsr >> 52) & 0x7ff);
             u64 m = bitsr & 0xfffffffffffffULL;
@@ -1752,7 +1821,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     const long long nbelow = cnt[0];
     const unsigned nc = *rn;
     __syncthreads();
-    if (in.fs.on) blk_sum8_add(cf, in.fsum, scr);
+    if (in.fs.on) blk_sum_fx8_add(cf, in.fsum);
     in.S0 = in.S0 + add;
     in.K0 += nbelow;
     in.U = U;
@@ -1908,6 +1977,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
                                         __HIP_MEMORY_SCOPE_AGENT);
     const unsigned errv = __hip_atomic_fetch_or(&w.ctl->err, 0u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
+    [[maybe_unused]] const unsigned c_in = c;
     const long long kbase = w.ctl->kbase;
     const double Ub = w.ctl->U;
     CandPre pre{};
@@ -2028,10 +2098,14 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 #ifdef SEL_PROF
     // one line per 13 calls, in 10-ns ticks: bounds phases (block 0 of bounds_gather), the
     // first gather block (start vs bounds start, wait, append, sums), the final's phases
-    if (t == 0 && (g_selcalls++ % 13u) == 6u) {
+#ifndef SEL_PROF_EVERY
+#define SEL_PROF_EVERY 13u
+#endif
+    if (t == 0 && (g_selcalls++ % SEL_PROF_EVERY) == 6u % SEL_PROF_EVERY) {
         const unsigned long long *g = g_selprof;
-        printf("SELPROF c=%u bounds %lld %lld %lld %lld %lld %lld | gather +%lld wait %lld app %lld sums %lld"
-               " | gap %lld final pro %lld small %lld %lld %lld %lld %lld post %lld tail %lld\n", c,
+        printf("SELPROF c=%u->%u k=%lld lev=%u radix=%u bounds %lld %lld %lld %lld %lld %lld | gather +%lld wait %lld app %lld sums %lld"
+               " | gap %lld final pro %lld small %lld %lld %lld %lld %lld post %lld tail %lld\n", c_in, c,
+               (long long)s_st.k, w.ctl->levels, w.ctl->radix,
                (long long)(g[9] - g[8]), (long long)(g[10] - g[9]), (long long)(g[11] - g[10]),
                (long long)(g[12] - g[11]), (long long)(g[13] - g[12]), (long long)(g[14] - g[13]),
                (long long)(g[26] - g[8]), (long long)(g[27] - g[26]), (long long)(g[28] - g[27]),

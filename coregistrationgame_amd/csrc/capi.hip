@@ -220,7 +220,7 @@ unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long lo
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
             bool want_keys, int warm = 0, const int *skip = nullptr,
             const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true,
-            const int *reuse = nullptr, bool store_key = true) {
+            const int *reuse = nullptr, bool store_key = true, bool multi = false) {
     NNArgs a{};
     a.sx = sx;
     a.sy = sy;
@@ -230,6 +230,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
     a.skip = skip;
     a.apply_flag = apply_flag;
     a.reuse = reuse;
+    a.multi = multi ? 1 : 0;
     a.idx = want_idx ? c->idx.as<int32_t>() : nullptr;  // the run loop reads idx only for traces
     a.dist = want_keys ? nullptr : c->dist.as<double>();
     a.r = c->r.as<double>();
@@ -558,6 +559,10 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // it from r (key_of_r): the NN stores 8 B per row less.  FICP_NN_KEYS=1: stored keys.
     const char *nk = getenv("FICP_NN_KEYS");
     const bool keys_from_r = fused && fuse_fit && !(nk && atoi(nk) != 0);
+    // the calls from this index on take k_nn_grid_q (mostly certified queries);
+    // FICP_NN_QPT_FROM overrides (a large value: never)
+    const char *qf = getenv("FICP_NN_QPT_FROM");
+    const int64_t nn_multi_from = qf ? atoll(qf) : nn_qpt_from();
     // part A of iteration i: the fit and the NN call; part B: the selection (and, not
     // fused, the loop step and the flag copy)
     auto enq_a = [&](int64_t i) -> int {
@@ -567,7 +572,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         }
         // (a later stage's head reuses the previous call's outputs: dst->nn_reuse)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
-                    false, tidx != nullptr, &dst->nn_reuse, !keys_from_r));
+                    false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from));
         return FICP_OK;
     };
     auto enq_b = [&](int64_t i) -> int {

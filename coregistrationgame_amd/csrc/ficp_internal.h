@@ -44,6 +44,90 @@ __device__ __forceinline__ unsigned long long fx_floor(double r, int L) {
     return sft >= 0 ? m << sft : (sft > -64 ? m >> (-sft) : 0ULL);
 }
 
+// ---- DPP wave reductions (GFX9 data-parallel primitives).  __shfl_xor compiles to
+// ds_bpermute through the LDS crossbar (~60-100 cycles a step, 12 steps for a double
+// butterfly); these take 6 VALU DPP steps.  The tree is fixed (quad, half-row, row, then
+// rows 0+1 / 2+3 and the halves), so the sums are deterministic; the total lands in lane
+// 63 only.  Every lane of the wave must be active.
+namespace dpp {
+constexpr int QP_XOR1 = 0xB1;          // quad_perm [1, 0, 3, 2]
+constexpr int QP_XOR2 = 0x4E;          // quad_perm [2, 3, 0, 1]
+constexpr int ROW_MIRROR = 0x140;      // lane i <- 15 - i within a row of 16
+constexpr int ROW_HALF_MIRROR = 0x141; // lane i <- 7 - i within a half-row of 8
+constexpr int ROW_BCAST15 = 0x142;     // lane 15 of each row -> the next row (row_mask selects)
+constexpr int ROW_BCAST31 = 0x143;     // lane 31 -> rows 2 and 3 (row_mask selects)
+template <int CTRL, int ROWM = 0xf>
+__device__ __forceinline__ double mov_d(double old, double x) {
+    const long long ux = __double_as_longlong(x), uo = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)uo, (int)ux, CTRL, ROWM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uo >> 32), (int)(ux >> 32), CTRL, ROWM, 0xf,
+                                               false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int CTRL, int ROWM = 0xf>
+__device__ __forceinline__ long long mov_ll(long long old, long long x) {
+    const int lo = __builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROWM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(old >> 32), (int)(x >> 32), CTRL, ROWM, 0xf,
+                                               false);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+}  // namespace dpp
+
+// wave sum, valid in lane 63
+__device__ __forceinline__ double wave_sum63(double x) {
+    x = x + dpp::mov_d<dpp::QP_XOR1>(0.0, x);
+    x = x + dpp::mov_d<dpp::QP_XOR2>(0.0, x);
+    x = x + dpp::mov_d<dpp::ROW_HALF_MIRROR>(0.0, x);
+    x = x + dpp::mov_d<dpp::ROW_MIRROR>(0.0, x);
+    x = x + dpp::mov_d<dpp::ROW_BCAST15, 0xA>(0.0, x);
+    x = x + dpp::mov_d<dpp::ROW_BCAST31, 0xC>(0.0, x);
+    return x;
+}
+
+// wave sum of integers, valid in lane 63
+__device__ __forceinline__ unsigned long long wave_sum63_u64(unsigned long long x) {
+    x += (unsigned long long)dpp::mov_ll<dpp::QP_XOR1>(0, (long long)x);
+    x += (unsigned long long)dpp::mov_ll<dpp::QP_XOR2>(0, (long long)x);
+    x += (unsigned long long)dpp::mov_ll<dpp::ROW_HALF_MIRROR>(0, (long long)x);
+    x += (unsigned long long)dpp::mov_ll<dpp::ROW_MIRROR>(0, (long long)x);
+    x += (unsigned long long)dpp::mov_ll<dpp::ROW_BCAST15, 0xA>(0, (long long)x);
+    x += (unsigned long long)dpp::mov_ll<dpp::ROW_BCAST31, 0xC>(0, (long long)x);
+    return x;
+}
+
+// lane 63's value in every lane (a scalar read, no LDS)
+__device__ __forceinline__ double bcast63(double x) {
+    const long long u = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)u, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), 63);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ unsigned long long bcast63_u64(unsigned long long x) {
+    const int lo = __builtin_amdgcn_readlane((int)x, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), 63);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+// wave min / max, valid in lane 63
+__device__ __forceinline__ double wave_min63(double x) {
+    x = fmin(x, dpp::mov_d<dpp::QP_XOR1>(INFINITY, x));
+    x = fmin(x, dpp::mov_d<dpp::QP_XOR2>(INFINITY, x));
+    x = fmin(x, dpp::mov_d<dpp::ROW_HALF_MIRROR>(INFINITY, x));
+    x = fmin(x, dpp::mov_d<dpp::ROW_MIRROR>(INFINITY, x));
+    x = fmin(x, dpp::mov_d<dpp::ROW_BCAST15, 0xA>(INFINITY, x));
+    x = fmin(x, dpp::mov_d<dpp::ROW_BCAST31, 0xC>(INFINITY, x));
+    return x;
+}
+__device__ __forceinline__ double wave_max63(double x) {
+    x = fmax(x, dpp::mov_d<dpp::QP_XOR1>(-INFINITY, x));
+    x = fmax(x, dpp::mov_d<dpp::QP_XOR2>(-INFINITY, x));
+    x = fmax(x, dpp::mov_d<dpp::ROW_HALF_MIRROR>(-INFINITY, x));
+    x = fmax(x, dpp::mov_d<dpp::ROW_MIRROR>(-INFINITY, x));
+    x = fmax(x, dpp::mov_d<dpp::ROW_BCAST15, 0xA>(-INFINITY, x));
+    x = fmax(x, dpp::mov_d<dpp::ROW_BCAST31, 0xC>(-INFINITY, x));
+    return x;
+}
+
 // wave-wide max of two u64 (all 64 lanes must be active)
 __device__ __forceinline__ void wave_range_reduce(unsigned long long &a, unsigned long long &b) {
 #pragma unroll
@@ -160,6 +244,8 @@ struct NNArgs {
     int cert_block;             // grid kernels, with gap and warm_c: > 0 packs each workgroup's
                                 // uncertified queries onto its first lanes, up to this many
                                 // lanes per query (1, 4 or 8) when they are few
+    int multi;                  // grid kernel, certified calls: QPT queries per thread
+                                // (k_nn_grid_q; the run loop's later calls)
     int warm_c;                 // grid kernels: start from the previous match held in
                                 // (cx, cy, dz2): its d^2 to the moved query, no record reload
     const int *apply_flag;      // T is applied only while *apply_flag != 0 (nullable: always)
@@ -454,6 +540,8 @@ hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_
                           bool reduce_range = true, hipEvent_t ev_start = nullptr,
                           hipEvent_t ev_stop = nullptr);
 int64_t nn_range_parts(int64_t n, int64_t m, bool grid);
+// first NN call index of a run that takes k_nn_grid_q (k_grid_nn.hip FICP_NN_QPT_FROM)
+int nn_qpt_from();
 int64_t brute_chunk_count(int64_t n, int64_t m);  // target chunks of the brute kernel
 hipError_t launch_nn_brute(const NNArgs &a, const double *tx, const double *ty,
                            const double *tz, int64_t m, int md, double *part_d2,

@@ -815,9 +815,10 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
     finish(a, S, i, qz, b, kmin_c, kmax);
 }
 
-// 7 waves per SIMD: without the hint the kernel's 106 SGPRs allow 6 (MI355X_MICROARCH.md
-// residency rule); with it the compiler keeps 94 (40 spilled to VGPR lanes, 71 VGPRs):
-// NN 43.4 -> 42.3 us per C3 call.  8 spills VGPRs to scratch (44 us).
+// Waves per SIMD.  k_nn_grid (one query per thread): 7 kept 71 VGPRs and 94 SGPRs (40
+// spilled to VGPR lanes): NN 43.4 -> 42.3 us per C3 call; 8 spilled VGPRs to scratch.
+// k_nn_grid_q (QPT = 4 queries per thread; the certified step holds 4 queries' inputs):
+// 7 spills 49 VGPRs to scratch, 6 spills 4, 5 none (87 VGPRs).
 #ifndef FICP_NN_WPE
 #define FICP_NN_WPE 7
 #endif
@@ -826,6 +827,187 @@ __device__ __forceinline__ void nn_query(const NNArgs &a, const GridView &g, con
 #else
 #define NN_WPE
 #endif
+#ifndef FICP_NNQ_WPE
+#define FICP_NNQ_WPE 5
+#endif
+#define NNQ_WPE __attribute__((amdgpu_waves_per_eu(FICP_NNQ_WPE, FICP_NNQ_WPE)))
+// Queries per thread of k_nn_grid: a workgroup takes 256 * QPT consecutive queries (in
+// the work order), thread t queries t, t + 256, ...  The certified calls (most of a run)
+// are a short load-test-store per query whose time was latency: 1 query per thread left
+// ~22 us per 1M-query call with >99.5 % certified; QPT queries' loads issue together.
+#ifndef FICP_NN_QPT
+#define FICP_NN_QPT 4
+#endif
+constexpr int QPT = FICP_NN_QPT;
+// the first calls of a run scan most queries (cold start, then every query's first cover
+// scan): those run one query per thread at 7 waves per SIMD (k_nn_grid); the later calls,
+// mostly certified, take QPT queries per thread at 5 waves (k_nn_grid_q) -- per call at
+// C3 the QPT form was 2-7 us faster from the 5th call on and 3-23 us slower before it
+#ifndef FICP_NN_QPT_FROM
+#define FICP_NN_QPT_FROM 4
+#endif
+
+// Step 1 of the certified path for the QPT queries of this thread: every input loaded
+// first (no store between them, so the loads issue back to back), then apply T, try the
+// certificate, store.  pend bit q: query q needs the scan (its moved XY stored), mv[q] its
+// move.
+template <int MD, int Q>
+__device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView &g, const Stems &S,
+                                                 int64_t i0, const double *T,
+                                                 unsigned long long &kmin_c,
+                                                 unsigned long long &kmax, double (&mv)[Q]) {
+    double ox[Q], oy[Q], wx[Q], wy[Q], wz[Q];
+    float gp[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int64_t i = i0 + (int64_t)q * 256;
+        const bool v = i < a.n;
+        ox[q] = v ? a.sx[i] : 0.0;
+        oy[q] = v ? a.sy[i] : 0.0;
+        wx[q] = v ? a.cx[i] : 0.0;
+        wy[q] = v ? a.cy[i] : 0.0;
+        wz[q] = (v && MD == 3) ? a.dz2[i] : 0.0;
+        gp[q] = v ? a.gap[i] : 0.0f;
+    }
+    unsigned pend = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int64_t i = i0 + (int64_t)q * 256;
+        mv[q] = 0.0;
+        if (i >= a.n) continue;
+        double qx = ox[q], qy = oy[q];
+        if (T) {
+            apply_T(T, qx, qy);
+            a.sx[i] = qx;
+            a.sy[i] = qy;
+        }
+        const double eps = cert_eps(g, qx, qy);
+        // the stored match's exact d2 at the moved query (eval_slot's operations)
+        const double dx = qx - wx[q], dy = qy - wy[q];
+        double d2w = dx * dx;
+        d2w = d2w + dy * dy;
+        if (MD == 3) d2w = d2w + wz[q];
+        const double mx = qx - ox[q], my = qy - oy[q];
+        mv[q] = sqrt(mx * mx + my * my);
+        const double G = (double)gp[q] - mv[q] - eps;
+        if (!(d2w < INFINITY && sqrt(d2w) + eps < G)) {
+            pend |= 1u << q;
+            continue;
+        }
+        NNST(2);
+        a.gap[i] = gap_rd(G);
+        if (a.idx) a.idx[i] = (int)load_zid(S.r, a.out_bp[i]).z;
+        const double d = sqrt(d2w);
+        const unsigned long long k = ordkey(d);
+        if (a.dist) a.dist[i] = d;
+        if (a.r) a.r[i] = d2w;
+        if (a.key) a.key[i] = k;
+        if (a.val) a.val[i] = (uint32_t)i;
+        kmin_c = max(kmin_c, ~k);
+        kmax = max(kmax, k);
+    }
+    return pend;
+}
+
+template <int MD, bool APPLY, int Q>
+__device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g) {
+    // the three flags load together (the apply flag's load used to wait for the other two)
+    const int sk = a.skip ? *a.skip : 0, ru = a.reuse ? *a.reuse : 0;
+    const int ap = (APPLY && a.apply_flag) ? *a.apply_flag : 1;
+    if (sk || ru) return;
+    const int t = threadIdx.x;
+    const int64_t i0 = xcd_block(blockIdx.x, gridDim.x) * (256 * Q);
+    unsigned long long kmin_c = 0, kmax = 0;
+    const double *T = (APPLY && ap) ? a.T : nullptr;
+    if (a.cert_block && a.gap && a.warm_c) {
+        // block-compacted: certificates first, then the workgroup's uncertified queries
+        // packed densely onto its lanes (GS lanes per query when there are few of them)
+        __shared__ int s_list[256 * Q];
+        __shared__ double s_mv[256 * Q];
+        __shared__ int s_n;
+        if (t == 0) s_n = 0;
+        __syncthreads();
+        const Stems S = stems_of(g.pts, g.m);
+        double mv[Q];
+        const unsigned pend = cert_try_qpt<MD, Q>(a, g, S, i0 + t, T, kmin_c, kmax, mv);
+        const int lane = t & 63;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const bool pq = (pend >> q) & 1u;
+            const unsigned long long m = __ballot(pq);
+            int base = 0;
+            if (lane == 0 && m) base = atomicAdd(&s_n, __popcll(m));
+            base = __shfl(base, 0);
+            if (pq) {
+                const int e = base + __popcll(m & ((1ULL << lane) - 1));
+                s_list[e] = q * 256 + t;
+                s_mv[e] = mv[q];
+            }
+        }
+        __syncthreads();
+        const int tot = s_n;
+        if (a.cert_block >= 16 && tot <= 16) {
+            if (t < tot * 16) cert_scan_group<MD, 16>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
+        } else if (a.cert_block >= 8 && tot <= 32) {
+            if (t < tot * 8) cert_scan_group<MD, 8>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
+        } else if (a.cert_block >= 4 && tot <= 64) {
+            if (t < tot * 4) cert_scan_group<MD, 4>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
+        } else if (a.cert_block >= 2 && tot <= 128) {
+            if (t < tot * 2) cert_scan_group<MD, 2>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
+        } else if constexpr (Q == 1) {
+            if (t < tot) cert_scan<MD>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
+        } else {
+            for (int e = t; e < tot; e += 256)
+                cert_scan<MD>(a, g, S, i0 + s_list[e], true, cert_pad(g, s_mv[e]), kmin_c, kmax);
+        }
+    } else {
+        const Stems S = stems_of(g.pts, g.m);
+        for (int q = 0; q < Q; ++q) {
+            const int64_t i = i0 + (int64_t)q * 256 + t;
+            if (i >= a.n) break;
+            if (a.gap && !a.warm_c) {
+                // the cold call: the plain scan (no cover) and no certificate for the next
+                // call, which scans every query with its cover.  A cold scan with the cover
+                // cost more than that first warm call saved (C3: +1.8 % without it)
+                nn_query<MD>(a, g, S, i, T, kmin_c, kmax);
+                a.gap[i] = 0;
+            } else if (a.gap) {
+                nn_query_cert<MD>(a, g, S, i, T, kmin_c, kmax);
+            } else {
+                nn_query<MD>(a, g, S, i, T, kmin_c, kmax);
+            }
+        }
+    }
+    if (a.range) {
+        if constexpr (Q == 1) {
+            block_range_store(a.range, true, kmin_c, kmax);
+        } else {
+            // the parts keep the one-query-per-thread layout (nblk(n) of them, whichever
+            // kernel ran): this workgroup's range in part Q b, neutral (0, 0) in the next
+            // Q - 1, so the selection reads no stale part
+            __shared__ unsigned long long s_ra[4], s_rb[4];
+            unsigned long long ra = kmin_c, rb = kmax;
+            wave_range_reduce(ra, rb);
+            if ((t & 63) == 0) {
+                s_ra[t >> 6] = ra;
+                s_rb[t >> 6] = rb;
+            }
+            __syncthreads();
+            const int64_t np = (a.n + 255) / 256, p0 = (int64_t)blockIdx.x * Q;
+            if (t < Q && p0 + t < np) {
+                unsigned long long x = 0, y = 0;
+                if (t == 0)
+                    for (int w = 0; w < 4; ++w) {
+                        x = s_ra[w] > x ? s_ra[w] : x;
+                        y = s_rb[w] > y ? s_rb[w] : y;
+                    }
+                a.range[2 + 2 * (p0 + t)] = x;
+                a.range[3 + 2 * (p0 + t)] = y;
+            }
+        }
+    }
+}
+
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
     // the three flags load together (the apply flag's load used to wait for the other two)
@@ -885,6 +1067,11 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
         }
     }
     if (a.range) block_range_store(a.range, true, kmin_c, kmax);
+}
+
+template <int MD, bool APPLY>
+__global__ __launch_bounds__(256) NNQ_WPE void k_nn_grid_q(NNArgs a, GridView g) {
+    nn_grid_body<MD, APPLY, QPT>(a, g);
 }
 
 // Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against
@@ -1377,23 +1564,15 @@ hipError_t launch_nn_grid(const NNArgs &a, const GridView &g, int md, hipStream_
         ~Pr() { hipLaunchKernelGGL(k_nn_stats_print, dim3(1), dim3(64), 0, s, a.skip, a.reuse); }
     } pr_{s, a};
 #endif
-    dim3 grid(nblk(a.n)), blk(256);
-    if (!e0) {
-        // plain dispatch without events
-        if (md == 3) {
-            if (a.T) hipLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, a, g);
-            else hipLaunchKernelGGL((k_nn_grid<3, false>), grid, blk, 0, s, a, g);
-        } else {
-            if (a.T) hipLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, a, g);
-            else hipLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, a, g);
-        }
-    } else if (md == 3) {
-        if (a.T) hipExtLaunchKernelGGL((k_nn_grid<3, true>), grid, blk, 0, s, e0, e1, 0, a, g);
-        else hipExtLaunchKernelGGL((k_nn_grid<3, false>), grid, blk, 0, s, e0, e1, 0, a, g);
-    } else {
-        if (a.T) hipExtLaunchKernelGGL((k_nn_grid<2, true>), grid, blk, 0, s, e0, e1, 0, a, g);
-        else hipExtLaunchKernelGGL((k_nn_grid<2, false>), grid, blk, 0, s, e0, e1, 0, a, g);
-    }
+    const bool q = a.multi && a.cert_block && a.gap && a.warm_c;
+    dim3 grid(q ? nblk(a.n, 256 * QPT) : nblk(a.n)), blk(256);
+    void (*kf)(NNArgs, GridView);
+    if (md == 3) kf = q ? (a.T ? k_nn_grid_q<3, true> : k_nn_grid_q<3, false>)
+                        : (a.T ? k_nn_grid<3, true> : k_nn_grid<3, false>);
+    else kf = q ? (a.T ? k_nn_grid_q<2, true> : k_nn_grid_q<2, false>)
+                : (a.T ? k_nn_grid<2, true> : k_nn_grid<2, false>);
+    if (!e0) hipLaunchKernelGGL(kf, grid, blk, 0, s, a, g);  // plain dispatch without events
+    else hipExtLaunchKernelGGL(kf, grid, blk, 0, s, e0, e1, 0, a, g);
     if (a.range && reduce_range) return launch_range_reduce(a.range, grid.x, s);
     return hipGetLastError();
 }
@@ -1434,6 +1613,8 @@ int64_t nn_range_parts(int64_t n, int64_t m, bool grid) {
     if (grid || brute_chunk_count(n, m) > 1) return (int64_t)nblk(n);
     return (n + 511) / 512;
 }
+
+int nn_qpt_from() { return FICP_NN_QPT_FROM; }
 
 // target chunks for the brute kernel: enough workgroups to fill 256 CUs
 int64_t brute_chunk_count(int64_t n, int64_t m) {

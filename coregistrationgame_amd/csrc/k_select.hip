@@ -39,6 +39,7 @@
 #include <math.h>
 #include <stddef.h>
 #include <stdlib.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -89,6 +90,7 @@ constexpr int NSB_LOG = 11;
 constexpr int NS = 4096;     // sub-bins of one refinement level
 constexpr int NS_LOG = 12;
 constexpr int MAXLEV = 4;
+constexpr int SMALL_C = 160;  // final_small: above it the binned sort ranks faster (390: 5.8 vs 3.4 us)
 #ifndef FICP_GT
 #define FICP_GT 512
 #endif
@@ -145,6 +147,13 @@ struct SelWS {
     uint32_t *oa, *ob;
     double *ra, *rb;
     uint32_t *pa, *pb;  // candidate row (work position): the fused fit reads its pair
+    // k_sel_reduce_bounds (the bounds spread over the reduce workgroups):
+    u64 *rbp;        // [RBLK * 5] each workgroup's bucket totals (count, lo, hi), tokened
+    double *lbv;     // [NB] lower bound of h inside each bucket (+inf: empty)
+    long long *cbef; // [NB] rows in the buckets before it
+    double *ublk;    // [RBLK] upper bound of min h from each workgroup's bucket ends
+    double *mlb;     // [RBLK] smallest lbv of each workgroup's buckets
+    double *fpre;    // [SMALL_C][4] fused fit: the pair of pack slots < SMALL_C (gather)
 };
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
@@ -209,6 +218,12 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.ob = (uint32_t *)take(nn * 4);
     x.pa = (uint32_t *)take(nn * 4);
     x.pb = (uint32_t *)take(nn * 4);
+    x.rbp = (u64 *)take((NB / 64) * 5 * 8);
+    x.lbv = (double *)take(NB * 8);
+    x.cbef = (long long *)take(NB * 8);
+    x.ublk = (double *)take((NB / 64) * 8);
+    x.mlb = (double *)take((NB / 64) * 8);
+    x.fpre = (double *)take(SMALL_C * 32);
     if (w) *w = x;
     return (int64_t)(p - p0) + 256;
 }
@@ -341,9 +356,8 @@ struct Scr {
 // deterministic: butterfly inside the wave (every lane ends with the same bits), wave
 // partials in wave order
 __device__ __forceinline__ double blk_sum(double x, Scr &s) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = x + __shfl_xor(x, o, 64);
-    if ((threadIdx.x & 63) == 0) s.d[threadIdx.x >> 6] = x;
+    x = wave_sum63(x);
+    if ((threadIdx.x & 63) == 63) s.d[threadIdx.x >> 6] = x;
     __syncthreads();
     double t = 0.0;
 #pragma unroll
@@ -355,10 +369,8 @@ __device__ __forceinline__ double blk_sum(double x, Scr &s) {
 // acc8[e] += block sum of c[e] (thread 0 adds; fixed tree: wave butterfly, waves in order)
 __device__ __forceinline__ void blk_sum8_add(double (&c)[8], double *acc8, Scr &s) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c[e] = c[e] + __shfl_xor(c[e], o, 64);
-    if ((threadIdx.x & 63) == 0)
+    for (int e = 0; e < 8; ++e) c[e] = wave_sum63(c[e]);
+    if ((threadIdx.x & 63) == 63)
 #pragma unroll
         for (int e = 0; e < 8; ++e) s.f[8 * (threadIdx.x >> 6) + e] = c[e];
     __syncthreads();
@@ -379,9 +391,8 @@ __device__ __forceinline__ void fit_row(double (&c)[8], const FitSrc &fs, uint32
 }
 
 __device__ __forceinline__ double blk_min_d(double x, Scr &s) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, 64));
-    if ((threadIdx.x & 63) == 0) s.d[threadIdx.x >> 6] = x;
+    x = wave_min63(x);
+    if ((threadIdx.x & 63) == 63) s.d[threadIdx.x >> 6] = x;
     __syncthreads();
     double t = s.d[0];
 #pragma unroll
@@ -391,9 +402,8 @@ __device__ __forceinline__ double blk_min_d(double x, Scr &s) {
 }
 
 __device__ __forceinline__ double blk_max_d(double x, Scr &s) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
-    if ((threadIdx.x & 63) == 0) s.d[threadIdx.x >> 6] = x;
+    x = wave_max63(x);
+    if ((threadIdx.x & 63) == 63) s.d[threadIdx.x >> 6] = x;
     __syncthreads();
     double t = s.d[0];
 #pragma unroll
@@ -567,16 +577,24 @@ __device__ __forceinline__ void blk_excl_scan3(long long &c, double &a, double &
 
 // block argmin of (f, k) with the first-minimum rule; result broadcast
 __device__ __forceinline__ void blk_argmin(double &f, long long &k, Scr &s) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double xf = __shfl_xor(f, o, 64);
-        const long long xk = __shfl_xor(k, o, 64);
-        if (better(xf, xk, f, k)) {
-            f = xf;
-            k = xk;
-        }
+    // DPP steps (fixed tree); a lane a step does not write keeps (inf, max): never better
+#define ARGMIN_STEP(CTRL, ROWM)                                                      \
+    {                                                                                \
+        const double xf = dpp::mov_d<CTRL, ROWM>(INFINITY, f);                       \
+        const long long xk = dpp::mov_ll<CTRL, ROWM>(0x7fffffffffffffffLL, k);       \
+        if (better(xf, xk, f, k)) {                                                  \
+            f = xf;                                                                  \
+            k = xk;                                                                  \
+        }                                                                            \
     }
-    if ((threadIdx.x & 63) == 0) {
+    ARGMIN_STEP(dpp::QP_XOR1, 0xf)
+    ARGMIN_STEP(dpp::QP_XOR2, 0xf)
+    ARGMIN_STEP(dpp::ROW_HALF_MIRROR, 0xf)
+    ARGMIN_STEP(dpp::ROW_MIRROR, 0xf)
+    ARGMIN_STEP(dpp::ROW_BCAST15, 0xA)
+    ARGMIN_STEP(dpp::ROW_BCAST31, 0xC)
+#undef ARGMIN_STEP
+    if ((threadIdx.x & 63) == 63) {
         s.d[threadIdx.x >> 6] = f;
         s.l[threadIdx.x >> 6] = k;
     }
@@ -777,6 +795,209 @@ __device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsig
     }
 }
 
+// k_sel_reduce + the bounds in one launch, spread over its NB / 64 workgroups (round 3:
+// the one-workgroup bounds took ~12 us at C3, and every gather block waited for them).
+// Workgroup j reduces buckets [64 j, 64 j + 64) (as k_sel_reduce), then its first wave:
+//  (1) scans its 64 buckets (count, lower and upper sum) and publishes the totals as five
+//      tokened 8-B granules (token in the high half: each granule is stored and seen whole,
+//      no fence; MI355X_MICROARCH.md hand-off table);
+//  (2) waits for the totals of workgroups 0..j-1 (dispatched before it: bounded spin, then
+//      ERR_SPIN), sums them in a fixed order: the rows and sums before its buckets;
+//  (3) evaluates every bucket: h at its end (an upper bound of the minimum) and the lower
+//      bound of h inside it, both exactly as the one-workgroup bounds did for the buckets
+//      it evaluated; stores them with the rows before each bucket.
+// The gather then takes U = min over workgroups and [b0, b1] = the buckets whose lower
+// bound is <= U (pre_bounds): the same test as bounds_body, over every bucket.
+constexpr int RBLK = NB / RBPB;  // workgroups of the reduce
+__device__ __forceinline__ u64 tok_pack(unsigned gen, uint32_t v) { return ((u64)gen << 32) | v; }
+
+__global__ __launch_bounds__(1024) void k_sel_reduce_bounds(SelWS w, int nhb, const int *skip,
+                                                            HistPack hp, double lam,
+                                                            const double *lam_dev, unsigned gen,
+                                                            unsigned pub_gen) {
+    const int sk = skip ? *skip : 0;
+    const double lamv = lam_dev ? *lam_dev : lam;
+    __shared__ unsigned s_c[RG][RBPB];
+    __shared__ u64 s_f[RG][RBPB];
+    const int bl = threadIdx.x % RBPB, g = threadIdx.x / RBPB;
+    const int bid = blockIdx.x;
+    const int b = bid * RBPB + bl;
+    const u64 mask = (1ULL << hp.shift) - 1ULL;
+    const int per = (nhb + RG - 1) / RG, q0 = g * per, q1 = min(nhb, q0 + per);
+    unsigned c = 0;
+    u64 f = 0;
+    int q = q0;
+    for (; q + 8 <= q1; q += 8) {
+        u64 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = w.ppk[(int64_t)(q + u) * NB + b];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            c += (unsigned)(v[u] >> hp.shift);
+            f += v[u] & mask;
+        }
+    }
+    for (; q < q1; ++q) {
+        const u64 v = w.ppk[(int64_t)q * NB + b];
+        c += (unsigned)(v >> hp.shift);
+        f += v & mask;
+    }
+    if (sk) return;
+    s_c[g][bl] = c;
+    s_f[g][bl] = f;
+    __syncthreads();
+    if (g != 0) return;
+#pragma unroll
+    for (int h = 1; h < RG; ++h) {
+        c += s_c[h][bl];
+        f += s_f[h][bl];
+    }
+    const BMap bm = w.ctl->map;
+    const int e = bucket_exp(bm, b);
+    double lo, hi;
+    if (e >= 1024) {
+        lo = hi = c ? INFINITY : 0.0;
+    } else {
+        lo = ldexp((double)f, e - hp.fixb);
+        hi = ldexp((double)(f + c), e - hp.fixb);
+    }
+    // (1) inclusive scans over the 64 buckets in bucket order (a fixed pattern)
+    u64 ic = c;
+    double il = lo, ih = hi;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const u64 xc = __shfl_up(ic, o, 64);
+        const double xl = __shfl_up(il, o, 64), xh = __shfl_up(ih, o, 64);
+        if (bl >= o) {
+            ic += xc;
+            il = xl + il;
+            ih = xh + ih;
+        }
+    }
+    const u64 tc = __shfl(ic, 63, 64);
+    const double tl = __shfl(il, 63, 64), th = __shfl(ih, 63, 64);
+    if (bl == 0) {
+        const u64 ul = (u64)__double_as_longlong(tl), uh = (u64)__double_as_longlong(th);
+        u64 *pb = w.rbp + (int64_t)bid * 5;
+        __hip_atomic_store(pb + 0, tok_pack(pub_gen, (uint32_t)tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pb + 1, tok_pack(pub_gen, (uint32_t)(ul >> 32)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pb + 2, tok_pack(pub_gen, (uint32_t)ul), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pb + 3, tok_pack(pub_gen, (uint32_t)(uh >> 32)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pb + 4, tok_pack(pub_gen, (uint32_t)uh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (bid == 0) __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // (2) the totals of workgroups 0..bid-1: lane l takes workgroups l and l + 64
+    u64 pc = 0;
+    double pl = 0.0, ph = 0.0;
+    bool late = false;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = bl + 64 * h;
+        if (j >= bid) continue;
+        const u64 *pb = w.rbp + (int64_t)j * 5;
+        u64 v[5];
+        unsigned it = 0;
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                v[k] = __hip_atomic_load(pb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = ok && (unsigned)(v[k] >> 32) == gen;
+            }
+            if (ok) break;
+            if (++it == (1u << 20)) {  // >= ~30 ms: the run fails with ERR_SPIN, no hang
+                __hip_atomic_fetch_or(&w.ctl->err, ERR_SPIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                late = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (late) break;
+        pc += (uint32_t)v[0];
+        pl = pl + __longlong_as_double((long long)((v[1] << 32) | (v[2] & 0xffffffffULL)));
+        ph = ph + __longlong_as_double((long long)((v[3] << 32) | (v[4] & 0xffffffffULL)));
+    }
+    pc = bcast63_u64(wave_sum63_u64(pc));
+    pl = bcast63(wave_sum63(pl));
+    ph = bcast63(wave_sum63(ph));
+    // (3) this bucket: rows and lower sum before it, upper sum through it
+    const u64 xc = __shfl_up(ic, 1, 64);
+    const double xl = __shfl_up(il, 1, 64);
+    const long long cb = (long long)(pc + (bl ? xc : 0ULL));
+    const double plo = pl + (bl ? xl : 0.0);
+    const double phi = ph + ih;
+    const double p = 2.0 * lamv + 1.0;
+    double hend = INFINITY, lb = INFINITY;
+    if (c) {
+        hend = h_of(cb + (long long)c, phi, p) + kMarg;
+        lb = (p >= 1.0) ? block_lb(cb, c, plo, lo_r(bucket_lo(bm, b)), p) : -INFINITY;
+    }
+    w.lbv[b] = lb;
+    w.cbef[b] = cb;
+    const double um = wave_min63(hend), lm = wave_min63(lb);
+    if (bl == 63) {
+        w.ublk[bid] = um;
+        w.mlb[bid] = lm;
+    }
+}
+
+// [b0, b1] and U from k_sel_reduce_bounds' per-bucket bounds (every gather block, GT
+// threads; a launch boundary after the reduce): U = min of the workgroups' upper bounds,
+// b0 / b1 = the first / last bucket whose lower bound is <= U (buckets of other
+// workgroups are skipped through their smallest lower bound).  Block 0 also stores b0,
+// b1, U and the rows below b0 for the final kernel.
+__device__ __forceinline__ void pre_bounds(const SelWS &w, int blk, int &b0, int &b1) {
+    static_assert(RBLK == 128 && GT >= 128, "two waves hold the reduce workgroups");
+    __shared__ double s_u[2];
+    __shared__ int s_j[4];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    double ub = INFINITY, mb = INFINITY;
+    if (t < RBLK) {
+        ub = w.ublk[t];
+        mb = w.mlb[t];
+    }
+    const double um = wave_min63(ub);
+    if (wv < 2 && lane == 63) s_u[wv] = um;
+    __syncthreads();
+    const double U = fmin(s_u[0], s_u[1]);
+    if (wv < 2) {
+        const u64 m = __ballot(t < RBLK && !(mb > U));
+        if (lane == 0) {
+            s_j[wv] = m ? wv * 64 + __builtin_ctzll(m) : 0x7fffffff;
+            s_j[2 + wv] = m ? wv * 64 + 63 - __builtin_clzll(m) : -1;
+        }
+    }
+    __syncthreads();
+    const int j0 = min(s_j[0], s_j[1]), j1 = max(s_j[2], s_j[3]);
+    if (j1 < 0) {  // no bucket qualifies (non-finite r): every row is a candidate
+        b0 = 0;
+        b1 = NB - 1;
+        if (blk == 0 && t == 0) {
+            w.ctl->b0 = b0;
+            w.ctl->b1 = b1;
+            w.ctl->U = U;
+            w.ctl->kbase = 0;
+        }
+        return;
+    }
+    __syncthreads();  // s_j is rewritten below
+    if (wv < 2) {
+        const int j = wv ? j1 : j0;
+        const double l = w.lbv[j * 64 + lane];
+        const u64 m = __ballot(!(l > U));
+        if (lane == 0) s_j[wv] = wv ? j * 64 + 63 - __builtin_clzll(m) : j * 64 + __builtin_ctzll(m);
+    }
+    __syncthreads();
+    b0 = s_j[0];
+    b1 = s_j[1];
+    if (blk == 0 && t == 0) {
+        w.ctl->b0 = b0;
+        w.ctl->b1 = b1;
+        w.ctl->U = U;
+        w.ctl->kbase = w.cbef[b0];
+    }
+}
+
 // Bounds of the FRMSD curve over the level-0 buckets (one workgroup).  Per-thread
 // chunks of PER consecutive buckets; the per-bucket work (two or four log2 each) runs
 // only for the chunks that can hold the minimum, one bucket per lane (a chunk walked by
@@ -963,7 +1184,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
 // published in ctl->bpub with the token gen; the rows' loads are issued before the wait
 __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig, const double *r,
                                             int64_t n, SelWS w, FitSrc fs, int blk,
-                                            unsigned gen, const int *skip) {
+                                            unsigned gen, const int *skip, bool pre = false) {
     GPROF(26);
     const int sk = skip ? *skip : 0;  // checked after the rows' loads have issued
     __shared__ double s_w[GT / 64];
@@ -1025,6 +1246,8 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
         __syncthreads();
         b0 = s_b[0];
         b1 = s_b[1];
+    } else if (pre) {
+        pre_bounds(w, blk, b0, b1);
     } else {
         b0 = w.ctl->b0;
         b1 = w.ctl->b1;
@@ -1083,6 +1306,12 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
                 w.oa[p] = orig ? orig[i] : (uint32_t)i;
                 w.ra[p] = rr[q];
                 w.pa[p] = (uint32_t)i;
+                if (fs.on && p < (unsigned)SMALL_C) {  // final_small's pairs, no row lookup
+                    w.fpre[4 * p] = fxs[q];
+                    w.fpre[4 * p + 1] = fys[q];
+                    w.fpre[4 * p + 2] = fxt[q];
+                    w.fpre[4 * p + 3] = fyt[q];
+                }
             }
             pos += (unsigned)__popcll(masks[q]);
         }
@@ -1095,16 +1324,13 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
         for (int q = 0; q < GI; ++q)
             if ((bel >> q) & 1u) fit_add(c, fxs[q], fys[q], fxt[q], fyt[q], fs.px, fs.py);
     }
-    // fixed tree: wave butterfly, then the waves in order
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc = acc + __shfl_xor(acc, o, 64);
-    if (lane == 0) s_w[threadIdx.x >> 6] = acc;
+    // fixed tree: DPP wave sums (lane 63), then the waves in order
+    acc = wave_sum63(acc);
+    if (lane == 63) s_w[threadIdx.x >> 6] = acc;
     if (fs.on) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) c[e] = c[e] + __shfl_xor(c[e], o, 64);
-        if (lane == 0)
+        for (int e = 0; e < 8; ++e) c[e] = wave_sum63(c[e]);
+        if (lane == 63)
 #pragma unroll
             for (int e = 0; e < 8; ++e) s_f[8 * (threadIdx.x >> 6) + e] = c[e];
     }
@@ -1124,8 +1350,8 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
 
 __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_t *orig,
                                                    const double *r, int64_t n, SelWS w,
-                                                   const int *skip, FitSrc fs) {
-    gather_body(key, orig, r, n, w, fs, blockIdx.x, 0u, skip);
+                                                   const int *skip, FitSrc fs, int pre) {
+    gather_body(key, orig, r, n, w, fs, blockIdx.x, 0u, skip, pre != 0);
 }
 
 // k_sel_bounds and k_sel_gather as one launch: block 0 computes the candidate buckets
@@ -1402,7 +1628,6 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
 // per thread, ranked by (key, orig) against all c in LDS (broadcast reads, no bins), one
 // block scan of r in sorted order, FRMSD of every position, first minimum.  Fewer
 // barriers than the binned sort of lds_sort_scan, whose fixed phases dominated at this c.
-constexpr int SMALL_C = 160;  // above it the binned sort ranks faster (390: 5.8 vs 3.4 us)
 // Pre: thread t < c holds candidate t (pk, po, pr; with the fused fit also its pair in
 // pf[4]), loaded in k_sel_final's prologue beside the state and S_base parts (they were a
 // second dependent round trip after the candidate count).
@@ -1982,12 +2207,18 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     const double Ub = w.ctl->U;
     CandPre pre{};
     const bool pfc = (int64_t)threadIdx.x < cap && threadIdx.x < (unsigned)SMALL_C;
-    uint32_t prow = 0;
     if (pfc) {
         pre.k = w.ka[threadIdx.x];
         pre.o = w.oa[threadIdx.x];
         pre.r = w.ra[threadIdx.x];
-        if (fs.on) prow = w.pa[threadIdx.x];
+        if (fs.on) {  // the gather stored the pairs of the first SMALL_C slots
+            const double2 a01 = *reinterpret_cast<const double2 *>(w.fpre + 4 * threadIdx.x);
+            const double2 a23 = *reinterpret_cast<const double2 *>(w.fpre + 4 * threadIdx.x + 2);
+            pre.f[0] = a01.x;
+            pre.f[1] = a01.y;
+            pre.f[2] = a23.x;
+            pre.f[3] = a23.y;
+        }
     }
     if (sk) {
         if (host_flag && threadIdx.x == 0)
@@ -2008,12 +2239,6 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
     if (t < 8) s_fit[t] = 0.0;
-    if (fs.on && pfc && t < c) {  // the candidate's pair (its row is known now)
-        pre.f[0] = fs.sx[prow];
-        pre.f[1] = fs.sy[prow];
-        pre.f[2] = fs.cx[prow];
-        pre.f[3] = fs.cy[prow];
-    }
     double a = 0.0;
     for (int p = t; p < nparts; p += HT) a = a + w.parts[p];  // fixed order per thread
     FinalIn in;
@@ -2225,7 +2450,7 @@ hipError_t launch_select_dist_gather(const unsigned long long *key, const uint32
     const int gb = gather_blocks(n);
     if (n > 0)
         hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip,
-                           FitSrc{});
+                           FitSrc{}, 0);
     hipLaunchKernelGGL(k_sel_pack, dim3(1), dim3(HT), 0, s, w, n > 0 ? gb : 0, skip, pack, capd);
     return hipGetLastError();
 }
@@ -2258,26 +2483,43 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     const HistPack hp = hist_pack(n);
     hipLaunchKernelGGL(k_sel_hist, dim3(hist_blocks(n)), dim3(HHT), 0, s, key, r, n, range,
                        range_parts, w, skip, hp, (const IterState *)st);
-    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip, hp,
-                       (long long *)nullptr);
     const int gb = gather_blocks(n);
     FitSrc fs{};
     if (fit && loop) fs = *fit;  // the fused fit needs the fused loop step (it runs after it)
-    static std::atomic<unsigned> s_gen{0};  // launch tokens, unique per process
-    unsigned gen = ++s_gen;
-    if (gen == 0) gen = ++s_gen;  // 0 means "no flag"
-    // FICP_SEL_SPLIT=1: the bounds and the gather as two launches (no in-launch hand-off:
-    // the one-launch form relies on block 0 being dispatched before the polling blocks,
-    // which HIP does not promise; the split form trades its +1.4 % for no such assumption)
+    // launch tokens, unique per launch in this process; the start is salted per process so
+    // that a token left in reused device memory by an earlier process cannot match
+    static std::atomic<unsigned> s_gen{((unsigned)getpid() * 2654435761u) & 0x3fffffffu};
+    unsigned gen = ++s_gen & 0x3fffffffu;
+    if (gen == 0) gen = ++s_gen & 0x3fffffffu;  // 0 means "no flag"
+    const unsigned pub = (fault & FICP_FAULT_SPIN) ? (gen ^ 0x40000000u) : gen;
+    // Three forms of the bounds (same candidate buckets):
+    //  * default: k_sel_reduce_bounds -- the bounds spread over the reduce's workgroups
+    //    (each waits only for the totals of the workgroups dispatched before it), the
+    //    gather reads [b0, b1] at its start;
+    //  * FICP_SEL_RB=0: k_sel_bounds_gather -- block 0 of the gather computes the bounds
+    //    and publishes them in-launch (relies on block 0 being dispatched first);
+    //  * FICP_SEL_SPLIT=1: k_sel_bounds + k_sel_gather, no in-launch hand-off at all.
+    // The first two raise ERR_SPIN instead of hanging should the dispatch order not hold.
     const char *sp = getenv("FICP_SEL_SPLIT");
     const bool split = sp && atoi(sp) != 0;
-    if (split) {
-        hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip, hp.fixb);
-        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs);
+    const char *rbe = getenv("FICP_SEL_RB");
+    const bool rb = !split && !(rbe && atoi(rbe) == 0);
+    if (rb) {
+        hipLaunchKernelGGL(k_sel_reduce_bounds, dim3(RBLK), dim3(1024), 0, s, w, hist_blocks(n), skip,
+                           hp, lam, lam_dev, gen, pub);
+        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs, 1);
     } else {
-        const unsigned pub = (fault & FICP_FAULT_SPIN) ? (gen ^ 0x40000000u) : gen;
-        hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n, w,
-                           lam, lam_dev, skip, hp.fixb, fs, gen, pub);
+        hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip,
+                           hp, (long long *)nullptr);
+        if (split) {
+            hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip,
+                               hp.fixb);
+            hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs,
+                               0);
+        } else {
+            hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n,
+                               w, lam, lam_dev, skip, hp.fixb, fs, gen, pub);
+        }
     }
     LoopCtl lc{};
     if (loop) lc = *loop;

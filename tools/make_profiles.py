@@ -2,7 +2,9 @@
 profiles/r1_c3_bench.json, r1_c3_kernel_stats.csv, r1_c3_trace_summary.json,
 r1_c3_timeline.txt, r1_pmc_c3_summary.json and r1_pmc_c3_nn.json (the NN kernel's HBM
 bytes per launch that bench.py reports as roofline.traffic).
-usage: python tools/make_profiles.py <tag> [prefix=r1]"""
+usage: python tools/make_profiles.py <tag> [prefix=r1]
+(<tag>/pmc/summary.json from tools/pmc.sh; an optional <tag>/cal_summary.json from
+tools/pmc_calib.py passes is recorded beside the NN bytes)"""
 import csv
 import json
 import re
@@ -41,30 +43,43 @@ def main(tag, prefix="r1"):
                    "active_dispatches": len(act), "active_avg_us": sum(act) / len(act),
                    "median_us": med}
     (dst / f"{prefix}_c3_trace_summary.json").write_text(json.dumps(summ, indent=1))
-    tl = subprocess.run([sys.executable, str(REPO / "tools" / "timeline.py"), str(trace)],  # FICP_TL_RUN picks the run
-                        capture_output=True, text=True, check=True).stdout
+    tl = subprocess.run([sys.executable, str(REPO / "tools" / "timeline.py"), str(trace), "k_run_start", "-v"],
+                        capture_output=True, text=True, check=True).stdout  # FICP_TL_RUN picks the run
     (dst / f"{prefix}_c3_timeline.txt").write_text(tl)
     pmc = json.loads((REPO / "gpurun_out" / tag / "pmc" / "summary.json").read_text())
     (dst / f"{prefix}_pmc_c3_summary.json").write_text(json.dumps(pmc, indent=1))
     nn = next(k for k in pmc if k.startswith("k_nn_grid<3"))
     d = pmc[nn]
+    groups = sorted({c for k in pmc for c in pmc[k] if c.isupper()})
+    mean = d.get("mean_active")
+    if mean and "fetch_bytes_raw" in mean and "write_bytes" in mean:
+        # per launch as the bench's average launch duration: the mean over the dispatches
+        # that did work (the cold call included); FETCH_SIZE x 2 as calibrated for 8-B
+        # lane reads (tools/pmc_calib.py: k_apply_inplace, 268,435,456 B read -> 134.2 MB)
+        hbm = 2.0 * mean["fetch_bytes_raw"] + mean["write_bytes"]
+        basis = "mean over active dispatches; FETCH_SIZE doubled (calibrated, tools/pmc_calib.py)"
+    else:
+        hbm = d["fetch_bytes_corrected"] + d["write_bytes"]
+        basis = "median over dispatches; FETCH_SIZE doubled per MI355X_MICROARCH.md"
+    cal = REPO / "gpurun_out" / tag / "cal_summary.json"
     nn_json = {
-        "source": "rocprofv3 --pmc, one pass per counter group (FETCH_SIZE / WRITE_SIZE / "
-                  "TCC_HIT_sum TCC_MISS_sum / SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES "
-                  "SQ_BUSY_CYCLES), tools/pmc.sh: python3 bench.py --no-cpu-baseline "
-                  "--steps 2 --warmup 1 (C3); medians over dispatches",
+        "source": "rocprofv3 --pmc, one pass per counter group (" + " ".join(groups) + "), "
+                  "python3 bench.py --no-extra --no-cpu-baseline --steps 2 --warmup 1 (C3)",
         "kernel": nn,
-        "per_launch_median": d,
-        "hbm_bytes_per_launch": d["fetch_bytes_corrected"] + d["write_bytes"],
-        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half of wide "
-                "reads); the kernel's reads are 8-16 B per lane, so the corrected fetch is "
-                "an estimate: raw fetch + write is the lower bound",
+        "per_launch_median": {k: v for k, v in d.items() if k != "mean_active"},
+        "per_launch_mean_active": mean,
+        "hbm_bytes_per_launch": hbm,
+        "basis": basis,
+        "calibration": json.loads(cal.read_text()) if cal.exists() else None,
     }
     (dst / f"{prefix}_pmc_c3_nn.json").write_text(json.dumps(nn_json, indent=1))
     # the bench line read the previous traffic file: carry this run's PMC bytes into it
     bj = json.loads((dst / f"{prefix}_c3_bench.json").read_text())
     bj["roofline"]["traffic"] = nn_json["hbm_bytes_per_launch"]
     (dst / f"{prefix}_c3_bench.json").write_text(json.dumps(bj) + "\n")
+    hp = src / "host_path_summary.json"
+    if hp.exists():
+        shutil.copy(hp, dst / f"{prefix}_host_path_trace.json")
     print(json.dumps({k: summ[k]["active_avg_us"] for k in summ if k.startswith("k_nn")}))
     print("hbm bytes per NN launch", nn_json["hbm_bytes_per_launch"])
 

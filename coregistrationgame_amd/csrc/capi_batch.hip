@@ -34,11 +34,12 @@ struct BatchBufs {
     int *h_flag = nullptr;                 // coherent pinned ring: plots still running
     PinBuf up;                             // pinned staging of the small per-run uploads
     PinBuf rep{nullptr, 0, hipHostMallocCoherent};  // report kernel target: states + flag
-    hipStream_t s2 = nullptr;              // the second sub-batch's stream (few plots)
-    hipEvent_t fork = nullptr, join = nullptr;
+    static constexpr int kSubMax = 4;
+    hipStream_t ss[kSubMax] = {};          // sub-batch streams 1.. (0 is the context's)
+    hipEvent_t fork = nullptr, join[kSubMax] = {};
 };
 constexpr int kBatchRing = 4;
-constexpr int kMaxSub = 2;  // sub-batches on their own streams (h_flag holds kMaxSub rings)
+constexpr int kMaxSub = BatchBufs::kSubMax;  // sub-batches on their own streams (h_flag: kMaxSub rings)
 
 void batch_release(BatchBufs *b) {
     if (!b) return;
@@ -52,9 +53,11 @@ void batch_release(BatchBufs *b) {
     for (DevBuf *d : bufs) d->release();
     b->up.release();
     b->rep.release();
-    if (b->s2) (void)hipStreamDestroy(b->s2);
+    for (int q = 0; q < kMaxSub; ++q) {
+        if (b->ss[q]) (void)hipStreamDestroy(b->ss[q]);
+        if (b->join[q]) (void)hipEventDestroy(b->join[q]);
+    }
     if (b->fork) (void)hipEventDestroy(b->fork);
-    if (b->join) (void)hipEventDestroy(b->join);
     if (b->h_flag) (void)hipHostFree(b->h_flag);
     delete b;
 }
@@ -253,16 +256,18 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // latency-bound selection (one workgroup per plot) runs beside the other half's
         // NN.  The plots are independent (app.py:658-660), so the split changes no result.
         // Measured with the fused step (tools/r3_iter6.sh, plot-it/s): 128 plots 846k vs
-        // 834k, 512 1,082k vs 1,019k, 1024 1,119k vs 1,061k.  FICP_BATCH_STREAMS=1|2
+        // 834k, 512 1,082k vs 1,019k, 1024 1,119k vs 1,061k.  FICP_BATCH_STREAMS=1..4
         // forces the count.
         int nsub = nplots >= 64 ? 2 : 1;
         if (const char *e = getenv("FICP_BATCH_STREAMS")) nsub = std::max(1, std::min(kMaxSub, atoi(e)));
         if (nsub > 1) {
-            if (!b.s2) HIPCHK(hipStreamCreateWithFlags(&b.s2, hipStreamNonBlocking));
             if (!b.fork) HIPCHK(hipEventCreateWithFlags(&b.fork, hipEventDisableTiming));
-            if (!b.join) HIPCHK(hipEventCreateWithFlags(&b.join, hipEventDisableTiming));
             HIPCHK(hipEventRecord(b.fork, c->stream));  // the grids, states and offsets are ready
-            HIPCHK(hipStreamWaitEvent(b.s2, b.fork, 0));
+            for (int q = 1; q < nsub; ++q) {
+                if (!b.ss[q]) HIPCHK(hipStreamCreateWithFlags(&b.ss[q], hipStreamNonBlocking));
+                if (!b.join[q]) HIPCHK(hipEventCreateWithFlags(&b.join[q], hipEventDisableTiming));
+                HIPCHK(hipStreamWaitEvent(b.ss[q], b.fork, 0));
+            }
         }
         struct Sub {
             int p0, np;
@@ -278,7 +283,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             u.np = (int)((int64_t)nplots * (q + 1) / nsub) - u.p0;
             u.r0 = so_h[u.p0];
             u.nr = so_h[u.p0 + u.np] - u.r0;
-            u.s = q == 0 ? c->stream : b.s2;
+            u.s = q == 0 ? c->stream : b.ss[q];
             u.ring = b.h_flag + q * kBatchRing;
             u.finished = u.np == 0;
         }
@@ -351,9 +356,9 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         }
         for (int q = 0; q < nsub; ++q)
             if (!subs[q].finished) return fail(FICP_EHIP, "batch did not converge within its bound");
-        if (nsub > 1) {
-            HIPCHK(hipEventRecord(b.join, b.s2));
-            HIPCHK(hipStreamWaitEvent(c->stream, b.join, 0));
+        for (int q = 1; q < nsub; ++q) {
+            HIPCHK(hipEventRecord(b.join[q], b.ss[q]));
+            HIPCHK(hipStreamWaitEvent(c->stream, b.join[q], 0));
         }
 
     }

@@ -148,12 +148,6 @@ constexpr int WCAP = 1024;          // candidate windows up to this many rows st
 
 typedef unsigned long long u64;
 
-__device__ __forceinline__ double wave_sum_d(double x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = x + __shfl_xor(x, o, 64);  // same bits on every lane
-    return x;
-}
-
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T x) {
     const int lane = threadIdx.x & 63;
@@ -176,8 +170,8 @@ struct SelRed {
 // block sum of a double in a fixed order (deterministic, same value on every thread)
 template <int NW>
 __device__ __forceinline__ double blk_sum_d(double x, SelRed<NW> &r) {
-    x = wave_sum_d(x);
-    if ((threadIdx.x & 63) == 0) r.d[threadIdx.x >> 6] = x;
+    x = wave_sum63(x);  // DPP (ficp_internal.h), lane 63
+    if ((threadIdx.x & 63) == 63) r.d[threadIdx.x >> 6] = x;
     __syncthreads();
     double t = r.d[0];
 #pragma unroll
@@ -188,9 +182,8 @@ __device__ __forceinline__ double blk_sum_d(double x, SelRed<NW> &r) {
 
 template <int NW>
 __device__ __forceinline__ double blk_min_d(double x, SelRed<NW> &r) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, 64));
-    if ((threadIdx.x & 63) == 0) r.d[threadIdx.x >> 6] = x;
+    x = wave_min63(x);
+    if ((threadIdx.x & 63) == 63) r.d[threadIdx.x >> 6] = x;
     __syncthreads();
     double t = r.d[0];
 #pragma unroll
@@ -202,14 +195,24 @@ __device__ __forceinline__ double blk_min_d(double x, SelRed<NW> &r) {
 // {max a, max b, sum c} over the block
 template <int NW>
 __device__ __forceinline__ void blk_max2_sum(u64 &a, u64 &b, unsigned &c, SelRed<NW> &r) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const u64 xa = __shfl_xor(a, o, 64), xb = __shfl_xor(b, o, 64);
-        a = xa > a ? xa : a;
-        b = xb > b ? xb : b;
-        c += __shfl_xor(c, o, 64);
+    // DPP steps; a lane a step does not write reads 0 (neutral for max of u64 and for +)
+#define MAX2SUM_STEP(CTRL, ROWM)                                                      \
+    {                                                                                 \
+        const u64 xa = (u64)dpp::mov_ll<CTRL, ROWM>(0, (long long)a);                 \
+        const u64 xb = (u64)dpp::mov_ll<CTRL, ROWM>(0, (long long)b);                 \
+        const unsigned xc = (unsigned)__builtin_amdgcn_update_dpp(0, (int)c, CTRL, ROWM, 0xf, false); \
+        a = xa > a ? xa : a;                                                          \
+        b = xb > b ? xb : b;                                                          \
+        c += xc;                                                                      \
     }
-    if ((threadIdx.x & 63) == 0) {
+    MAX2SUM_STEP(dpp::QP_XOR1, 0xf)
+    MAX2SUM_STEP(dpp::QP_XOR2, 0xf)
+    MAX2SUM_STEP(dpp::ROW_HALF_MIRROR, 0xf)
+    MAX2SUM_STEP(dpp::ROW_MIRROR, 0xf)
+    MAX2SUM_STEP(dpp::ROW_BCAST15, 0xA)
+    MAX2SUM_STEP(dpp::ROW_BCAST31, 0xC)
+#undef MAX2SUM_STEP
+    if ((threadIdx.x & 63) == 63) {
         r.a[threadIdx.x >> 6] = a;
         r.b[threadIdx.x >> 6] = b;
         r.c[threadIdx.x >> 6] = c;
@@ -300,16 +303,23 @@ __device__ __forceinline__ double blk_excl_scan_d(double x, double &total, SelRe
 
 template <int NW>
 __device__ __forceinline__ void blk_argmin(double &f, long long &k, SelRed<NW> &r) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double of = __shfl_xor(f, o, 64);
-        const long long ok = __shfl_xor(k, o, 64);
-        if (better(of, ok, f, k)) {
-            f = of;
-            k = ok;
-        }
+#define ARGMIN_STEP(CTRL, ROWM)                                                      \
+    {                                                                                \
+        const double of = dpp::mov_d<CTRL, ROWM>(INFINITY, f);                       \
+        const long long ok = dpp::mov_ll<CTRL, ROWM>(0x7fffffffffffffffLL, k);       \
+        if (better(of, ok, f, k)) {                                                  \
+            f = of;                                                                  \
+            k = ok;                                                                  \
+        }                                                                            \
     }
-    if ((threadIdx.x & 63) == 0) {
+    ARGMIN_STEP(dpp::QP_XOR1, 0xf)
+    ARGMIN_STEP(dpp::QP_XOR2, 0xf)
+    ARGMIN_STEP(dpp::ROW_HALF_MIRROR, 0xf)
+    ARGMIN_STEP(dpp::ROW_MIRROR, 0xf)
+    ARGMIN_STEP(dpp::ROW_BCAST15, 0xA)
+    ARGMIN_STEP(dpp::ROW_BCAST31, 0xC)
+#undef ARGMIN_STEP
+    if ((threadIdx.x & 63) == 63) {
         r.d[threadIdx.x >> 6] = f;
         r.l[threadIdx.x >> 6] = k;
     }
@@ -444,8 +454,8 @@ __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, do
         }
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) c[q] = wave_sum_d(c[q]);
-    if ((t & 63) == 0)
+    for (int q = 0; q < 8; ++q) c[q] = wave_sum63(c[q]);
+    if ((t & 63) == 63)
 #pragma unroll
         for (int q = 0; q < 8; ++q) s8[8 * (t >> 6) + q] = c[q];
     __syncthreads();
@@ -882,11 +892,11 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
             }
         }
     }
-    // the chunk's sums: wave butterfly, then the waves in order (fixed tree)
+    // the chunk's sums: DPP wave sums, then the waves in order (fixed tree)
     constexpr int FW = BB / 64;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) c[q] = wave_sum_d(c[q]);
-    if ((threadIdx.x & 63) == 0)
+    for (int q = 0; q < 8; ++q) c[q] = wave_sum63(c[q]);
+    if ((threadIdx.x & 63) == 63)
 #pragma unroll
         for (int q = 0; q < 8; ++q) s[8 * (threadIdx.x >> 6) + q] = c[q];
     __syncthreads();

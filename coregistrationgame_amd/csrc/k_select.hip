@@ -53,8 +53,8 @@ typedef unsigned __int128 u128;
 
 // phase timestamps of the final kernel (tools/selcheck built with -DSEL_PROF only)
 #ifdef SEL_PROF
-__device__ unsigned long long g_selprof[32];
-__device__ unsigned long long g_selclk[32];
+__device__ unsigned long long g_selprof[40];
+__device__ unsigned long long g_selclk[40];
 #define SELPROF(i)                                       \
     do {                                                 \
         __syncthreads();                                 \
@@ -69,7 +69,15 @@ __device__ unsigned long long g_selclk[32];
         if (blk == 0 && threadIdx.x == 0) g_selprof[i] = wall_clock64(); \
     } while (0)
 __device__ unsigned g_selcalls;
+// thread 0 of workgroup B stamps slot i (no barrier)
+#define BPROF(B, i)                                                         \
+    do {                                                                    \
+        if (blockIdx.x == (B) && threadIdx.x == 0) g_selprof[i] = wall_clock64(); \
+    } while (0)
 #else
+#define BPROF(B, i) \
+    do {            \
+    } while (0)
 #define SELPROF(i) \
     do {           \
     } while (0)
@@ -149,10 +157,10 @@ struct SelWS {
     uint32_t *pa, *pb;  // candidate row (work position): the fused fit reads its pair
     // k_sel_reduce_bounds (the bounds spread over the reduce workgroups):
     u64 *rbp;        // [RBLK * 5] each workgroup's bucket totals (count, lo, hi), tokened
-    double *lbv;     // [NB] lower bound of h inside each bucket (+inf: empty)
-    long long *cbef; // [NB] rows in the buckets before it
     double *ublk;    // [RBLK] upper bound of min h from each workgroup's bucket ends
-    double *mlb;     // [RBLK] smallest lbv of each workgroup's buckets
+    double *sblb;    // [NB / 4] smallest lower bound of h in each run of 4 buckets (+inf:
+                     // empty)
+    long long *sbcb; // [NB / 4] rows in the buckets before each run
     double *fpre;    // [SMALL_C][4] fused fit: the pair of pack slots < SMALL_C (gather)
 };
 
@@ -219,10 +227,9 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.pa = (uint32_t *)take(nn * 4);
     x.pb = (uint32_t *)take(nn * 4);
     x.rbp = (u64 *)take((NB / 64) * 5 * 8);
-    x.lbv = (double *)take(NB * 8);
-    x.cbef = (long long *)take(NB * 8);
     x.ublk = (double *)take((NB / 64) * 8);
-    x.mlb = (double *)take((NB / 64) * 8);
+    x.sblb = (double *)take(NB / 4 * 8);
+    x.sbcb = (long long *)take(NB / 4 * 8);
     x.fpre = (double *)take(SMALL_C * 32);
     if (w) *w = x;
     return (int64_t)(p - p0) + 256;
@@ -617,6 +624,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
                                                  u64 *range, int64_t nparts, SelWS w,
                                                  const int *skip, HistPack hp,
                                                  const IterState *st) {
+    BPROF(1, 30);
     const int sk = skip ? *skip : 0;  // checked after the first rows' loads have issued
     __shared__ u64 sp[NB];
     __shared__ u64 s_u[HHT / 64], s_v[HHT / 64];
@@ -673,6 +681,7 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
     }
     // every block derives the same map; block 0 publishes it for the later kernels
     const BMap bm = make_bmap(kmin, kmax, pv);
+    BPROF(1, 31);
     if (blockIdx.x == 0 && threadIdx.x == 0) w.ctl->map = bm;
     const u64 one = 1ULL << hp.shift;
     for (int64_t i = ib; i < i1; i += (int64_t)U * HHT) {
@@ -697,8 +706,10 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
         }
     }
     __syncthreads();
+    BPROF(1, 32);
     u64 *pp = w.ppk + (int64_t)blockIdx.x * NB;
     for (int b = threadIdx.x; b < NB; b += HHT) pp[b] = sp[b];
+    BPROF(1, 33);
 }
 
 // sum of the per-block histograms (integer sums: exact, order-free).  RG thread groups
@@ -805,9 +816,11 @@ __device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsig
 //      ERR_SPIN), sums them in a fixed order: the rows and sums before its buckets;
 //  (3) evaluates every bucket: h at its end (an upper bound of the minimum) and the lower
 //      bound of h inside it, both exactly as the one-workgroup bounds did for the buckets
-//      it evaluated; stores them with the rows before each bucket.
-// The gather then takes U = min over workgroups and [b0, b1] = the buckets whose lower
-// bound is <= U (pre_bounds): the same test as bounds_body, over every bucket.
+//      it evaluated; stores the smallest upper bound of the workgroup and, per run of 4
+//      buckets, the smallest lower bound and the rows before the run.
+// The gather then takes U = min over workgroups and [b0, b1] = the first to the last run
+// whose lower bound is <= U (pre_bounds): the buckets bounds_body selects, and at most 3
+// more on either side.
 constexpr int RBLK = NB / RBPB;  // workgroups of the reduce
 __device__ __forceinline__ u64 tok_pack(unsigned gen, uint32_t v) { return ((u64)gen << 32) | v; }
 
@@ -815,6 +828,7 @@ __global__ __launch_bounds__(1024) void k_sel_reduce_bounds(SelWS w, int nhb, co
                                                             HistPack hp, double lam,
                                                             const double *lam_dev, unsigned gen,
                                                             unsigned pub_gen) {
+    BPROF(64, 34);
     const int sk = skip ? *skip : 0;
     const double lamv = lam_dev ? *lam_dev : lam;
     __shared__ unsigned s_c[RG][RBPB];
@@ -852,6 +866,7 @@ __global__ __launch_bounds__(1024) void k_sel_reduce_bounds(SelWS w, int nhb, co
         c += s_c[h][bl];
         f += s_f[h][bl];
     }
+    BPROF(64, 35);
     const BMap bm = w.ctl->map;
     const int e = bucket_exp(bm, b);
     double lo, hi;
@@ -917,6 +932,7 @@ __global__ __launch_bounds__(1024) void k_sel_reduce_bounds(SelWS w, int nhb, co
         pl = pl + __longlong_as_double((long long)((v[1] << 32) | (v[2] & 0xffffffffULL)));
         ph = ph + __longlong_as_double((long long)((v[3] << 32) | (v[4] & 0xffffffffULL)));
     }
+    BPROF(64, 36);
     pc = bcast63_u64(wave_sum63_u64(pc));
     pl = bcast63(wave_sum63(pl));
     ph = bcast63(wave_sum63(ph));
@@ -932,13 +948,18 @@ __global__ __launch_bounds__(1024) void k_sel_reduce_bounds(SelWS w, int nhb, co
         hend = h_of(cb + (long long)c, phi, p) + kMarg;
         lb = (p >= 1.0) ? block_lb(cb, c, plo, lo_r(bucket_lo(bm, b)), p) : -INFINITY;
     }
-    w.lbv[b] = lb;
-    w.cbef[b] = cb;
-    const double um = wave_min63(hend), lm = wave_min63(lb);
-    if (bl == 63) {
-        w.ublk[bid] = um;
-        w.mlb[bid] = lm;
+    {  // runs of SBW = 4 buckets: their smallest lower bound and the rows before them
+        static_assert(NB / 4 == 2048, "sub-block layout");
+        double m = fmin(lb, dpp::mov_d<dpp::QP_XOR1>(INFINITY, lb));
+        m = fmin(m, dpp::mov_d<dpp::QP_XOR2>(INFINITY, m));
+        if ((bl & 3) == 0) {
+            w.sblb[b >> 2] = m;
+            w.sbcb[b >> 2] = cb;
+        }
     }
+    const double um = wave_min63(hend);
+    if (bl == 63) w.ublk[bid] = um;
+    BPROF(64, 37);
 }
 
 // [b0, b1] and U from k_sel_reduce_bounds' per-bucket bounds (every gather block, GT
@@ -947,54 +968,55 @@ __global__ __launch_bounds__(1024) void k_sel_reduce_bounds(SelWS w, int nhb, co
 // workgroups are skipped through their smallest lower bound).  Block 0 also stores b0,
 // b1, U and the rows below b0 for the final kernel.
 __device__ __forceinline__ void pre_bounds(const SelWS &w, int blk, int &b0, int &b1) {
-    static_assert(RBLK == 128 && GT >= 128, "two waves hold the reduce workgroups");
-    __shared__ double s_u[2];
-    __shared__ int s_j[4];
+    // one round of loads: the workgroups' upper bounds and the 2048 runs of 4 buckets'
+    // smallest lower bounds.  [b0, b1] spans the first to the last run that may hold a
+    // candidate: the exact buckets plus at most 3 on either side (their rows are scanned
+    // exactly by the final, the answer is the same), without the dependent per-bucket load
+    // of the exact form (which took ~6 us at C3 against ~2 for the rest of the gather)
+    static_assert(RBLK == 128 && GT == 512, "two waves hold the reduce workgroups, 4 runs per thread");
+    __shared__ double s_u[GT / 64];
+    __shared__ int s_j[2 * (GT / 64)];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    double ub = INFINITY, mb = INFINITY;
-    if (t < RBLK) {
-        ub = w.ublk[t];
-        mb = w.mlb[t];
-    }
+    const double ub = t < RBLK ? w.ublk[t] : INFINITY;
+    const double4 sv = *reinterpret_cast<const double4 *>(w.sblb + 4 * t);
     const double um = wave_min63(ub);
-    if (wv < 2 && lane == 63) s_u[wv] = um;
+    if (lane == 63) s_u[wv] = um;
     __syncthreads();
     const double U = fmin(s_u[0], s_u[1]);
-    if (wv < 2) {
-        const u64 m = __ballot(t < RBLK && !(mb > U));
-        if (lane == 0) {
-            s_j[wv] = m ? wv * 64 + __builtin_ctzll(m) : 0x7fffffff;
-            s_j[2 + wv] = m ? wv * 64 + 63 - __builtin_clzll(m) : -1;
-        }
+    int f = 0x7fffffff, l = -1;
+    if (!(sv.w > U)) { f = 4 * t + 3; l = 4 * t + 3; }
+    if (!(sv.z > U)) { f = 4 * t + 2; l = l < 0 ? 4 * t + 2 : l; }
+    if (!(sv.y > U)) { f = 4 * t + 1; l = l < 0 ? 4 * t + 1 : l; }
+    if (!(sv.x > U)) { f = 4 * t; l = l < 0 ? 4 * t : l; }
+    // block min of f, max of l (integers: any order)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        f = min(f, __shfl_xor(f, o, 64));
+        l = max(l, __shfl_xor(l, o, 64));
+    }
+    if (lane == 0) {
+        s_j[wv] = f;
+        s_j[GT / 64 + wv] = l;
     }
     __syncthreads();
-    const int j0 = min(s_j[0], s_j[1]), j1 = max(s_j[2], s_j[3]);
-    if (j1 < 0) {  // no bucket qualifies (non-finite r): every row is a candidate
+    int jf = s_j[0], jl = s_j[GT / 64];
+#pragma unroll
+    for (int q = 1; q < GT / 64; ++q) {
+        jf = min(jf, s_j[q]);
+        jl = max(jl, s_j[GT / 64 + q]);
+    }
+    if (jl < 0) {  // no bucket qualifies (non-finite r): every row is a candidate
         b0 = 0;
         b1 = NB - 1;
-        if (blk == 0 && t == 0) {
-            w.ctl->b0 = b0;
-            w.ctl->b1 = b1;
-            w.ctl->U = U;
-            w.ctl->kbase = 0;
-        }
-        return;
+    } else {
+        b0 = 4 * jf;
+        b1 = 4 * jl + 3;
     }
-    __syncthreads();  // s_j is rewritten below
-    if (wv < 2) {
-        const int j = wv ? j1 : j0;
-        const double l = w.lbv[j * 64 + lane];
-        const u64 m = __ballot(!(l > U));
-        if (lane == 0) s_j[wv] = wv ? j * 64 + 63 - __builtin_clzll(m) : j * 64 + __builtin_ctzll(m);
-    }
-    __syncthreads();
-    b0 = s_j[0];
-    b1 = s_j[1];
     if (blk == 0 && t == 0) {
         w.ctl->b0 = b0;
         w.ctl->b1 = b1;
         w.ctl->U = U;
-        w.ctl->kbase = w.cbef[b0];
+        w.ctl->kbase = jl < 0 ? 0 : w.sbcb[jf];
     }
 }
 
@@ -2328,12 +2350,14 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 #endif
     if (t == 0 && (g_selcalls++ % SEL_PROF_EVERY) == 6u % SEL_PROF_EVERY) {
         const unsigned long long *g = g_selprof;
-        printf("SELPROF c=%u->%u k=%lld lev=%u radix=%u bounds %lld %lld %lld %lld %lld %lld | gather +%lld wait %lld app %lld sums %lld"
+        printf("SELPROF c=%u->%u k=%lld lev=%u radix=%u hist %lld %lld %lld | rb +%lld %lld %lld %lld"
+               " | gather +%lld bounds %lld app %lld sums %lld"
                " | gap %lld final pro %lld small %lld %lld %lld %lld %lld post %lld tail %lld\n", c_in, c,
                (long long)s_st.k, w.ctl->levels, w.ctl->radix,
-               (long long)(g[9] - g[8]), (long long)(g[10] - g[9]), (long long)(g[11] - g[10]),
-               (long long)(g[12] - g[11]), (long long)(g[13] - g[12]), (long long)(g[14] - g[13]),
-               (long long)(g[26] - g[8]), (long long)(g[27] - g[26]), (long long)(g[28] - g[27]),
+               (long long)(g[31] - g[30]), (long long)(g[32] - g[31]), (long long)(g[33] - g[32]),
+               (long long)(g[34] - g[33]), (long long)(g[35] - g[34]), (long long)(g[36] - g[35]),
+               (long long)(g[37] - g[36]),
+               (long long)(g[26] - g[37]), (long long)(g[27] - g[26]), (long long)(g[28] - g[27]),
                (long long)(g[29] - g[28]), (long long)(g[0] - g[29]), (long long)(g[1] - g[0]),
                (long long)(g[21] - g[1]), (long long)(g[22] - g[21]), (long long)(g[23] - g[22]),
                (long long)(g[24] - g[23]), (long long)(g[25] - g[24]), (long long)(g[5] - g[25]),
@@ -2492,18 +2516,22 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     unsigned gen = ++s_gen & 0x3fffffffu;
     if (gen == 0) gen = ++s_gen & 0x3fffffffu;  // 0 means "no flag"
     const unsigned pub = (fault & FICP_FAULT_SPIN) ? (gen ^ 0x40000000u) : gen;
-    // Three forms of the bounds (same candidate buckets):
-    //  * default: k_sel_reduce_bounds -- the bounds spread over the reduce's workgroups
-    //    (each waits only for the totals of the workgroups dispatched before it), the
-    //    gather reads [b0, b1] at its start;
-    //  * FICP_SEL_RB=0: k_sel_bounds_gather -- block 0 of the gather computes the bounds
-    //    and publishes them in-launch (relies on block 0 being dispatched first);
+    // Three forms of the bounds:
+    //  * default: k_sel_bounds_gather -- block 0 of the gather computes the bounds and
+    //    publishes them in-launch (relies on block 0 being dispatched first) while the
+    //    other blocks' row loads are in flight;
+    //  * FICP_SEL_RB=1: k_sel_reduce_bounds -- the bounds spread over the reduce's
+    //    workgroups (each waits only for the totals of the workgroups dispatched before
+    //    it), the gather reads [b0, b1] (runs of 4 buckets) at its start.  Measured 2 %
+    //    slower at C3 (8,296-8,319 vs 8,456-8,476 it/s, tools/r3_iter13.sh): the gather's
+    //    row loads take as long as the one-workgroup bounds, which they hid, and the
+    //    reduce grew by its exchange;
     //  * FICP_SEL_SPLIT=1: k_sel_bounds + k_sel_gather, no in-launch hand-off at all.
     // The first two raise ERR_SPIN instead of hanging should the dispatch order not hold.
     const char *sp = getenv("FICP_SEL_SPLIT");
     const bool split = sp && atoi(sp) != 0;
     const char *rbe = getenv("FICP_SEL_RB");
-    const bool rb = !split && !(rbe && atoi(rbe) == 0);
+    const bool rb = !split && rbe && atoi(rbe) != 0;
     if (rb) {
         hipLaunchKernelGGL(k_sel_reduce_bounds, dim3(RBLK), dim3(1024), 0, s, w, hist_blocks(n), skip,
                            hp, lam, lam_dev, gen, pub);

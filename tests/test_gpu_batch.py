@@ -54,8 +54,9 @@ def test_batch_real_stand10():
 
 
 @pytest.mark.parametrize("knobs", [{}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_BATCH_STREAMS": "1"},
-                                   {"FICP_BATCH_FUSE": "0"}],
-                         ids=["bsort_grid_2streams", "atomic_grid", "one_stream", "fit_update_launches"])
+                                   {"FICP_BATCH_STREAMS": "4"}, {"FICP_BATCH_FUSE": "0"}],
+                         ids=["bsort_grid_2streams", "atomic_grid", "one_stream", "four_streams",
+                              "fit_update_launches"])
 def test_batch_vs_oracle_mixed(oracle, knobs, monkeypatch):
     """64 synthetic plots of mixed sizes (incl. 1-tree plots, empty layers, md=2 plots)
     vs the oracle run of each plot alone, with the batch grid built by the bucket sort

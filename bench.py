@@ -162,7 +162,7 @@ def pmc_traffic(kernel_prefix, tag):
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if str(d.get("kernel", "")).startswith(kernel_prefix):
+        if str(d.get("kernel", "")).startswith(kernel_prefix):  # str or tuple of prefixes
             best = (d["hbm_bytes_per_launch"], f.name)
     return best
 
@@ -450,7 +450,9 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
         avg_ms = nn["ms"] / max(timed_calls, 1)
         bytes_launch = nn_bytes_per_launch(n, m, md)
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic = pmc_traffic("k_nn_grid<3" if md == 3 else "k_nn_grid<2", "c3") if wl == "c3" else None
+        # the C3 NN's two kernels together (k_nn_grid + k_nn_grid_q, tools/pmc_summary.py)
+        traffic = (pmc_traffic(("k_nn_grid+q<3", "k_nn_grid<3") if md == 3 else ("k_nn_grid+q<2", "k_nn_grid<2"), "c3")
+                   if wl == "c3" else None)
         ib = iteration_bytes(n, m, md, n)
         out = {
             "metric": METRIC, "value": fits_all / dt_max, "unit": "iterations/s", "n_gpus": world,

@@ -30,6 +30,7 @@ struct BatchBufs {
     DevBuf key, gap, r, ccx, ccy, bp, dz2, wkey, skey, wrow, srow, wr, sr;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
     DevBuf fpart, fctr;                    // batch fit: per-chunk sums, per-plot arrivals
+    DevBuf arrive;                         // fused step: per sub-batch arrival/live counter
     unsigned fctr_init_gen = 0;            // fctr allocation whose counters are zeroed
     int *h_flag = nullptr;                 // coherent pinned ring: plots still running
     PinBuf up;                             // pinned staging of the small per-run uploads
@@ -49,7 +50,7 @@ void batch_release(BatchBufs *b) {
                       &b->r,        &b->ccx,     &b->ccy,      &b->wkey,  &b->skey,  &b->wrow,
                       &b->srow,     &b->wr,      &b->sr,       &b->sx,    &b->sy,    &b->sz,
                       &b->tx,       &b->ty,      &b->tz,       &b->stage, &b->bp,
-                      &b->dz2,      &b->bs_tmp,  &b->fpart,   &b->fctr};
+                      &b->dz2,      &b->bs_tmp,  &b->fpart,   &b->fctr, &b->arrive};
     for (DevBuf *d : bufs) d->release();
     b->up.release();
     b->rep.release();
@@ -260,6 +261,10 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // forces the count.
         int nsub = nplots >= 64 ? 2 : 1;
         if (const char *e = getenv("FICP_BATCH_STREAMS")) nsub = std::max(1, std::min(kMaxSub, atoi(e)));
+        // the fused step's arrival counters start at zero (each launch's last workgroup
+        // resets its own); zeroed here, before the fork, so an earlier failed run leaves none
+        CHK(b.arrive.ensure(kMaxSub * 8));
+        HIPCHK(hipMemsetAsync(b.arrive.p, 0, kMaxSub * 8, c->stream));
         if (nsub > 1) {
             if (!b.fork) HIPCHK(hipEventCreateWithFlags(&b.fork, hipEventDisableTiming));
             HIPCHK(hipEventRecord(b.fork, c->stream));  // the grids, states and offsets are ready
@@ -328,14 +333,18 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                                             b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
                                             md, u.s));
             }
+            BatchStepArgs su_step = step;  // this sub-batch's counter and flag
+            su_step.arrive = b.arrive.as<unsigned long long>() + (&u - subs);
+            su_step.flag = flag;
             {
                 ProfScope ps(c, prof ? P_FRAC : 0, "batch_select");
                 HIPCHK(launch_batch_select(b.key.as<unsigned long long>(), b.r.as<double>(), sou, u.np,
                                            max_rows, b.lams.as<double>(), su, ws, u.s,
-                                           bfuse ? &step : nullptr));
+                                           bfuse ? &su_step : nullptr));
             }
-            if (bfuse) HIPCHK(launch_batch_live(u.np, su, flag, u.s));
-            else HIPCHK(launch_batch_update(u.np, nstages, threshold, max_iter, su, flag, u.s));
+            // (fused: the selection's last workgroup stores the live count, k_batch.hip
+            // batch_arrive -- the k_batch_live launch cost ~5-8 us per batch iteration)
+            if (!bfuse) HIPCHK(launch_batch_update(u.np, nstages, threshold, max_iter, su, flag, u.s));
             return FICP_OK;
         };
         for (int q = 0; q < nsub; ++q)

@@ -810,6 +810,11 @@ struct BatchStepArgs {
     const PlotGrid *grids;
     int allow_refl, nstages, max_iter;
     double threshold;
+    // non-null: the selection's workgroups count their plots' arrivals here (zero before
+    // the first launch; the last one resets it) and the last stores the live count in *flag
+    // (no k_batch_live launch)
+    unsigned long long *arrive = nullptr;
+    int *flag = nullptr;
 };
 hipError_t launch_batch_live(int nplots, const PlotState *st, int *flag, hipStream_t s);
 hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,

@@ -408,7 +408,25 @@ struct BatchStep {
     const PlotGrid *grids;
     int fuse, allow_refl, nstages, max_iter;
     double threshold;
+    unsigned long long *arrive;  // (arrivals << 32) + live plots of this launch (nullable)
+    int *flag;                   // the last arrival stores the live count (pinned host word)
+    int nplots;
 };
+
+// thread 0 of plot p's workgroup, its state final for this call: one agent-scope atomic
+// adds (1 << 32) + live; the workgroup that completes the count stores the number of live
+// plots into the host's flag and resets the counter for the next launch (stream-ordered)
+__device__ __forceinline__ void batch_arrive(const BatchStep &bs, int live) {
+    if (!bs.arrive) return;
+    const u64 add = (1ULL << 32) | (u64)(unsigned)live;
+    const u64 old = __hip_atomic_fetch_add(bs.arrive, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)(old >> 32) + 1 == bs.nplots) {
+        const int tot = (int)(old & 0xffffffffULL) + live;
+        __hip_atomic_exchange(bs.arrive, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+        __hip_atomic_store(bs.flag, tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 
 template <int NW>
 __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, double frmsd,
@@ -428,6 +446,7 @@ __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, do
         step_plot(s, bs.nstages, bs.threshold, bs.max_iter);
         s_flag[0] = s.phase == PH_LOOP && s.k > 0;  // a loop body (fit -> apply -> NN) follows
         st[p] = s;
+        batch_arrive(bs, s.phase != PH_DONE ? 1 : 0);
     }
     __syncthreads();
     if (!s_flag[0]) return;
@@ -532,7 +551,10 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     // the phase, the stage and the plot's row range load together (one latency, not two)
     const int ph = st[p].phase, stg = st[p].stage;
     const int64_t b = so[p], e = so[p + 1];
-    if (ph == PH_DONE) return;  // uniform per workgroup
+    if (ph == PH_DONE) {  // uniform per workgroup
+        if (t == 0) batch_arrive(bs, 0);
+        return;
+    }
 #ifdef FICP_BSEL_PROF
     long long bt_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1079,6 +1101,9 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
         bs.nstages = step->nstages;
         bs.max_iter = step->max_iter;
         bs.threshold = step->threshold;
+        bs.arrive = step->arrive;
+        bs.flag = step->flag;
+        bs.nplots = nplots;
     }
     // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
     // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers)

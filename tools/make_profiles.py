@@ -48,7 +48,8 @@ def main(tag, prefix="r1"):
     (dst / f"{prefix}_c3_timeline.txt").write_text(tl)
     pmc = json.loads((REPO / "gpurun_out" / tag / "pmc" / "summary.json").read_text())
     (dst / f"{prefix}_pmc_c3_summary.json").write_text(json.dumps(pmc, indent=1))
-    nn = next(k for k in pmc if k.startswith("k_nn_grid<3"))
+    nn = next((k for k in pmc if k.startswith("k_nn_grid+q<3")), None) or \
+        next(k for k in pmc if k.startswith("k_nn_grid<3"))
     d = pmc[nn]
     groups = sorted({c for k in pmc for c in pmc[k] if c.isupper()})
     mean = d.get("mean_active")
@@ -76,6 +77,7 @@ def main(tag, prefix="r1"):
     # the bench line read the previous traffic file: carry this run's PMC bytes into it
     bj = json.loads((dst / f"{prefix}_c3_bench.json").read_text())
     bj["roofline"]["traffic"] = nn_json["hbm_bytes_per_launch"]
+    bj["roofline"]["traffic_source"] = f"{prefix}_pmc_c3_nn.json"
     (dst / f"{prefix}_c3_bench.json").write_text(json.dumps(bj) + "\n")
     hp = src / "host_path_summary.json"
     if hp.exists():

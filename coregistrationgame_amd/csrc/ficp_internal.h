@@ -73,6 +73,49 @@ __device__ __forceinline__ long long mov_ll(long long old, long long x) {
 }
 }  // namespace dpp
 
+// inclusive wave scans (every lane; fixed association: Hillis-Steele inside each row of
+// 16 lanes by row_shr, then rows 0->1, 2->3 by row_bcast15 and rows 0-1 -> 2, 3 by
+// row_bcast31), and the exclusive form by wave_shr:1 (lane 0 gets 0)
+namespace dpp {
+constexpr int ROW_SHR1 = 0x111, ROW_SHR2 = 0x112, ROW_SHR4 = 0x114, ROW_SHR8 = 0x118;
+constexpr int WAVE_SHR1 = 0x138;
+template <int CTRL, int ROWM = 0xf>
+__device__ __forceinline__ double movz_d(double x) {  // out-of-range source: 0
+    const long long ux = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)ux, CTRL, ROWM, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(ux >> 32), CTRL, ROWM, 0xf, true);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int CTRL, int ROWM = 0xf>
+__device__ __forceinline__ long long movz_ll(long long x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWM, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), CTRL, ROWM, 0xf, true);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+}  // namespace dpp
+
+__device__ __forceinline__ double wave_incl_scan_d(double x) {
+    x = x + dpp::movz_d<dpp::ROW_SHR1>(x);
+    x = x + dpp::movz_d<dpp::ROW_SHR2>(x);
+    x = x + dpp::movz_d<dpp::ROW_SHR4>(x);
+    x = x + dpp::movz_d<dpp::ROW_SHR8>(x);
+    x = x + dpp::mov_d<dpp::ROW_BCAST15, 0xA>(0.0, x);
+    x = x + dpp::mov_d<dpp::ROW_BCAST31, 0xC>(0.0, x);
+    return x;
+}
+__device__ __forceinline__ long long wave_incl_scan_ll(long long x) {
+    x += dpp::movz_ll<dpp::ROW_SHR1>(x);
+    x += dpp::movz_ll<dpp::ROW_SHR2>(x);
+    x += dpp::movz_ll<dpp::ROW_SHR4>(x);
+    x += dpp::movz_ll<dpp::ROW_SHR8>(x);
+    x += dpp::mov_ll<dpp::ROW_BCAST15, 0xA>(0, x);
+    x += dpp::mov_ll<dpp::ROW_BCAST31, 0xC>(0, x);
+    return x;
+}
+// the value of the lane below (lane 0: 0)
+__device__ __forceinline__ double wave_shr1_d(double x) { return dpp::movz_d<dpp::WAVE_SHR1>(x); }
+__device__ __forceinline__ long long wave_shr1_ll(long long x) { return dpp::movz_ll<dpp::WAVE_SHR1>(x); }
+
 // wave sum, valid in lane 63
 __device__ __forceinline__ double wave_sum63(double x) {
     x = x + dpp::mov_d<dpp::QP_XOR1>(0.0, x);

@@ -148,17 +148,6 @@ constexpr int WCAP = 1024;          // candidate windows up to this many rows st
 
 typedef unsigned long long u64;
 
-template <typename T>
-__device__ __forceinline__ T wave_incl_scan(T x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const T y = __shfl_up(x, o, 64);
-        if (lane >= o) x = x + y;
-    }
-    return x;
-}
-
 template <int NW>
 struct SelRed {
     double d[NW];
@@ -256,15 +245,12 @@ __device__ __forceinline__ void blk_minmax_ll(long long &lo, long long &hi, SelR
 // exclusive scan over the block (thread order) of a count and a sum; fixed schedule
 template <int NW>
 __device__ __forceinline__ void blk_excl_scan2(unsigned &c, double &x, SelRed<NW> &r) {
-    const unsigned ci = wave_incl_scan(c);
-    const double xi = wave_incl_scan(x);
+    // DPP wave scans (ficp_internal.h)
+    const unsigned ci = (unsigned)wave_incl_scan_ll((long long)c);
+    const double xi = wave_incl_scan_d(x);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    unsigned ce = __shfl_up(ci, 1, 64);
-    double xe = __shfl_up(xi, 1, 64);
-    if (lane == 0) {
-        ce = 0;
-        xe = 0.0;
-    }
+    const unsigned ce = (unsigned)wave_shr1_ll((long long)ci);
+    const double xe = wave_shr1_d(xi);
     if (lane == 63) {
         r.c[w] = ci;
         r.d[w] = xi;
@@ -284,10 +270,9 @@ __device__ __forceinline__ void blk_excl_scan2(unsigned &c, double &x, SelRed<NW
 // exclusive scan of a double over the block + the block total; fixed schedule
 template <int NW>
 __device__ __forceinline__ double blk_excl_scan_d(double x, double &total, SelRed<NW> &r) {
-    const double xi = wave_incl_scan(x);
+    const double xi = wave_incl_scan_d(x);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double xe = __shfl_up(xi, 1, 64);
-    if (lane == 0) xe = 0.0;
+    const double xe = wave_shr1_d(xi);
     if (lane == 63) r.d[w] = xi;
     __syncthreads();
     double xp = 0.0, tot = 0.0;

@@ -500,15 +500,9 @@ __device__ __forceinline__ long long blk_min_ll(long long x, Scr &s) {
 // exclusive scans (deterministic: Hillis-Steele in the wave, wave offsets in order)
 __device__ __forceinline__ double blk_excl_scan_d(double v, Scr &s, double &total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    double x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_up(x, o, 64);
-        if (lane >= o) x = y + x;
-    }
+    const double x = wave_incl_scan_d(v);  // DPP (ficp_internal.h)
     if (lane == 63) s.d[wave] = x;
-    double ex = __shfl_up(x, 1, 64);
-    if (lane == 0) ex = 0.0;
+    const double ex = wave_shr1_d(x);
     __syncthreads();
     double off = 0.0, tot = 0.0;
 #pragma unroll
@@ -523,12 +517,7 @@ __device__ __forceinline__ double blk_excl_scan_d(double v, Scr &s, double &tota
 
 __device__ __forceinline__ long long blk_excl_scan_ll(long long v, Scr &s, long long &total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    long long x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const long long x = wave_incl_scan_ll(v);
     if (lane == 63) s.l[wave] = x;
     __syncthreads();
     long long off = 0, tot = 0;
@@ -546,25 +535,14 @@ __device__ __forceinline__ long long blk_excl_scan_ll(long long v, Scr &s, long 
 // order, as blk_excl_scan_ll + two blk_excl_scan_d; one set of barriers)
 __device__ __forceinline__ void blk_excl_scan3(long long &c, double &a, double &b, Scr &s) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    long long xc = c;
-    double xa = a, xb = b;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long yc = __shfl_up(xc, o, 64);
-        const double ya = __shfl_up(xa, o, 64), yb = __shfl_up(xb, o, 64);
-        if (lane >= o) {
-            xc += yc;
-            xa = ya + xa;
-            xb = yb + xb;
-        }
-    }
+    const long long xc = wave_incl_scan_ll(c);
+    const double xa = wave_incl_scan_d(a), xb = wave_incl_scan_d(b);
     if (lane == 63) {
         s.l[wave] = xc;
         s.d[wave] = xa;
         s.u[wave] = (u64)__double_as_longlong(xb);
     }
-    double ea = __shfl_up(xa, 1, 64), eb = __shfl_up(xb, 1, 64);
-    if (lane == 0) ea = eb = 0.0;
+    const double ea = wave_shr1_d(xa), eb = wave_shr1_d(xb);
     __syncthreads();
     long long oc = 0;
     double oa = 0.0, ob = 0.0;
@@ -1049,6 +1027,38 @@ __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
     const BMap bm = w.ctl->map;
     const long long ct = w.acnt[t];
     const double tlo = w.alo[t], thi = w.ahi[t];
+    unsigned cc[PER];
+    double blo[PER], bhi[PER];
+#ifndef FICP_BOUNDS_PRELOAD
+#define FICP_BOUNDS_PRELOAD 0
+#endif
+    // FICP_BOUNDS_PRELOAD=1: every thread loads its 16 buckets with the chunk totals (one
+    // round of loads, 160 KB) instead of only the active chunks after U1 (a second,
+    // dependent round): 136 VGPRs for the gather blocks too, measured 4-5 % slower at C3
+    // (8,140 vs 8,486-8,555 it/s, tools/r3_iter18.sh)
+    auto load_buckets = [&]() {
+#pragma unroll
+        for (int j = 0; j < PER; j += 4) {
+            const uint4 c4 = *reinterpret_cast<const uint4 *>(w.hcnt + t * PER + j);
+            const double2 l0 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j);
+            const double2 l1 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j + 2);
+            const double2 h0 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j);
+            const double2 h1 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j + 2);
+            cc[j] = c4.x;
+            cc[j + 1] = c4.y;
+            cc[j + 2] = c4.z;
+            cc[j + 3] = c4.w;
+            blo[j] = l0.x;
+            blo[j + 1] = l0.y;
+            blo[j + 2] = l1.x;
+            blo[j + 3] = l1.y;
+            bhi[j] = h0.x;
+            bhi[j + 1] = h0.y;
+            bhi[j + 2] = h1.x;
+            bhi[j + 3] = h1.y;
+        }
+    };
+    if (FICP_BOUNDS_PRELOAD) load_buckets();
     if (sk) return kBoundsSkipped;
     lam = lamv;
     SELPROF(8);
@@ -1073,29 +1083,8 @@ __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
     const bool active = ct && (!(block_lb(Cex, ct, Plo, lo_r(bucket_lo(bm, t * PER)), p) -
                                        1e-9 > U1) ||
                                !(p >= 1.0));
-    unsigned cc[PER];
-    double blo[PER], bhi[PER];
     if (active) {
-#pragma unroll
-        for (int j = 0; j < PER; j += 4) {
-            const uint4 c4 = *reinterpret_cast<const uint4 *>(w.hcnt + t * PER + j);
-            const double2 l0 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j);
-            const double2 l1 = *reinterpret_cast<const double2 *>(w.hlo + t * PER + j + 2);
-            const double2 h0 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j);
-            const double2 h1 = *reinterpret_cast<const double2 *>(w.hhi + t * PER + j + 2);
-            cc[j] = c4.x;
-            cc[j + 1] = c4.y;
-            cc[j + 2] = c4.z;
-            cc[j + 3] = c4.w;
-            blo[j] = l0.x;
-            blo[j + 1] = l0.y;
-            blo[j + 2] = l1.x;
-            blo[j + 3] = l1.y;
-            bhi[j] = h0.x;
-            bhi[j + 1] = h0.y;
-            bhi[j + 2] = h1.x;
-            bhi[j + 3] = h1.y;
-        }
+        if (!FICP_BOUNDS_PRELOAD) load_buckets();
         const int a = atomicAdd(&s_nact, 1);
         if (a < MAXACT) {
             s_act[a] = t;

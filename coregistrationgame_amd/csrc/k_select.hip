@@ -660,7 +660,13 @@ __global__ __launch_bounds__(HHT) void k_sel_hist(const u64 *key, const double *
     // every block derives the same map; block 0 publishes it for the later kernels
     const BMap bm = make_bmap(kmin, kmax, pv);
     BPROF(1, 31);
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.ctl->map = bm;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        w.ctl->map = bm;
+        // the candidate counter of this call starts at zero: reset here, a launch before
+        // the gather's appends (k_sel_bounds_gather's block 0 then publishes the bounds
+        // without first draining a reset of its own)
+        __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const u64 one = 1ULL << hp.shift;
     for (int64_t i = ib; i < i1; i += (int64_t)U * HHT) {
         if (i != ib) {
@@ -1009,7 +1015,7 @@ constexpr int MAXACT = HT / (NB / HT);  // active chunks evaluated one bucket pe
 constexpr unsigned kBoundsSkipped = 0xffffffffu;
 __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
                                                 const double *lam_dev, const int *skip,
-                                                int fixb) {
+                                                int fixb, bool reset_ccount = true) {
     constexpr int PER = NB / HT;
     __shared__ Scr scr;
     __shared__ int s_act[MAXACT];
@@ -1179,7 +1185,8 @@ __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
         w.ctl->b0 = (int)bmin;
         w.ctl->b1 = (int)bmax;
         w.ctl->U = U;
-        __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (reset_ccount)
+            __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     SELPROF(14);
     return ((unsigned)bmin << 16) | (unsigned)bmax;
@@ -1376,12 +1383,12 @@ __global__ __launch_bounds__(GT) void k_sel_bounds_gather(const u64 *key, const 
                                                           const int *skip, int fixb, FitSrc fs,
                                                           unsigned gen, unsigned pub_gen) {
     if (blockIdx.x == 0) {
-        const unsigned bb = bounds_body(w, n, lam, lam_dev, skip, fixb);
+        // (ccount was reset by k_sel_hist, a launch earlier: nothing to drain before the
+        // flag; b0, b1, U and kbase are read by k_sel_final, a later launch)
+        const unsigned bb = bounds_body(w, n, lam, lam_dev, skip, fixb, false);
         if (bb != kBoundsSkipped && threadIdx.x == 0) {
-            // thread 0 reset ccount (atomic) inside bounds_body: drain it before the flag,
-            // so no gather block's append can precede the reset.  (pub_gen == gen except
-            // under the test-only fault injection FICP_FAULT_SPIN, ficp_set_fault)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // (pub_gen == gen except under the test-only fault injection FICP_FAULT_SPIN,
+            // ficp_set_fault)
             __hip_atomic_store(&w.ctl->bpub, ((u64)pub_gen << 32) | bb, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2339,14 +2346,15 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 #endif
     if (t == 0 && (g_selcalls++ % SEL_PROF_EVERY) == 6u % SEL_PROF_EVERY) {
         const unsigned long long *g = g_selprof;
-        printf("SELPROF c=%u->%u k=%lld lev=%u radix=%u hist %lld %lld %lld | rb +%lld %lld %lld %lld"
+        printf("SELPROF c=%u->%u k=%lld lev=%u radix=%u hist %lld %lld %lld | b0 +%lld %lld %lld %lld %lld %lld %lld"
                " | gather +%lld bounds %lld app %lld sums %lld"
                " | gap %lld final pro %lld small %lld %lld %lld %lld %lld post %lld tail %lld\n", c_in, c,
                (long long)s_st.k, w.ctl->levels, w.ctl->radix,
                (long long)(g[31] - g[30]), (long long)(g[32] - g[31]), (long long)(g[33] - g[32]),
-               (long long)(g[34] - g[33]), (long long)(g[35] - g[34]), (long long)(g[36] - g[35]),
-               (long long)(g[37] - g[36]),
-               (long long)(g[26] - g[37]), (long long)(g[27] - g[26]), (long long)(g[28] - g[27]),
+               (long long)(g[8] - g[33]), (long long)(g[9] - g[8]), (long long)(g[10] - g[9]),
+               (long long)(g[11] - g[10]), (long long)(g[12] - g[11]), (long long)(g[13] - g[12]),
+               (long long)(g[14] - g[13]),
+               (long long)(g[26] - g[8]), (long long)(g[27] - g[26]), (long long)(g[28] - g[27]),
                (long long)(g[29] - g[28]), (long long)(g[0] - g[29]), (long long)(g[1] - g[0]),
                (long long)(g[21] - g[1]), (long long)(g[22] - g[21]), (long long)(g[23] - g[22]),
                (long long)(g[24] - g[23]), (long long)(g[25] - g[24]), (long long)(g[5] - g[25]),

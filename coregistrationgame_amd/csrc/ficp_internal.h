@@ -172,14 +172,26 @@ __device__ __forceinline__ double wave_max63(double x) {
 }
 
 // wave-wide max of two u64 (all 64 lanes must be active)
+// (DPP steps, like wave_sum63 below; a step's unwritten lanes read 0, neutral for max)
+// -- the result is valid in lane 63 only
+template <int CTRL, int ROWM>
+__device__ __forceinline__ void range_step(unsigned long long &a, unsigned long long &b) {
+    const int alo = __builtin_amdgcn_update_dpp(0, (int)a, CTRL, ROWM, 0xf, false);
+    const int ahi = __builtin_amdgcn_update_dpp(0, (int)(a >> 32), CTRL, ROWM, 0xf, false);
+    const int blo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWM, 0xf, false);
+    const int bhi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWM, 0xf, false);
+    const unsigned long long xa = ((unsigned long long)(unsigned)ahi << 32) | (unsigned)alo;
+    const unsigned long long xb = ((unsigned long long)(unsigned)bhi << 32) | (unsigned)blo;
+    a = xa > a ? xa : a;
+    b = xb > b ? xb : b;
+}
 __device__ __forceinline__ void wave_range_reduce(unsigned long long &a, unsigned long long &b) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long xa = __shfl_xor(a, o, 64);
-        const unsigned long long xb = __shfl_xor(b, o, 64);
-        a = xa > a ? xa : a;
-        b = xb > b ? xb : b;
-    }
+    range_step<0xB1, 0xf>(a, b);   // quad_perm [1, 0, 3, 2]
+    range_step<0x4E, 0xf>(a, b);   // quad_perm [2, 3, 0, 1]
+    range_step<0x141, 0xf>(a, b);  // row_half_mirror
+    range_step<0x140, 0xf>(a, b);  // row_mirror
+    range_step<0x142, 0xA>(a, b);  // row_bcast15 -> rows 1, 3
+    range_step<0x143, 0xC>(a, b);  // row_bcast31 -> rows 2, 3
 }
 
 // Key range of a sort input, produced without atomics: every producing workgroup stores
@@ -196,12 +208,14 @@ __device__ __forceinline__ void block_range_store(unsigned long long *range, boo
     unsigned long long a = valid ? kmin_c : 0ULL, b = valid ? kmax : 0ULL;
     wave_range_reduce(a, b);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) {
+    if (lane == 63) {
         s_ra[wave] = a;
         s_rb[wave] = b;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        a = s_ra[0];
+        b = s_rb[0];
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
             a = s_ra[w] > a ? s_ra[w] : a;
             b = s_rb[w] > b ? s_rb[w] : b;

@@ -987,8 +987,8 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g)
             // Q - 1, so the selection reads no stale part
             __shared__ unsigned long long s_ra[4], s_rb[4];
             unsigned long long ra = kmin_c, rb = kmax;
-            wave_range_reduce(ra, rb);
-            if ((t & 63) == 0) {
+            wave_range_reduce(ra, rb);  // (lane 63)
+            if ((t & 63) == 63) {
                 s_ra[t >> 6] = ra;
                 s_rb[t >> 6] = rb;
             }

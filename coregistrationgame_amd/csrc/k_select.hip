@@ -422,13 +422,23 @@ __device__ __forceinline__ double blk_max_d(double x, Scr &s) {
 // {min, max} of two u64 quantities at once: returns min(a), max(b)
 template <int NW = NWAVE>
 __device__ __forceinline__ void blk_minmax_u64(u64 &a, u64 &b, u64 *su, u64 *sv) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const u64 xa = __shfl_xor(a, o, 64), xb = __shfl_xor(b, o, 64);
-        a = xa < a ? xa : a;
-        b = xb > b ? xb : b;
+    // DPP steps (lane 63 ends with the wave's values; unwritten lanes read the neutral
+    // values ~0 for the min and 0 for the max)
+#define MINMAX_STEP(CTRL, ROWM)                                                       \
+    {                                                                                 \
+        const u64 xa = (u64)dpp::mov_ll<CTRL, ROWM>(-1LL, (long long)a);              \
+        const u64 xb = (u64)dpp::mov_ll<CTRL, ROWM>(0, (long long)b);                 \
+        a = xa < a ? xa : a;                                                          \
+        b = xb > b ? xb : b;                                                          \
     }
-    if ((threadIdx.x & 63) == 0) {
+    MINMAX_STEP(dpp::QP_XOR1, 0xf)
+    MINMAX_STEP(dpp::QP_XOR2, 0xf)
+    MINMAX_STEP(dpp::ROW_HALF_MIRROR, 0xf)
+    MINMAX_STEP(dpp::ROW_MIRROR, 0xf)
+    MINMAX_STEP(dpp::ROW_BCAST15, 0xA)
+    MINMAX_STEP(dpp::ROW_BCAST31, 0xC)
+#undef MINMAX_STEP
+    if ((threadIdx.x & 63) == 63) {
         su[threadIdx.x >> 6] = a;
         sv[threadIdx.x >> 6] = b;
     }

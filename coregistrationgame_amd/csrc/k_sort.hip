@@ -104,14 +104,16 @@ __global__ __launch_bounds__(1024) void k_range_reduce(unsigned long long *range
         a = max(a, v.x);
         b = max(b, v.y);
     }
-    wave_range_reduce(a, b);
+    wave_range_reduce(a, b);  // (lane 63)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) {
+    if (lane == 63) {
         s_a[wave] = a;
         s_b[wave] = b;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        a = s_a[0];
+        b = s_b[0];
         for (int w = 1; w < 16; ++w) {
             a = max(a, s_a[w]);
             b = max(b, s_b[w]);

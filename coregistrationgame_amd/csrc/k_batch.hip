@@ -437,7 +437,10 @@ __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, do
     if (!s_flag[0]) return;
     const PlotGrid g = bs.grids[p];
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    constexpr int FU = 8;  // rows in flight per thread (every load before its predicate)
+#ifndef FICP_BFIT_FU
+#define FICP_BFIT_FU 8
+#endif
+    constexpr int FU = FICP_BFIT_FU;  // rows in flight per thread (every load before its predicate)
     for (int64_t i0 = b + t; i0 < e; i0 += (int64_t)FU * NT) {
         u64 kv[FU];
         double xs[FU], ys[FU], xt[FU], yt[FU];

@@ -171,10 +171,10 @@ inline int gather_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + GT *
 // wave-instruction per ~50 ns per CU (MI355X_MICROARCH.md, global atomics), so flushing
 // 8192 buckets with atomics cost ~15 us and reading + resetting them from one CU ~25 us.
 #ifndef FICP_HIST_ROWS
-#define FICP_HIST_ROWS 8192
+#define FICP_HIST_ROWS 4096  // 256 x 4096 rows: +0.5 % at C3 over 128 x 8192 (tools/r3_iter23.sh)
 #endif
 #ifndef FICP_HBMAX
-#define FICP_HBMAX 128
+#define FICP_HBMAX 256
 #endif
 constexpr int HBMAX = FICP_HBMAX;
 constexpr int HROWS = FICP_HIST_ROWS;  // rows per histogram block (target)

@@ -51,7 +51,7 @@ def main(tag, prefix="r1"):
     nn = next((k for k in pmc if k.startswith("k_nn_grid+q<3")), None) or \
         next(k for k in pmc if k.startswith("k_nn_grid<3"))
     d = pmc[nn]
-    groups = sorted({c for k in pmc for c in pmc[k] if c.isupper()})
+    groups = sorted({c for k in pmc for c in pmc[k] if re.match(r"^[A-Z][A-Z0-9_]*(_sum|_avr|_max|_min)?$", c)})
     mean = d.get("mean_active")
     if mean and "fetch_bytes_raw" in mean and "write_bytes" in mean:
         # per launch as the bench's average launch duration: the mean over the dispatches

@@ -165,7 +165,7 @@ int main(int argc, char **argv) {
                                (const double *)nullptr, (const int *)nullptr, hist_pack(n).fixb);
             CK(hipEventRecord(ev[2], 0));
             hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
-                               (const int *)nullptr, FitSrc{});
+                               (const int *)nullptr, FitSrc{}, 0);
         }
         CK(hipEventRecord(ev[3], 0));
         LoopCtl lc{};
@@ -205,13 +205,9 @@ int main(int argc, char **argv) {
                        it, h.k, h.frmsd, h.tkey, h.torig, bk, bf);
         }
     }
-    unsigned stats[3];
-    unsigned *dstats;
-    CK(hipMalloc(&dstats, 16));
-    CK(launch_select_stats(tmp, n, dstats, 0));
-    CK(hipMemcpy(stats, dstats, 12, hipMemcpyDeviceToHost));
     SelCtl ctl;
     CK(hipMemcpy(&ctl, w.ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    const unsigned stats[3] = {ctl.err, ctl.levels, ctl.radix};  // the report's three words
     const char *names[4] = {"hist+red", "bounds", "gather", "final"};
     printf("n=%lld mode=%d lam=%g k=%lld cand=%u window cand (+0,+8,-64,+512)=%u,%u,%u,%u "
            "buckets=[%d,%d] levels=%u chunked=%u radix=%u err=%u bad=%d/%d\n",

@@ -122,6 +122,7 @@ def lib():
         "ficp_set_fault": ([_vp, _i32], C.c_int),
         "ficp_profile_enable": ([_vp, _i32], C.c_int),
         "ficp_profile_report": ([_vp, C.c_char_p, _i64], C.c_int),
+        "ficp_path_stats": ([_vp, C.POINTER(C.c_int64)], C.c_int),
         "ficp_set_target": ([_vp, _dp, _i64, _i64, _i32], C.c_int),
         "ficp_set_target_device": ([_vp, _vp, _vp, _vp, _i64, _i32], C.c_int),
         "ficp_nn": ([_vp, _dp, _i64, _i64, _ip32, _dp], C.c_int),
@@ -252,6 +253,12 @@ class Context:
 
     def profile_enable(self, mask: int):
         _check(lib().ficp_profile_enable(self.h, int(mask)))
+
+    def path_stats(self) -> dict:
+        """Selection path counters (include/ficp.h ficp_path_stats)."""
+        out = (C.c_int64 * 4)()
+        _check(lib().ficp_path_stats(self.h, out))
+        return {"win_calls": out[0], "win_retries": out[1], "sel_levels": out[2], "sel_radix": out[3]}
 
     def profile_report(self) -> str:
         buf = C.create_string_buffer(1 << 16)

@@ -575,9 +575,20 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
                     false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from));
         return FICP_OK;
     };
-    auto enq_b = [&](int64_t i) -> int {
+    // the window path (k_sel_win, one launch instead of four) for the calls whose previous
+    // flag carried kFlagWinNext; FICP_SEL_WIN=0 turns it off
+    const char *wv = getenv("FICP_SEL_WIN");
+    const bool use_win = fused && fuse_fit && keys_from_r && !(wv && atoi(wv) == 0);
+    auto enq_b = [&](int64_t i, bool win) -> int {
         const int slot = (int)(i % kLoopRing);
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
+        if (win) {
+            ProfScope ps(c, P_SORT, "select");
+            HIPCHK(launch_select_win(c->r.as<double>(), worig, n, range_ptr(c),
+                                     nn_range_parts(n, c->m, use_grid(c, n)), c->sel_tmp.p, dst, lc,
+                                     &c->h_flags[slot], c->stream, fsrc, c->fault));
+            return FICP_OK;
+        }
         {
             ProfScope ps(c, P_SORT, "select");
             HIPCHK(launch_select(keys_from_r ? nullptr : c->key.as<unsigned long long>(), worig,
@@ -600,12 +611,14 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         }
         return FICP_OK;
     };
+    int flag_v = 0;  // the last flag read (fused): kFlagDone | kFlagWinNext, or kFlagRetry
     auto wait_flag = [&](int64_t i) -> int {
         const int old = (int)(i % kLoopRing);
         if (fused) {
             int v = 0;
             CHK(poll_flag(c, &c->h_flags[old], v));
-            finished = v != 0;
+            flag_v = v;
+            finished = (v & kFlagDone) != 0;
         } else {
             HIPCHK(hipEventSynchronize(c->loop_ev[old]));
             finished = c->h_flags[old] != 0;
@@ -617,16 +630,30 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         // for i's flag.  The device runs that fit + NN (>= 30 us) while the host wakes and
         // enqueues the next selection, and a finished run leaves two no-op launches
         // queued instead of a whole iteration's seven
+        // With the window path: a call whose previous flag allowed it takes k_sel_win; if
+        // that cannot decide (kFlagRetry: the NN launch behind it was a no-op), the full
+        // selection of the same call and the NN launch are enqueued again.
         if (!finished && cap > 0) CHK(enq_a(0));
+        bool win = false;
         for (; j < cap && !finished; ++j) {
-            CHK(enq_b(j));
+            CHK(enq_b(j, win));
             if (j + 1 < cap) CHK(enq_a(j + 1));
             CHK(wait_flag(j));
+            if (flag_v & kFlagRetry) {
+                c->win_retries += 1;
+                CHK(enq_b(j, false));
+                if (j + 1 < cap) CHK(enq_a(j + 1));
+                CHK(wait_flag(j));
+                if (flag_v & kFlagRetry) return fail(FICP_EHIP, "selection retry did not decide");
+            } else if (win) {
+                c->win_calls += 1;
+            }
+            win = use_win && (flag_v & kFlagWinNext) != 0;
         }
     } else {
         for (; j < cap && !finished; ++j) {
             CHK(enq_a(j));
-            CHK(enq_b(j));
+            CHK(enq_b(j, false));
             if (j >= la) CHK(wait_flag(j - la));
         }
     }
@@ -840,6 +867,16 @@ int ficp_set_nn_mode(ficp_ctx *c, int32_t mode) {
 int ficp_profile_enable(ficp_ctx *c, int32_t mask) {
     if (!c) return fail(FICP_EINVAL, "null context");
     c->prof_mask = mask;
+    return FICP_OK;
+}
+
+int ficp_path_stats(ficp_ctx *c, int64_t out[4]) {
+    CHK(check_ctx(c));
+    if (!out) return fail(FICP_EINVAL, "null out");
+    out[0] = c->win_calls;
+    out[1] = c->win_retries;
+    out[2] = (int64_t)c->sel_levels;
+    out[3] = (int64_t)c->sel_radix;
     return FICP_OK;
 }
 
@@ -1597,7 +1634,7 @@ int ficp_dist_wait(ficp_ctx *c, int64_t iteration, int32_t *done) {
     if (!c->dist_mode || !done || iteration < 0) return fail(FICP_EINVAL, "bad call");
     int v = 0;
     CHK(poll_flag(c, &c->h_flags[iteration % kLoopRing], v));
-    *done = v != 0;
+    *done = (v & kFlagDone) != 0;
     return FICP_OK;
 }
 

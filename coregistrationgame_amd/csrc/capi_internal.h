@@ -170,6 +170,7 @@ struct ficp_ctx {
     unsigned sel_init_gen = 0;  // sel_tmp allocation whose atomic words are initialised
     unsigned fit_init_gen = 0;  // fit_tmp allocation whose arrival counter is zeroed
     unsigned sel_levels = 0, sel_radix = 0;  // selection statistics (cumulative)
+    int64_t win_calls = 0, win_retries = 0;  // window-path fraction calls / fallbacks
     int *h_flags = nullptr;                        // pinned ring of per-iteration done flags
     unsigned *h_misc = nullptr;                    // pinned: sort flag, selection stats
     HostReport *h_rep = nullptr;                   // coherent pinned (report kernel)

@@ -346,8 +346,29 @@ struct alignas(16) IterState {
     // sizes the next call's fine bucket window (k_select.hip make_bmap)
     unsigned long long tmove;
     int n_reuse;           // NN calls answered by nn_reuse (ficp_stats::n_nn_reused)
-    int pad2;
+    int win_fail;          // the window path (k_sel_win) could not decide this call: it set
+                           // nn_reuse so the queued NN launch is a no-op, and the full
+                           // selection of the same call (k_sel_final) clears both
 };
+
+// The loop's done flag in pinned host memory (fused selection): bit 0 = the run is over;
+// bit 1 = the next call may take the window path (win_ok below); kFlagRetry (alone) = the
+// window path could not decide this call, the host enqueues the full selection for it.
+constexpr int kFlagDone = 1, kFlagWinNext = 2, kFlagRetry = 4;
+// window half-width 2^lh keys around the previous threshold key, lh = max(40, bits(tmove)
+// + 2) <= 43 (k_select.hip k_sel_win)
+constexpr int kWinHMinLog = 40, kWinHMaxLog = 43;
+__host__ __device__ __forceinline__ int win_lh(unsigned long long tmove) {
+    const int b = tmove ? 64 - __builtin_clzll(tmove) : 0;
+    return b + 2 > kWinHMinLog ? b + 2 : kWinHMinLog;
+}
+// the next fraction call may take the window path: a loop body of the same stage follows
+// one (so tkey and tmove come from loop-body calls), the threshold moved less than 2^41
+// keys, p = 2 lambda + 1 >= 1 (the bounds' quasi-concavity)
+__device__ __forceinline__ bool win_ok(const IterState &s) {
+    return s.phase == PH_LOOP && !s.done && s.it >= 1 && s.k > 0 && win_lh(s.tmove) <= kWinHMaxLog &&
+           2.0 * s.lam_cur + 1.0 >= 1.0;
+}
 
 // FRMSD(k) = (1 / (k/N)**lambda) * sqrt(S_k / k), in the reference's operation order
 // (ficp.py:59-60, 81)
@@ -717,9 +738,19 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
 // the selection's sticky error word inside its workspace (k_run_start resets it per run),
 // followed by its statistics words levels and radix (the report reads all three)
 unsigned *sel_err_word(void *tmp, int64_t n);
+// the window path (k_select.hip k_sel_win): one launch for a later loop-body call of a
+// stage (the host takes it when the previous call's flag had kFlagWinNext); on success the
+// same outputs as launch_select with loop and fit, on failure kFlagRetry (state unchanged
+// but win_fail / nn_reuse)
+hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
+                             const unsigned long long *range, int64_t range_parts, void *tmp,
+                             IterState *st, const LoopCtl &loop, int *host_flag, hipStream_t s,
+                             const FitSrc &fit, int fault = 0);
 // test-only fault injection (ficp_set_fault): block 0 of k_sel_bounds_gather publishes a
 // wrong token, so every gather block times out (ERR_SPIN)
 constexpr int FICP_FAULT_SPIN = 1;
+// test-only: k_sel_win reports kFlagRetry after doing its work (the fallback path)
+constexpr int FICP_FAULT_WIN = 2;
 
 // selection + fit + apply (k_select_fit.hip)
 int64_t frac_tmp_bytes(int64_t n);

@@ -98,6 +98,13 @@ constexpr int NSB_LOG = 11;
 constexpr int NS = 4096;     // sub-bins of one refinement level
 constexpr int NS_LOG = 12;
 constexpr int MAXLEV = 4;
+// window path (k_sel_win): rows a workgroup may hand over, coarse buckets per side of the
+// window (4 per octave of distance), record words per workgroup, arrival counter stride
+constexpr int WSLOT = 64;
+constexpr int NCS = 128;
+constexpr int NCB = 2 * NCS;
+constexpr int WREC = 16;
+constexpr int WCTR = 64;
 constexpr int SMALL_C = 160;  // final_small: above it the binned sort ranks faster (390: 5.8 vs 3.4 us)
 #ifndef FICP_GT
 #define FICP_GT 512
@@ -162,6 +169,14 @@ struct SelWS {
                      // empty)
     long long *sbcb; // [NB / 4] rows in the buckets before each run
     double *fpre;    // [SMALL_C][4] fused fit: the pair of pack slots < SMALL_C (gather)
+    // the window path (k_sel_win):
+    u64 *wrec;       // [gather blocks][WREC] each workgroup's record (sc1 stores)
+    u64 *wsk;        // [gather blocks][WSLOT] its window rows: key, r, caller index, work row
+    double *wsr;
+    uint32_t *wso, *wsp;
+    unsigned *gcc;   // [NCB] coarse bucket counts (agent-scope atomics; the last workgroup
+    u64 *gcf;        //   reads and zeroes them with exchanges) and fixed-point sums of r
+    unsigned *wctr;  // arrival counters: top + 8 groups, WCTR words apart (atomics only)
 };
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
@@ -231,6 +246,15 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.sblb = (double *)take(NB / 4 * 8);
     x.sbcb = (long long *)take(NB / 4 * 8);
     x.fpre = (double *)take(SMALL_C * 32);
+    const int64_t gbw = gather_blocks(n);
+    x.wrec = (u64 *)take(gbw * WREC * 8);
+    x.wsk = (u64 *)take(gbw * WSLOT * 8);
+    x.wsr = (double *)take(gbw * WSLOT * 8);
+    x.wso = (uint32_t *)take(gbw * WSLOT * 4);
+    x.wsp = (uint32_t *)take(gbw * WSLOT * 4);
+    x.gcc = (unsigned *)take(NCB * 4);
+    x.gcf = (u64 *)take(NCB * 8);
+    x.wctr = (unsigned *)take(9 * WCTR * 4);
     if (w) *w = x;
     return (int64_t)(p - p0) + 256;
 }
@@ -1515,7 +1539,7 @@ struct ScanOut {
 };
 
 // sort c <= CAPT candidates in LDS and scan them from (K0, S0): positions K0 + 1 .. K0 + c
-template <int CAPT, bool RL>
+template <int CAPT, bool RL, bool PRE = false>
 __device__ ScanOut lds_sort_scan(const Cand &src, unsigned c, long long K0, double S0,
                                  const FinalIn &in, unsigned char *sm, Scr &scr) {
     using LY = LdsLay<CAPT, RL>;
@@ -1529,11 +1553,14 @@ __device__ ScanOut lds_sort_scan(const Cand &src, unsigned c, long long K0, doub
     const int t = threadIdx.x;
     u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
     for (unsigned i = t; i < c; i += HT) {
-        const u64 k = src.k[i];
-        const uint32_t o = src.o[i];
-        lk[i] = k;
-        lo[i] = o;
-        if (RL) lr[i] = src.r[i];
+        // (PRE: the caller staged the candidates in LDS and passed a barrier)
+        const u64 k = PRE ? lk[i] : src.k[i];
+        const uint32_t o = PRE ? lo[i] : src.o[i];
+        if (!PRE) {
+            lk[i] = k;
+            lo[i] = o;
+            if (RL) lr[i] = src.r[i];
+        }
         kmn = k < kmn ? k : kmn;
         kmx = k > kmx ? k : kmx;
         omn = o < omn ? o : omn;
@@ -2332,6 +2359,12 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     }
     SELPROF(5);
     if (t == 0) {
+        // the window path could not decide this call (k_sel_win): the NN launch queued
+        // behind it was a no-op by nn_reuse, which the state machine restores here
+        if (s_st.win_fail) {
+            s_st.win_fail = 0;
+            s_st.nn_reuse = 0;
+        }
         if (fuse_loop) loop_step(&s_st, lc);
         // a sticky selection error (ERR_SPIN, ERR_CAP): this call's result is invalid, so
         // the device loop ends here and the host reports the flag (no further calls)
@@ -2346,7 +2379,8 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     __syncthreads();
     for (int q = t; q < SW; q += HT) ((uint32_t *)st)[q] = ((const uint32_t *)&s_st)[q];
     if (t == 0 && host_flag)
-        __hip_atomic_store(host_flag, s_st.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_flag, s_st.done | (win_ok(s_st) ? kFlagWinNext : 0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     SELPROF(6);
 #ifdef SEL_PROF
     // one line per 13 calls, in 10-ns ticks: bounds phases (block 0 of bounds_gather), the
@@ -2373,6 +2407,442 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 #endif
 }
 
+// ======================================================== window path (one launch)
+// A later loop-body call of a stage (win_ok: C3 from the sixth call on) moves the
+// threshold by a few to a few dozen rows, so one launch replaces hist / reduce / bounds +
+// gather / final (~47 us of four launches at C3):
+//  * every workgroup (HT threads x GI rows, the gather's shape) classifies its rows against
+//    the key window [wlo, whi) of half-width H = 2^win_lh(tmove) around the previous
+//    threshold key: a row below it is selected whatever k is, so it adds to the count,
+//    the fp64 sum of r (fixed tree) and the 8 fit sums; a row inside is handed over (key,
+//    r, caller index, work row; at most WSLOT per workgroup, in row order); every row
+//    outside adds to one of NCS coarse buckets per side, whose widths grow with the
+//    distance from the window (H/4 units: 1, 1, 1, 1, then 4 per octave), counted with
+//    exact fixed-point sums of r (LDS atomics, then agent-scope atomics into NCB words);
+//  * the last workgroup to arrive (k_fit_sums' two-level hand-off) sorts the window rows
+//    in LDS, scans them from (K0, S0) and takes the first FRMSD minimum inside the window,
+//    then proves it global as k_sel_bounds does: every non-empty coarse bucket's lower
+//    bound of h (block_lb: its rows are >= the bucket's lowest r) exceeds h at the
+//    minimum + kMarg.  A bucket's width is at most ~1/4 of its distance from the window,
+//    so its lower bound stays above the curve's rise there (fixed-width coarse buckets
+//    next to the window were ~1e-3 loose in h at the window edge, where the curve rises
+//    ~1e-7 above its minimum).  Then publish, the loop step, the fit of the next body
+//    (the rows below the window + the selected window rows, in a fixed order) and the
+//    host flag, as k_sel_final.
+//  * Anything unproven (a workgroup with > WSLOT window rows, > CAP in all, none, a
+//    non-finite r, a bound <= U): the launch leaves the state alone except win_fail and
+//    nn_reuse (the queued NN launch becomes a no-op) and stores kFlagRetry; the host
+//    then enqueues launch_select for the same call.  The result never depends on which
+//    path decided: both give the first minimum of the same exact curve (S sums differ in
+//    their last bits only: k is pinned where the curve separates by > 1e-9).
+struct WMap {
+    u64 kmin, kmax, wlo, whi;
+    int su;   // coarse unit 2^su keys (H / 4)
+    int fxs;  // fixed point: m = floor(r * 2^fxs), every finite r < 2^(62 - bits(n) - fxs)
+    int ok;
+};
+
+__device__ __forceinline__ WMap win_map(u64 kmin, u64 kmax, u64 c, u64 tmove, int64_t n) {
+    WMap m{};
+    m.kmin = kmin;
+    m.kmax = kmax;
+    const int lh = win_lh(tmove);
+    const u64 H = 1ULL << lh;
+    m.su = lh - 2;
+    m.wlo = (c > kmin && c - kmin > H) ? c - H : kmin;
+    m.whi = (kmax >= c && kmax - c >= H) ? c + H : kmax + 1ULL;
+    const int ex = (int)((kmax >> 52) & 0x7ffULL);  // d_max < 2^(ex - 1022): r < 2^(2 ex - 2044)
+    m.ok = (kmax >> 63) && ex < 0x7ff && kmax != ~0ULL && lh <= kWinHMaxLog;
+    m.fxs = (62 - bits_of((u64)max<int64_t>(n, 1))) - (2 * ex - 2044);
+    return m;
+}
+
+// coarse bucket of a distance of q units from the window edge (0..3: one unit each, then 4
+// per octave) and the smallest q of bucket j
+__device__ __forceinline__ int win_cq(u64 q) {
+    if (q < 4) return (int)q;
+    const int e = 63 - __clzll((long long)q);
+    return min(4 * (e - 1) + (int)((q >> (e - 2)) & 3ULL), NCS - 1);
+}
+__device__ __forceinline__ u64 win_cq_lo(int j) {
+    if (j < 4) return (u64)j;
+    return (u64)(4 + (j & 3)) << (j / 4 - 1);
+}
+
+// lowest key any row of coarse bucket b (key order: b < NCS below the window, NCS - 1 the
+// nearest; b >= NCS above it, NCS the nearest) can have
+__device__ __forceinline__ u64 win_bucket_lo(const WMap &m, int b) {
+    if (b < NCS) {
+        const int j = NCS - 1 - b;  // rows with (wlo - 1 - key) >> su in [lo(j), lo(j + 1))
+        if (j + 1 >= NCS) return m.kmin;
+        const u64 q = win_cq_lo(j + 1);
+        if (q >= (1ULL << (64 - m.su))) return m.kmin;
+        const u64 d = q << m.su;  // lowest key = wlo - d
+        return d >= m.wlo - m.kmin ? m.kmin : m.wlo - d;
+    }
+    const u64 q = win_cq_lo(b - NCS);
+    if (q >= (1ULL << (64 - m.su))) return m.kmax;
+    const u64 d = q << m.su;
+    return d > m.kmax - m.whi ? m.kmax : m.whi + d;
+}
+
+__device__ __forceinline__ void win_retry(IterState *st, int *host_flag) {
+    st->nn_reuse = 1;  // the NN launch queued behind this one keeps the current outputs
+    st->win_fail = 1;
+    if (host_flag) __hip_atomic_store(host_flag, kFlagRetry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// candidates staged in LDS for lds_sort_scan<CAP, true, true> + their work rows
+constexpr int W_ROW = LdsLay<CAP, true>::END;
+constexpr int W_SMEM = W_ROW + CAP * 4;
+static_assert(W_SMEM <= 132 * 1024, "window path LDS");
+
+#ifdef FICP_WIN_PROF
+__device__ unsigned long long g_winp[4];
+#define WINP_B(i)                                                         \
+    do {                                                                  \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_winp[i] = wall_clock64(); \
+    } while (0)
+#define WINP_T(i)                                 \
+    do {                                          \
+        __syncthreads();                          \
+        if (threadIdx.x == 0) wt_[i] = wall_clock64(); \
+    } while (0)
+#else
+#define WINP_B(i) \
+    do {          \
+    } while (0)
+#define WINP_T(i) \
+    do {          \
+    } while (0)
+#endif
+
+__global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t *orig, int64_t n,
+                                               const u64 *range, int64_t nparts, SelWS w,
+                                               IterState *st, LoopCtl lc, int *host_flag,
+                                               FitSrc fs, int force_retry) {
+    constexpr int WI = GI;  // rows per thread (stride HT)
+    static_assert(GT == HT, "k_sel_win: gather's workgroup shape");
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    __shared__ Scr scr;
+    __shared__ unsigned s_cc[NCB];
+    __shared__ u64 s_cf[NCB];
+    __shared__ double s_red[NWAVE][10];
+    __shared__ unsigned s_wc[NWAVE];
+    __shared__ int s_last;
+    WINP_B(0);
+    // every independent load first: the state's window inputs, the rows, the range parts
+    const int sk = st->done;
+    const int ph = st->phase, itv = st->it;
+    const long long kprev = st->k;
+    const u64 tkey = st->tkey, tmove = st->tmove;
+    const double lamv = st->lam_cur;
+    const int64_t base = (int64_t)blockIdx.x * (HT * WI) + t;
+    double rr[WI], xs[WI], ys[WI], xt[WI], yt[WI];
+    uint32_t oo[WI];
+#pragma unroll
+    for (int q = 0; q < WI; ++q) {
+        const int64_t i = base + (int64_t)q * HT;
+        const bool in = i < n;
+        rr[q] = in ? r[i] : 0.0;
+        oo[q] = in ? (orig ? orig[i] : (uint32_t)i) : 0u;
+        xs[q] = in ? fs.sx[i] : 0.0;
+        ys[q] = in ? fs.sy[i] : 0.0;
+        xt[q] = in ? fs.cx[i] : 0.0;
+        yt[q] = in ? fs.cy[i] : 0.0;
+    }
+    u64 ka = nparts > 0 ? 0ULL : range[0], kb = nparts > 0 ? 0ULL : range[1];  // (~kmin, kmax)
+    for (int64_t q0 = t; q0 < nparts; q0 += 4 * HT) {
+        ulonglong2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t q = q0 + (int64_t)u * HT;
+            v[u] = q < nparts ? *reinterpret_cast<const ulonglong2 *>(range + 2 + 2 * q)
+                              : ulonglong2{0ULL, 0ULL};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            ka = max(ka, v[u].x);
+            kb = max(kb, v[u].y);
+        }
+    }
+    if (sk) {  // the run is over: the flag as k_sel_final's no-op
+        if (blockIdx.x == 0 && t == 0 && host_flag)
+            __hip_atomic_store(host_flag, kFlagDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (t < NCB) {
+        s_cc[t] = 0u;
+        s_cf[t] = 0ULL;
+    }
+    ka = ~ka;
+    blk_minmax_u64(ka, kb, scr);  // (its barriers also cover the LDS zeroing)
+    const WMap m = win_map(ka, kb, tkey, tmove, n);
+    // (uniform over the launch: every workgroup decides the same way, none arrives)
+    if (!(ph == PH_LOOP && itv >= 1 && kprev > 0 && 2.0 * lamv + 1.0 >= 1.0 && m.ok)) {
+        if (blockIdx.x == 0 && t == 0) win_retry(st, host_flag);
+        return;
+    }
+    WINP_B(1);
+    // classify the rows
+    unsigned nbel = 0, nbad = 0;
+    double sb = 0.0;
+    double c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 kk[WI];
+    unsigned inw = 0;
+#pragma unroll
+    for (int q = 0; q < WI; ++q) {
+        const int64_t i = base + (int64_t)q * HT;
+        kk[q] = 0ULL;
+        if (i < n) {
+            const double v = rr[q];
+            if (!(v < INFINITY)) {  // inf / NaN: the full selection's special cases
+                ++nbad;
+                continue;
+            }
+            const u64 k = key_of_r(v);
+            kk[q] = k;
+            const u64 fx = (u64)ldexp(v, m.fxs);
+            if (k < m.wlo) {
+                ++nbel;
+                sb = sb + v;
+                fit_add(c8, xs[q], ys[q], xt[q], yt[q], fs.px, fs.py);
+                const int b = NCS - 1 - win_cq((m.wlo - 1ULL - k) >> m.su);
+                atomicAdd(&s_cc[b], 1u);
+                atomicAdd(&s_cf[b], fx);
+            } else if (k < m.whi) {
+                inw |= 1u << q;
+            } else {
+                const int b = NCS + win_cq((k - m.whi) >> m.su);
+                atomicAdd(&s_cc[b], 1u);
+                atomicAdd(&s_cf[b], fx);
+            }
+        }
+    }
+    // window rows handed over in row order (wave, then row slot, then lane): deterministic
+    u64 masks[WI];
+    unsigned wtot = 0;
+#pragma unroll
+    for (int q = 0; q < WI; ++q) {
+        masks[q] = __ballot((inw >> q) & 1u);
+        wtot += (unsigned)__popcll(masks[q]);
+    }
+    if (lane == 0) s_wc[wave] = wtot;
+    // the workgroup's sums (fixed trees: DPP wave sums, then the waves in order)
+    sb = wave_sum63(sb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) c8[e] = wave_sum63(c8[e]);
+    const u64 cnt = wave_sum63_u64((u64)nbel | ((u64)nbad << 32));
+    if (lane == 63) {
+        s_red[wave][0] = sb;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s_red[wave][1 + e] = c8[e];
+        s_red[wave][9] = __longlong_as_double((long long)cnt);
+    }
+    __syncthreads();  // (the LDS atomics, the wave counts and sums are complete)
+    unsigned wpos = 0, wall = 0;
+#pragma unroll
+    for (int q = 0; q < NWAVE; ++q) {
+        wpos += q < wave ? s_wc[q] : 0u;
+        wall += s_wc[q];
+    }
+    const int blk = blockIdx.x;
+    if (wtot && wall <= (unsigned)WSLOT) {
+        const u64 lt = (1ULL << lane) - 1ULL;
+#pragma unroll
+        for (int q = 0; q < WI; ++q) {
+            if ((inw >> q) & 1u) {
+                const int64_t slot = (int64_t)blk * WSLOT + wpos + (unsigned)__popcll(masks[q] & lt);
+                __hip_atomic_store(&w.wsk[slot], kk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&w.wsr[slot], rr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&w.wso[slot], oo[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&w.wsp[slot], (uint32_t)(base + (int64_t)q * HT), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            wpos += (unsigned)__popcll(masks[q]);
+        }
+    }
+    if (t < 10) {  // the record: count below, window rows, bad rows, sum of r, fit sums
+        double v = s_red[0][t];
+        u64 cv = (u64)__double_as_longlong(s_red[0][9]);
+        for (int q = 1; q < NWAVE; ++q) {
+            v = v + s_red[q][t];
+            cv += (u64)__double_as_longlong(s_red[q][9]);
+        }
+        u64 *rec = w.wrec + (int64_t)blk * WREC;
+        if (t == 9) {
+            const u64 bad = (cv >> 32) + (wall > (unsigned)WSLOT ? 1ULL : 0ULL);
+            __hip_atomic_store(&rec[0], cv & 0xffffffffULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rec[1], (u64)wall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rec[2], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&rec[3 + t], (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (t < NCB && s_cc[t]) {
+        __hip_atomic_fetch_add(&w.gcc[t], s_cc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&w.gcf[t], s_cf[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    WINP_B(2);
+    // hand-off (k_fit_sums' form): every storing wave waits for its stores and atomics,
+    // then one lane arrives at its group counter and the group's last at the top counter
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        const unsigned grp = blockIdx.x & 7u, ng = min(gridDim.x, 8u);
+        const unsigned gsz = (gridDim.x - grp + 7u) / 8u;
+        unsigned *gc = w.wctr + WCTR * (1 + grp);
+        bool last = false;
+        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
+            __hip_atomic_exchange(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = __hip_atomic_fetch_add(w.wctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+            if (last) __hip_atomic_exchange(w.wctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+
+    // ---- the last workgroup: the coarse buckets (read and zeroed), the records
+#ifdef FICP_WIN_PROF
+    unsigned long long wt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    WINP_T(0);
+    __shared__ __align__(16) unsigned char sm[W_SMEM];
+    __shared__ IterState s_st;
+    __shared__ double s_fit[8];
+    __shared__ u64 s_tko[2];
+    unsigned cc = 0;
+    u64 cf = 0;
+    if (t < NCB) {
+        cc = __hip_atomic_exchange(&w.gcc[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cf = __hip_atomic_exchange(&w.gcf[t], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    constexpr int SW = (int)(sizeof(IterState) / 4);
+    for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
+    if (t < 8) s_fit[t] = 0.0;
+    const int nwb = gridDim.x;
+    const int G = (nwb + HT - 1) / HT;  // this thread's records: [g0, g1) (in order)
+    const int g0 = min(nwb, t * G), g1 = min(nwb, g0 + G);
+    long long nb_t = 0, nw_t = 0, bad_t = 0;
+    double sb_t = 0.0, f8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int g = g0; g < g1; ++g) {
+        const u64 *rec = w.wrec + (int64_t)g * WREC;
+        u64 v[12];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) v[e] = __hip_atomic_load(&rec[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nb_t += (long long)v[0];
+        nw_t += (long long)v[1];
+        bad_t += (long long)v[2];
+        sb_t = sb_t + __longlong_as_double((long long)v[3]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f8[e] = f8[e] + __longlong_as_double((long long)v[4 + e]);
+    }
+    long long K0, Wt;
+    (void)blk_excl_scan_ll(nb_t, scr, K0);
+    long long woff = blk_excl_scan_ll(nw_t, scr, Wt);
+    const long long bad = blk_max_ll(bad_t, scr);
+    const double S0 = blk_sum(sb_t, scr);
+    blk_sum8_add(f8, s_fit, scr);
+    bool fail = bad != 0 || Wt <= 0 || Wt > CAP;
+    WINP_T(1);
+    // the window rows into LDS, in workgroup order (lds_sort_scan's layout + work rows)
+    using LY = LdsLay<CAP, true>;
+    u64 *lk = (u64 *)(sm + LY::K);
+    double *lr = (double *)(sm + LY::R);
+    uint32_t *lo = (uint32_t *)(sm + LY::O);
+    uint32_t *lrow = (uint32_t *)(sm + W_ROW);
+    if (!fail) {
+        for (int g = g0; g < g1; ++g) {
+            const int cnt = (int)__hip_atomic_load(&w.wrec[(int64_t)g * WREC + 1], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+            for (int j = 0; j < cnt; ++j) {
+                const int64_t sl = (int64_t)g * WSLOT + j;
+                lk[woff + j] = __hip_atomic_load(&w.wsk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lr[woff + j] = __hip_atomic_load(&w.wsr[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lo[woff + j] = __hip_atomic_load(&w.wso[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lrow[woff + j] = __hip_atomic_load(&w.wsp[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            woff += cnt;
+        }
+    }
+    __syncthreads();
+    WINP_T(2);
+    const double lam = lamv;
+    const double p = 2.0 * lam + 1.0;
+    FinalIn in;
+    in.N = n;
+    in.lam = lam;
+    in.S0 = S0;
+    in.K0 = K0;
+    in.U = 0.0;
+    in.fs = fs;
+    in.fsum = s_fit;
+    ScanOut rs{INFINITY, 0x7fffffffffffffffLL, 0, 0, 0.0};
+    if (!fail) {
+        const Cand none{nullptr, nullptr, nullptr, nullptr};
+        rs = lds_sort_scan<CAP, true, true>(none, (unsigned)Wt, K0, S0, in, sm, scr);
+        fail = rs.bk == 0x7fffffffffffffffLL;
+    }
+    WINP_T(3);
+    // the minimum is global: every coarse bucket's lower bound of h exceeds U
+    double U = INFINITY;
+    if (!fail) {
+        U = h_of(rs.bk, S0 + lr[rs.bk - K0 - 1], p) + kMarg;  // (lr: prefix sums by position)
+        if (t == 0) {
+            s_tko[0] = rs.tk;
+            s_tko[1] = (u64)rs.to;
+        }
+    }
+    const double unit = ldexp(1.0, -m.fxs);
+    long long C0 = t < NCB ? (long long)cc : 0;
+    double Pb = (t < NCS) ? (double)cf * unit : 0.0;
+    double Pa = (t >= NCS && t < NCB) ? (double)cf * unit : 0.0;
+    blk_excl_scan3(C0, Pb, Pa, scr);  // (its barriers publish s_tko)
+    bool ok = true;
+    if (!fail && t < NCB) {
+        if (t == NCS - 1 && C0 + (long long)cc != K0) ok = false;  // (a row lost: never)
+        if (cc) {
+            const long long c0 = t < NCS ? C0 : C0 + Wt;  // (C0 counts every row below the window)
+            const double P0 = t < NCS ? Pb : (S0 + rs.total) + Pa;
+            const double lb = block_lb(c0, (long long)cc, P0, lo_r(win_bucket_lo(m, t)), p);
+            ok = lb > U;
+        }
+    }
+    fail = fail || blk_max_ll(ok ? 0 : 1, scr) != 0 || force_retry;
+    WINP_T(4);
+#ifdef FICP_WIN_PROF
+    if (t == 0)
+        printf("WINPROF W=%lld K0=%lld fail=%d | b0 load %llu pass %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu (10 ns)\n",
+               Wt, K0, (int)fail, g_winp[1] - g_winp[0], g_winp[2] - g_winp[1], wt_[0] - g_winp[2],
+               wt_[1] - wt_[0], wt_[2] - wt_[1], wt_[3] - wt_[2], wt_[4] - wt_[3]);
+#endif
+    if (fail) {
+        if (t == 0) win_retry(st, host_flag);
+        return;
+    }
+    // the fit of the selected window rows, candidate order (deterministic)
+    const u64 tk = s_tko[0];
+    const uint32_t to = (uint32_t)s_tko[1];
+    double cf8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (fs.on)
+        for (int e = t; e < (int)Wt; e += HT)
+            if (!less_ko(tk, to, lk[e], lo[e])) fit_row(cf8, fs, lrow[e]);
+    if (fs.on) blk_sum8_add(cf8, s_fit, scr);
+    if (t == 0) {
+        publish(&s_st, in, rs.bf, rs.bk, tk, to);
+        loop_step(&s_st, lc);
+        if (fs.on && !s_st.no_fit && s_st.k > 0)
+            fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
+    }
+    __syncthreads();
+    for (int q = t; q < SW; q += HT) ((uint32_t *)st)[q] = ((const uint32_t *)&s_st)[q];
+    if (t == 0 && host_flag)
+        __hip_atomic_store(host_flag, s_st.done | (win_ok(s_st) ? kFlagWinNext : 0),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void k_sel_init(SelWS w) {
     if (threadIdx.x == 0) {
         __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2381,6 +2851,13 @@ __global__ void k_sel_init(SelWS w) {
         w.ctl->radix = 0;
         __hip_atomic_store(&w.ctl->bpub, (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // the window path's coarse buckets and arrival counters
+    for (int b = threadIdx.x; b < NCB; b += blockDim.x) {
+        __hip_atomic_exchange(&w.gcc[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_exchange(&w.gcf[b], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int b = threadIdx.x; b < 9 * WCTR; b += blockDim.x)
+        __hip_atomic_exchange(&w.wctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- distributed selection (source rows split over ranks) -------
@@ -2496,6 +2973,17 @@ hipError_t launch_select_dist_final(const long long *packs, int world, int capd,
     if (loop) lc = *loop;
     hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, world, n_total, lam, lam_dev, st,
                        skip, lc, loop ? 1 : 0, host_flag, FitSrc{}, std::max<int64_t>(n_ws, 1));
+    return hipGetLastError();
+}
+
+hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
+                             const unsigned long long *range, int64_t range_parts, void *tmp,
+                             IterState *st, const LoopCtl &loop, int *host_flag, hipStream_t s,
+                             const FitSrc &fit, int fault) {
+    if (n <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_sel_win, dim3(gather_blocks(n)), dim3(HT), 0, s, r, orig, n, range,
+                       range_parts, carve(tmp, n), st, loop, host_flag, fit,
+                       (fault & FICP_FAULT_WIN) ? 1 : 0);
     return hipGetLastError();
 }
 

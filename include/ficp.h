@@ -77,13 +77,21 @@ void ficp_destroy(ficp_ctx *ctx);
 int ficp_set_nn_mode(ficp_ctx *ctx, int32_t mode);
 /* Test-only fault injection (no reference counterpart): mask 1 makes the selection's
    bounds hand-off never arrive, so the run must fail with the ERR_SPIN flag (4) instead of
-   hanging or writing out of bounds.  0 = off (the default). */
+   hanging or writing out of bounds; mask 2 makes every window-path fraction call report
+   that it could not decide, so the run takes the full selection for each of them (the
+   fallback's test).  0 = off (the default). */
 int ficp_set_fault(ficp_ctx *ctx, int32_t mask);
 /* Kernel timing with HIP events on the context stream: mask bit per kernel class
    (1 = nn, 2 = sort, 4 = scan/fraction, 8 = fit, 16 = grid build); 0 = off. */
 int ficp_profile_enable(ficp_ctx *ctx, int32_t mask);
 /* JSON {"kernel": {"count": c, "ms": total}, ...} of the timings so far; resets them. */
 int ficp_profile_report(ficp_ctx *ctx, char *buf, int64_t buflen);
+/* Selection path counters of this context since its creation (no reference counterpart;
+   diagnostics of find_optimal_fraction, ficp.py:73-86, inside ficp_run): out[0] = fraction
+   calls decided by the one-launch window path, out[1] = window-path calls that fell back to
+   the full bucketed selection, out[2] = refinement levels, out[3] = radix fallbacks (the
+   last two: the last run). */
+int ficp_path_stats(ficp_ctx *ctx, int64_t out[4]);
 
 /* --- static CHM layer (target) ----------------------------------------- */
 /* Replaces the per-call cKDTree(target) of ficp.py:69: uploads the target once and

@@ -190,7 +190,7 @@ int ensure_fit(ficp_ctx *c, int64_t n) {
 int ensure_work(ficp_ctx *c, int64_t n) {
     CHK(c->idx.ensure(n * 4));
     CHK(c->dist.ensure(n * 8));
-    CHK(c->r.ensure(n * 8));
+    CHK(c->r.ensure((n + 1) * 8));  // (+1: k_sel_win's 16-B row-pair loads)
     CHK(c->key.ensure(n * 8));
     CHK(c->val.ensure(n * 4));
     CHK(c->order.ensure(n * 4));
@@ -198,8 +198,8 @@ int ensure_work(ficp_ctx *c, int64_t n) {
     CHK(c->frac_tmp.ensure(frac_tmp_bytes(n)));
     CHK(ensure_fit(c, n));
     CHK(c->state_dev.ensure(sizeof(IterState)));
-    CHK(c->ccx.ensure(n * 8));
-    CHK(c->ccy.ensure(n * 8));
+    CHK(c->ccx.ensure((n + 1) * 8));
+    CHK(c->ccy.ensure((n + 1) * 8));
     CHK(c->rs.ensure(n * 8));
     CHK(c->range.ensure(range_words(n) * 8));
     CHK(c->sel_tmp.ensure(sel_tmp_bytes(n)));
@@ -220,8 +220,12 @@ unsigned long long *range_ptr(ficp_ctx *c) { return c->range.as<unsigned long lo
 int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, const double *T,
             bool want_keys, int warm = 0, const int *skip = nullptr,
             const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true,
-            const int *reuse = nullptr, bool store_key = true, bool multi = false) {
+            const int *reuse = nullptr, bool store_key = true, bool multi = false,
+            const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr) {
     NNArgs a{};
+    a.fin_orig = fin_orig;
+    a.fin_x = fin_x;
+    a.fin_y = fin_y;
     a.sx = sx;
     a.sy = sy;
     a.sz = sz;
@@ -308,10 +312,10 @@ int read_state(ficp_ctx *c) {
 // job: as in ensure_grid (the bucket-sort path returns its job instead of launching)
 int build_work_order(ficp_ctx *c, const double *sx, const double *sy, const double *sz,
                      int64_t n, BSJob *job = nullptr) {
-    CHK(c->wx.ensure(n * 8));
-    CHK(c->wy.ensure(n * 8));
+    CHK(c->wx.ensure((n + 1) * 8));  // (+1: k_sel_win's 16-B row-pair loads)
+    CHK(c->wy.ensure((n + 1) * 8));
     if (sz) CHK(c->wz.ensure(n * 8));
-    CHK(c->worig.ensure(n * 4));
+    CHK(c->worig.ensure((n + 1) * 4));
     ProfScope ps(c, P_MISC, "work_order");
     const GridView &g = c->gv;
     const int64_t nkeys = (int64_t)((g.gx + 7) / 8) * (int64_t)((g.gy + 7) / 8) * 64;
@@ -565,20 +569,25 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     const int64_t nn_multi_from = qf ? atoll(qf) : nn_qpt_from();
     // part A of iteration i: the fit and the NN call; part B: the selection (and, not
     // fused, the loop step and the flag copy)
+    int64_t last_a = -1;  // the last iteration whose fit + NN were enqueued
     auto enq_a = [&](int64_t i) -> int {
         if (!(fused && fuse_fit)) {
             ProfScope ps(c, P_FIT, "fit");
             HIPCHK(launch_fit(fa, allow_refl, c->fit_tmp.p, dst, &dst->no_fit, c->stream));
         }
         // (a later stage's head reuses the previous call's outputs: dst->nn_reuse)
+        // (a launch queued behind the loop's end writes the caller-order XY: fin_*)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
-                    false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from));
+                    false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from,
+                    worig, sx, sy));
+        last_a = i;
         return FICP_OK;
     };
     // the window path (k_sel_win, one launch instead of four) for the calls whose previous
     // flag carried kFlagWinNext; FICP_SEL_WIN=0 turns it off
     const char *wv = getenv("FICP_SEL_WIN");
-    const bool use_win = fused && fuse_fit && keys_from_r && !(wv && atoi(wv) == 0);
+    // (the work-order arrays: library buffers, 16-B aligned for the window pass's loads)
+    const bool use_win = fused && fuse_fit && keys_from_r && worig && !(wv && atoi(wv) == 0);
     auto enq_b = [&](int64_t i, bool win) -> int {
         const int slot = (int)(i % kLoopRing);
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
@@ -612,6 +621,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         return FICP_OK;
     };
     int flag_v = 0;  // the last flag read (fused): kFlagDone | kFlagWinNext, or kFlagRetry
+    int64_t fin_j = INT64_MAX;  // the call whose flag ended the loop
     auto wait_flag = [&](int64_t i) -> int {
         const int old = (int)(i % kLoopRing);
         if (fused) {
@@ -623,6 +633,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             HIPCHK(hipEventSynchronize(c->loop_ev[old]));
             finished = c->h_flags[old] != 0;
         }
+        if (finished) fin_j = i;
         return FICP_OK;
     };
     if (fused && la == 1) {
@@ -660,7 +671,9 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // one host round trip for everything the run reports: the caller-order XY, the loop
     // state, the sort's timeout flag and the selection's statistics (each separate sync
     // cost ~40 us of idle device at C3)
-    if (worig) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
+    // the caller-order XY: written by an NN launch queued behind the loop's last call
+    // (fin_scatter: it found the done flag), else here
+    if (worig && !(last_a > fin_j)) HIPCHK(launch_scatter_xy(worig, wx, wy, n, sx, sy, c->stream));
     c->h_rep->misc[1] = c->h_rep->misc[2] = c->h_rep->misc[3] = 0u;
     CHK(report_wait(c, ReportSeg{c->state_dev.p, &c->h_rep->st, (int)(sizeof(IterState) / 4)},
                     ReportSeg{tflag, &c->h_rep->misc[0], 1},

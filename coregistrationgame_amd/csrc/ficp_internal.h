@@ -308,7 +308,24 @@ struct NNArgs {
     const int *apply_flag;      // T is applied only while *apply_flag != 0 (nullable: always)
     const int *reuse;           // grid kernel: a no-op while *reuse != 0 -- the source has not
                                 // moved since the previous call, whose outputs stand (nullable)
+    // grid kernels, run loop: a launch that finds *skip set (the loop ended before it: the
+    // launch queued behind the last selection) writes the caller-order XY instead,
+    // fin_x[fin_orig[p]] = sx[p] (k_scatter_xy's work, no launch or host round trip of its own)
+    const uint32_t *fin_orig;
+    double *fin_x, *fin_y;
 };
+
+// k_scatter_xy's work for rows [p0, p0 + cnt) of the work order
+__device__ __forceinline__ void fin_scatter(const NNArgs &a, int64_t p0, int cnt) {
+    for (int q = threadIdx.x; q < cnt; q += blockDim.x) {
+        const int64_t p = p0 + q;
+        if (p < a.n) {
+            const uint32_t i = a.fin_orig[p];
+            a.fin_x[i] = a.sx[p];
+            a.fin_y[i] = a.sy[p];
+        }
+    }
+}
 
 // Device-resident state of one ICP stage (written by kernels, read back per iteration).
 enum PlotPhase { PH_HEAD = 0, PH_LOOP = 1, PH_DONE = 2 };
@@ -349,6 +366,9 @@ struct alignas(16) IterState {
     int win_fail;          // the window path (k_sel_win) could not decide this call: it set
                            // nn_reuse so the queued NN launch is a no-op, and the full
                            // selection of the same call (k_sel_final) clears both
+    int wfloor;            // log2 of the window path's smallest half-width (keys): adapted
+                           // by each window call to keep its window at ~48-384 rows
+    int pad3;
 };
 
 // The loop's done flag in pinned host memory (fused selection): bit 0 = the run is over;
@@ -357,17 +377,21 @@ struct alignas(16) IterState {
 constexpr int kFlagDone = 1, kFlagWinNext = 2, kFlagRetry = 4;
 // window half-width 2^lh keys around the previous threshold key, lh = max(40, bits(tmove)
 // + 2) <= 43 (k_select.hip k_sel_win)
-constexpr int kWinHMinLog = 40, kWinHMaxLog = 43;
-__host__ __device__ __forceinline__ int win_lh(unsigned long long tmove) {
+// lh = max(wfloor, bits(tmove) + 1): at least twice the last move (C3's moves shrink
+// ~3-10x per call); wfloor starts at 2^40 (C3 stage 1: ~40-160 rows) and follows the
+// window's row count (stage 2's density put ~1,000 rows into 2^40)
+constexpr int kWinHMinLog = 36, kWinHStartLog = 40, kWinHMaxLog = 44;
+__host__ __device__ __forceinline__ int win_lh(unsigned long long tmove, int wfloor) {
     const int b = tmove ? 64 - __builtin_clzll(tmove) : 0;
-    return b + 2 > kWinHMinLog ? b + 2 : kWinHMinLog;
+    return b + 1 > wfloor ? b + 1 : wfloor;
 }
-// the next fraction call may take the window path: a loop body of the same stage follows
-// one (so tkey and tmove come from loop-body calls), the threshold moved less than 2^41
-// keys, p = 2 lambda + 1 >= 1 (the bounds' quasi-concavity)
+// the next fraction call may take the window path: a loop body follows a loop body of the
+// same stage (tkey and tmove from loop-body calls; a stage's first body moves far: C3 4,228
+// rows in stage 1, and stage 2's 73 rows put its minimum at the 2^40 window's edge), the
+// threshold moved less than 2^43 keys, p = 2 lambda + 1 >= 1 (the bounds' quasi-concavity)
 __device__ __forceinline__ bool win_ok(const IterState &s) {
-    return s.phase == PH_LOOP && !s.done && s.it >= 1 && s.k > 0 && win_lh(s.tmove) <= kWinHMaxLog &&
-           2.0 * s.lam_cur + 1.0 >= 1.0;
+    return s.phase == PH_LOOP && !s.done && s.it >= 1 && s.k > 0 &&
+           win_lh(s.tmove, s.wfloor) <= kWinHMaxLog && 2.0 * s.lam_cur + 1.0 >= 1.0;
 }
 
 // FRMSD(k) = (1 / (k/N)**lambda) * sqrt(S_k / k), in the reference's operation order

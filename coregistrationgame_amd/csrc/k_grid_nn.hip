@@ -914,6 +914,7 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g)
     // the three flags load together (the apply flag's load used to wait for the other two)
     const int sk = a.skip ? *a.skip : 0, ru = a.reuse ? *a.reuse : 0;
     const int ap = (APPLY && a.apply_flag) ? *a.apply_flag : 1;
+    if (sk && a.fin_orig) fin_scatter(a, (int64_t)blockIdx.x * (256 * Q), 256 * Q);
     if (sk || ru) return;
     const int t = threadIdx.x;
     const int64_t i0 = xcd_block(blockIdx.x, gridDim.x) * (256 * Q);
@@ -1013,6 +1014,7 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
     // the three flags load together (the apply flag's load used to wait for the other two)
     const int sk = a.skip ? *a.skip : 0, ru = a.reuse ? *a.reuse : 0;
     const int ap = (APPLY && a.apply_flag) ? *a.apply_flag : 1;
+    if (sk && a.fin_orig) fin_scatter(a, (int64_t)blockIdx.x * blockDim.x, (int)blockDim.x);
     if (sk || ru) return;
     const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     unsigned long long kmin_c = 0, kmax = 0;

@@ -2412,7 +2412,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 // threshold by a few to a few dozen rows, so one launch replaces hist / reduce / bounds +
 // gather / final (~47 us of four launches at C3):
 //  * every workgroup (HT threads x GI rows, the gather's shape) classifies its rows against
-//    the key window [wlo, whi) of half-width H = 2^win_lh(tmove) around the previous
+//    the key window [wlo, whi) of half-width H = 2^win_lh(tmove, wfloor) around the previous
 //    threshold key: a row below it is selected whatever k is, so it adds to the count,
 //    the fp64 sum of r (fixed tree) and the 8 fit sums; a row inside is handed over (key,
 //    r, caller index, work row; at most WSLOT per workgroup, in row order); every row
@@ -2442,11 +2442,12 @@ struct WMap {
     int ok;
 };
 
-__device__ __forceinline__ WMap win_map(u64 kmin, u64 kmax, u64 c, u64 tmove, int64_t n) {
+__device__ __forceinline__ WMap win_map(u64 kmin, u64 kmax, u64 c, u64 tmove, int wfloor,
+                                        int64_t n) {
     WMap m{};
     m.kmin = kmin;
     m.kmax = kmax;
-    const int lh = win_lh(tmove);
+    const int lh = win_lh(tmove, wfloor);
     const u64 H = 1ULL << lh;
     m.su = lh - 2;
     m.wlo = (c > kmin && c - kmin > H) ? c - H : kmin;
@@ -2492,13 +2493,59 @@ __device__ __forceinline__ void win_retry(IterState *st, int *host_flag) {
     if (host_flag) __hip_atomic_store(host_flag, kFlagRetry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// c <= SMALL_C window rows (the normal case: tens): one row per thread, ranked
+// by (key, orig) against all of them (LDS broadcast reads), one block scan in sorted order,
+// FRMSD of every position, first minimum (final_small's arithmetic, on rows already in
+// LDS).  s_aux receives S at the minimum and its threshold pair.
+__device__ ScanOut win_scan_small(unsigned c, const FinalIn &in, const u64 *lk, const uint32_t *lo,
+                                  const double *lr, uint16_t *pos, Scr &scr, u64 *s_aux) {
+    const unsigned t = threadIdx.x;
+    if (t < c) {
+        const u64 k = lk[t];
+        const uint32_t o = lo[t];
+        unsigned rank = 0;
+        for (unsigned j = 0; j < c; ++j) rank += less_ko(lk[j], lo[j], k, o) ? 1u : 0u;
+        pos[rank] = (uint16_t)t;
+    }
+    __syncthreads();
+    const unsigned e = t < c ? pos[t] : 0u;
+    const double v = t < c ? lr[e] : 0.0;
+    double all;
+    const double ex = blk_excl_scan_d(v, scr, all);
+    const double S = in.S0 + (ex + v);
+    double bf = INFINITY;
+    long long bk = 0x7fffffffffffffffLL;
+    if (t < c) {
+        const long long kk = in.K0 + (long long)t + 1;
+        const double f = frmsd_of(kk, in.N, S, in.lam);
+        if (f < bf) {
+            bf = f;
+            bk = kk;
+        }
+    }
+    blk_argmin(bf, bk, scr);
+    if (t < c && in.K0 + (long long)t + 1 == bk) {
+        s_aux[0] = (u64)__double_as_longlong(S);
+        s_aux[1] = lk[e];
+        s_aux[2] = (u64)lo[e];
+    }
+    __syncthreads();
+    ScanOut r{bf, bk, 0, 0, all};
+    if (bk != 0x7fffffffffffffffLL) {
+        r.tk = s_aux[1];
+        r.to = (uint32_t)s_aux[2];
+    }
+    return r;
+}
+
 // candidates staged in LDS for lds_sort_scan<CAP, true, true> + their work rows
 constexpr int W_ROW = LdsLay<CAP, true>::END;
+constexpr int W_MAXWG = 2 * NSB - 1;  // workgroups of one launch (8M rows: 1954)
 constexpr int W_SMEM = W_ROW + CAP * 4;
 static_assert(W_SMEM <= 132 * 1024, "window path LDS");
 
 #ifdef FICP_WIN_PROF
-__device__ unsigned long long g_winp[4];
+__device__ unsigned long long g_winp[8];
 #define WINP_B(i)                                                         \
     do {                                                                  \
         if (blockIdx.x == 0 && threadIdx.x == 0) g_winp[i] = wall_clock64(); \
@@ -2525,59 +2572,100 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     static_assert(GT == HT, "k_sel_win: gather's workgroup shape");
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     __shared__ Scr scr;
-    __shared__ unsigned s_cc[NCB];
-    __shared__ u64 s_cf[NCB];
-    __shared__ double s_red[NWAVE][10];
+    // coarse buckets in LDS, WREP copies by lane % WREP (most rows of a wave fall into a
+    // few coarse buckets: one copy serialised up to 64 lanes per atomic), rows padded so
+    // that a bucket's copies sit in different banks
+    constexpr int WREP = 8, WRS = NCB + 1;
+    __shared__ unsigned s_cc[WREP * WRS];
+    __shared__ u64 s_cf[WREP * WRS];
+    __shared__ double s_red[NWAVE][11];
     __shared__ unsigned s_wc[NWAVE];
     __shared__ int s_last;
     WINP_B(0);
     // every independent load first: the state's window inputs, the rows, the range parts
     const int sk = st->done;
-    const int ph = st->phase, itv = st->it;
+    const int ph = st->phase, itv = st->it, wfl = st->wfloor;
     const long long kprev = st->k;
     const u64 tkey = st->tkey, tmove = st->tmove;
     const double lamv = st->lam_cur;
-    const int64_t base = (int64_t)blockIdx.x * (HT * WI) + t;
+    // the range parts issue first (PU per thread: the NN's 3,907 parts at 1M rows) and are
+    // reduced after the rows' loads have issued: the reduction waits for them alone
+    constexpr int PU = 8;
+    u64 ka = nparts > 0 ? 0ULL : range[0], kb = nparts > 0 ? 0ULL : range[1];  // (~kmin, kmax)
+    // (every load unconditional, its index clamped: a branch around a load made the
+    // compiler wait for it at the join, which serialised every load of this kernel)
+    ulonglong2 pv[PU];
+    const int64_t plast = max<int64_t>(nparts - 1, 0);
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+        const int64_t q = min<int64_t>(t + (int64_t)u * HT, plast);  // (a repeat: max unchanged)
+        pv[u] = *reinterpret_cast<const ulonglong2 *>(range + 2 + 2 * q);
+    }
+    // row q of this thread: pairs of consecutive rows per lane, so that every load is 16 B
+    // (8-B lanes stream at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md)
+    const int64_t base = (int64_t)blockIdx.x * (HT * WI) + 2 * t;
+    auto row_of = [&](int q) -> int64_t { return base + (int64_t)(q >> 1) * (2 * HT) + (q & 1); };
     double rr[WI], xs[WI], ys[WI], xt[WI], yt[WI];
     uint32_t oo[WI];
 #pragma unroll
-    for (int q = 0; q < WI; ++q) {
-        const int64_t i = base + (int64_t)q * HT;
-        const bool in = i < n;
-        rr[q] = in ? r[i] : 0.0;
-        oo[q] = in ? (orig ? orig[i] : (uint32_t)i) : 0u;
-        xs[q] = in ? fs.sx[i] : 0.0;
-        ys[q] = in ? fs.sy[i] : 0.0;
-        xt[q] = in ? fs.cx[i] : 0.0;
-        yt[q] = in ? fs.cy[i] : 0.0;
+    for (int q = 0; q < WI; q += 2) {
+        // (i is even; the buffers hold n + 1 rows, so the pair of row n - 1 is readable; a
+        // pair at or past n reads pair 0, whose values the row tests below ignore)
+        const int64_t i = row_of(q) < n ? row_of(q) : 0;
+        const double2 a = *reinterpret_cast<const double2 *>(r + i);
+        const double2 b = *reinterpret_cast<const double2 *>(fs.sx + i);
+        const double2 c = *reinterpret_cast<const double2 *>(fs.sy + i);
+        const double2 d = *reinterpret_cast<const double2 *>(fs.cx + i);
+        const double2 e = *reinterpret_cast<const double2 *>(fs.cy + i);
+        const uint2 o = *reinterpret_cast<const uint2 *>(orig + i);
+        rr[q] = a.x, rr[q + 1] = a.y;
+        xs[q] = b.x, xs[q + 1] = b.y;
+        ys[q] = c.x, ys[q + 1] = c.y;
+        xt[q] = d.x, xt[q + 1] = d.y;
+        yt[q] = e.x, yt[q + 1] = e.y;
+        oo[q] = o.x, oo[q + 1] = o.y;
     }
-    u64 ka = nparts > 0 ? 0ULL : range[0], kb = nparts > 0 ? 0ULL : range[1];  // (~kmin, kmax)
-    for (int64_t q0 = t; q0 < nparts; q0 += 4 * HT) {
-        ulonglong2 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t q = q0 + (int64_t)u * HT;
-            v[u] = q < nparts ? *reinterpret_cast<const ulonglong2 *>(range + 2 + 2 * q)
-                              : ulonglong2{0ULL, 0ULL};
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            ka = max(ka, v[u].x);
-            kb = max(kb, v[u].y);
-        }
+    for (int u = 0; u < PU; ++u) {
+        ka = max(ka, pv[u].x);
+        kb = max(kb, pv[u].y);
+    }
+    for (int64_t q = t + (int64_t)PU * HT; q < nparts; q += HT) {  // (more than PU x HT parts)
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(range + 2 + 2 * q);
+        ka = max(ka, v.x);
+        kb = max(kb, v.y);
     }
     if (sk) {  // the run is over: the flag as k_sel_final's no-op
         if (blockIdx.x == 0 && t == 0 && host_flag)
             __hip_atomic_store(host_flag, kFlagDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
-    if (t < NCB) {
-        s_cc[t] = 0u;
-        s_cf[t] = 0ULL;
+    for (int b = t; b < WREP * WRS; b += HT) {
+        s_cc[b] = 0u;
+        s_cf[b] = 0ULL;
     }
-    ka = ~ka;
-    blk_minmax_u64(ka, kb, scr);  // (its barriers also cover the LDS zeroing)
-    const WMap m = win_map(ka, kb, tkey, tmove, n);
+    {
+        // block max of (~kmin, kmax) with an LDS-only barrier: __syncthreads() would also
+        // wait for every row's load (vmcnt(0)); this way the rows are classified as their
+        // loads land
+#define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+        wave_range_reduce(ka, kb);
+        if (lane == 63) {
+            scr.u[wave] = ka;
+            scr.v[wave] = kb;
+        }
+        LDS_BARRIER();
+        u64 a = scr.u[0], b = scr.v[0];
+#pragma unroll
+        for (int q = 1; q < NWAVE; ++q) {
+            a = max(a, scr.u[q]);
+            b = max(b, scr.v[q]);
+        }
+        ka = ~a;
+        kb = b;
+#undef LDS_BARRIER
+    }
+    const WMap m = win_map(ka, kb, tkey, tmove, wfl, n);
     // (uniform over the launch: every workgroup decides the same way, none arrives)
     if (!(ph == PH_LOOP && itv >= 1 && kprev > 0 && 2.0 * lamv + 1.0 >= 1.0 && m.ok)) {
         if (blockIdx.x == 0 && t == 0) win_retry(st, host_flag);
@@ -2586,13 +2674,15 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     WINP_B(1);
     // classify the rows
     unsigned nbel = 0, nbad = 0;
-    double sb = 0.0;
+    double sb = 0.0, swn = 0.0;
     double c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     u64 kk[WI];
     unsigned inw = 0;
+    unsigned *my_cc = s_cc + (lane % WREP) * WRS;
+    u64 *my_cf = s_cf + (lane % WREP) * WRS;
 #pragma unroll
     for (int q = 0; q < WI; ++q) {
-        const int64_t i = base + (int64_t)q * HT;
+        const int64_t i = row_of(q);
         kk[q] = 0ULL;
         if (i < n) {
             const double v = rr[q];
@@ -2608,17 +2698,19 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
                 sb = sb + v;
                 fit_add(c8, xs[q], ys[q], xt[q], yt[q], fs.px, fs.py);
                 const int b = NCS - 1 - win_cq((m.wlo - 1ULL - k) >> m.su);
-                atomicAdd(&s_cc[b], 1u);
-                atomicAdd(&s_cf[b], fx);
+                atomicAdd(&my_cc[b], 1u);
+                atomicAdd(&my_cf[b], fx);
             } else if (k < m.whi) {
                 inw |= 1u << q;
+                swn = swn + v;
             } else {
                 const int b = NCS + win_cq((k - m.whi) >> m.su);
-                atomicAdd(&s_cc[b], 1u);
-                atomicAdd(&s_cf[b], fx);
+                atomicAdd(&my_cc[b], 1u);
+                atomicAdd(&my_cf[b], fx);
             }
         }
     }
+    WINP_B(3);
     // window rows handed over in row order (wave, then row slot, then lane): deterministic
     u64 masks[WI];
     unsigned wtot = 0;
@@ -2630,6 +2722,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     if (lane == 0) s_wc[wave] = wtot;
     // the workgroup's sums (fixed trees: DPP wave sums, then the waves in order)
     sb = wave_sum63(sb);
+    swn = wave_sum63(swn);
 #pragma unroll
     for (int e = 0; e < 8; ++e) c8[e] = wave_sum63(c8[e]);
     const u64 cnt = wave_sum63_u64((u64)nbel | ((u64)nbad << 32));
@@ -2638,8 +2731,24 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
 #pragma unroll
         for (int e = 0; e < 8; ++e) s_red[wave][1 + e] = c8[e];
         s_red[wave][9] = __longlong_as_double((long long)cnt);
+        s_red[wave][10] = swn;
     }
     __syncthreads();  // (the LDS atomics, the wave counts and sums are complete)
+    WINP_B(4);
+    // the coarse buckets first: their atomics complete while the rest is stored
+    if (t < NCB) {
+        unsigned c = 0;
+        u64 f = 0;
+#pragma unroll
+        for (int q = 0; q < WREP; ++q) {
+            c += s_cc[q * WRS + t];
+            f += s_cf[q * WRS + t];
+        }
+        if (c) {
+            __hip_atomic_fetch_add(&w.gcc[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&w.gcf[t], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     unsigned wpos = 0, wall = 0;
 #pragma unroll
     for (int q = 0; q < NWAVE; ++q) {
@@ -2656,39 +2765,39 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
                 __hip_atomic_store(&w.wsk[slot], kk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&w.wsr[slot], rr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&w.wso[slot], oo[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&w.wsp[slot], (uint32_t)(base + (int64_t)q * HT), __ATOMIC_RELAXED,
+                __hip_atomic_store(&w.wsp[slot], (uint32_t)row_of(q), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
             wpos += (unsigned)__popcll(masks[q]);
         }
     }
-    if (t < 10) {  // the record: count below, window rows, bad rows, sum of r, fit sums
-        double v = s_red[0][t];
+    if (t >= HT - 11) {  // the record (the last wave: wave 0 flushed the buckets): count
+                         // below, window rows, bad rows, sum of r below, fit sums, window r
+        const int f = t - (HT - 11);
+        double v = s_red[0][f];
         u64 cv = (u64)__double_as_longlong(s_red[0][9]);
         for (int q = 1; q < NWAVE; ++q) {
-            v = v + s_red[q][t];
+            v = v + s_red[q][f];
             cv += (u64)__double_as_longlong(s_red[q][9]);
         }
         u64 *rec = w.wrec + (int64_t)blk * WREC;
-        if (t == 9) {
+        if (f == 9) {
             const u64 bad = (cv >> 32) + (wall > (unsigned)WSLOT ? 1ULL : 0ULL);
             __hip_atomic_store(&rec[0], cv & 0xffffffffULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&rec[1], (u64)wall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&rec[2], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(&rec[3 + t], (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
+            __hip_atomic_store(&rec[f < 9 ? 3 + f : 12], (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (t < NCB && s_cc[t]) {
-        __hip_atomic_fetch_add(&w.gcc[t], s_cc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&w.gcf[t], s_cf[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    WINP_B(5);
     WINP_B(2);
     // hand-off (k_fit_sums' form): every storing wave waits for its stores and atomics,
     // then one lane arrives at its group counter and the group's last at the top counter
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    WINP_B(6);
     if (t == 0) {
         const unsigned grp = blockIdx.x & 7u, ng = min(gridDim.x, 8u);
         const unsigned gsz = (gridDim.x - grp + 7u) / 8u;
@@ -2721,31 +2830,95 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     }
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
-    if (t < 8) s_fit[t] = 0.0;
     const int nwb = gridDim.x;
     const int G = (nwb + HT - 1) / HT;  // this thread's records: [g0, g1) (in order)
     const int g0 = min(nwb, t * G), g1 = min(nwb, g0 + G);
-    long long nb_t = 0, nw_t = 0, bad_t = 0;
-    double sb_t = 0.0, f8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int g = g0; g < g1; ++g) {
-        const u64 *rec = w.wrec + (int64_t)g * WREC;
-        u64 v[12];
+    constexpr int GMAX = 8;  // records per thread (nwb <= W_MAXWG)
+    long long nb_t = 0, nw_t = 0, bad_t = nwb > W_MAXWG ? 1 : 0;
+    long long nwg[GMAX];
+    double sb_t = 0.0, sw_t = 0.0, f8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-        for (int e = 0; e < 12; ++e) v[e] = __hip_atomic_load(&rec[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        nb_t += (long long)v[0];
-        nw_t += (long long)v[1];
-        bad_t += (long long)v[2];
-        sb_t = sb_t + __longlong_as_double((long long)v[3]);
+    for (int q = 0; q < GMAX; ++q) {
+        const int g = g0 + q;
+        nwg[q] = 0;
+        if (g < g1) {
+            const u64 *rec = w.wrec + (int64_t)g * WREC;
+            u64 v[13];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f8[e] = f8[e] + __longlong_as_double((long long)v[4 + e]);
+            for (int e = 0; e < 13; ++e) v[e] = __hip_atomic_load(&rec[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sw_t = sw_t + __longlong_as_double((long long)v[12]);
+            nb_t += (long long)v[0];
+            nwg[q] = (long long)v[1];
+            nw_t += (long long)v[1];
+            bad_t += (long long)v[2];
+            sb_t = sb_t + __longlong_as_double((long long)v[3]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f8[e] = f8[e] + __longlong_as_double((long long)v[4 + e]);
+        }
     }
-    long long K0, Wt;
-    (void)blk_excl_scan_ll(nb_t, scr, K0);
-    long long woff = blk_excl_scan_ll(nw_t, scr, Wt);
-    const long long bad = blk_max_ll(bad_t, scr);
-    const double S0 = blk_sum(sb_t, scr);
-    blk_sum8_add(f8, s_fit, scr);
+    // one reduction for all of them (one barrier): DPP wave sums / the window rows' wave
+    // scan, lane 63's totals in LDS, the waves added in order (the same fixed trees as
+    // blk_sum and blk_sum8_add)
+    __shared__ double s_rr[NWAVE][12];
+    {
+        const long long nwi = wave_incl_scan_ll(nw_t);
+        const double sbw = wave_sum63(sb_t);
+        const double sww = wave_sum63(sw_t);
+        const u64 cnt = wave_sum63_u64((u64)nb_t | ((u64)min(bad_t, 1LL) << 40));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f8[e] = wave_sum63(f8[e]);
+        if (lane == 63) {
+            s_rr[wave][0] = __longlong_as_double((long long)cnt);
+            s_rr[wave][1] = __longlong_as_double(nwi);
+            s_rr[wave][2] = sbw;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s_rr[wave][3 + e] = f8[e];
+            s_rr[wave][11] = sww;
+        }
+        nw_t = nwi - nw_t;  // exclusive inside the wave
+    }
+    __syncthreads();
+    long long K0 = 0, Wt = 0, woff = nw_t, bad = 0;
+    double S0 = 0.0, Swin = 0.0;
+#pragma unroll
+    for (int q = 0; q < NWAVE; ++q) {
+        const u64 cq = (u64)__double_as_longlong(s_rr[q][0]);
+        const long long wq = __double_as_longlong(s_rr[q][1]);
+        K0 += (long long)(cq & ((1ULL << 40) - 1ULL));
+        bad += (long long)(cq >> 40);
+        if (q < wave) woff += wq;
+        Wt += wq;
+        S0 = S0 + s_rr[q][2];
+        Swin = Swin + s_rr[q][11];
+    }
+    if (t < 8) {
+        double v = 0.0;
+        for (int q = 0; q < NWAVE; ++q) v = v + s_rr[q][3 + t];
+        s_fit[t] = v;  // (the window rows' part is added after the sort)
+    }
     bool fail = bad != 0 || Wt <= 0 || Wt > CAP;
+    const double p = 2.0 * lamv + 1.0;
+    // each coarse bucket's lower bound of h (k_sel_bounds' block_lb), before the sort: only
+    // its comparison with U waits for the minimum.  Rows before a bucket: the buckets before
+    // it, + K0 + Wt above the window; lower sum: the fixed-point brackets (the window's
+    // exact S0 + Swin above it)
+    double lbv = INFINITY;
+    bool lbok = true;
+    {
+        const double unit = ldexp(1.0, -m.fxs);
+        long long C0 = t < NCB ? (long long)cc : 0;
+        double Pb = (t < NCS) ? (double)cf * unit : 0.0;
+        double Pa = (t >= NCS && t < NCB) ? (double)cf * unit : 0.0;
+        blk_excl_scan3(C0, Pb, Pa, scr);
+        if (t < NCB) {
+            if (t == NCS - 1 && C0 + (long long)cc != K0) lbok = false;  // (a row lost: never)
+            if (cc) {
+                const long long c0 = t < NCS ? C0 : C0 + Wt;  // (C0 counts every row below the window)
+                const double P0 = t < NCS ? Pb : (S0 + Swin) + Pa;
+                lbv = block_lb(c0, (long long)cc, P0, lo_r(win_bucket_lo(m, t)), p);
+            }
+        }
+    }
     WINP_T(1);
     // the window rows into LDS, in workgroup order (lds_sort_scan's layout + work rows)
     using LY = LdsLay<CAP, true>;
@@ -2753,24 +2926,64 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     double *lr = (double *)(sm + LY::R);
     uint32_t *lo = (uint32_t *)(sm + LY::O);
     uint32_t *lrow = (uint32_t *)(sm + W_ROW);
+    // each workgroup's first candidate index (in the sort's bin area, free until the sort),
+    // then every candidate loads its slot: one round of loads (a per-workgroup loop of
+    // dependent loads serialised them)
+    unsigned *s_off = (unsigned *)(sm + LY::BC);  // [nwb + 1]
+    static_assert(2 * NSB >= W_MAXWG + 1, "workgroup offsets in the bin area");
     if (!fail) {
-        for (int g = g0; g < g1; ++g) {
-            const int cnt = (int)__hip_atomic_load(&w.wrec[(int64_t)g * WREC + 1], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-            for (int j = 0; j < cnt; ++j) {
-                const int64_t sl = (int64_t)g * WSLOT + j;
-                lk[woff + j] = __hip_atomic_load(&w.wsk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                lr[woff + j] = __hip_atomic_load(&w.wsr[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                lo[woff + j] = __hip_atomic_load(&w.wso[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                lrow[woff + j] = __hip_atomic_load(&w.wsp[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int q = 0; q < GMAX; ++q)
+            if (g0 + q < g1) {
+                s_off[g0 + q] = (unsigned)woff;
+                woff += nwg[q];
             }
-            woff += cnt;
+        if (t == 0) s_off[nwb] = (unsigned)Wt;
+    }
+    __syncthreads();
+    if (!fail) {
+        constexpr int EU = CAP / HT;
+        int64_t sl[EU];
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+            const int e = t + u * HT;
+            sl[u] = -1;
+            if (e < Wt) {
+                int lo_g = 0, hi_g = nwb;  // the last workgroup whose first index is <= e
+                while (hi_g - lo_g > 1) {
+                    const int mid = (lo_g + hi_g) >> 1;
+                    if ((int)s_off[mid] <= e) lo_g = mid;
+                    else hi_g = mid;
+                }
+                sl[u] = (int64_t)lo_g * WSLOT + (e - (int)s_off[lo_g]);
+            }
+        }
+        u64 vk[EU];
+        double vr[EU];
+        uint32_t vo[EU], vp[EU];
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+            if (sl[u] >= 0) {
+                vk[u] = __hip_atomic_load(&w.wsk[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vr[u] = __hip_atomic_load(&w.wsr[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vo[u] = __hip_atomic_load(&w.wso[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vp[u] = __hip_atomic_load(&w.wsp[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+            if (sl[u] >= 0) {
+                const int e = t + u * HT;
+                lk[e] = vk[u];
+                lr[e] = vr[u];
+                lo[e] = vo[u];
+                lrow[e] = vp[u];
+            }
         }
     }
     __syncthreads();
     WINP_T(2);
     const double lam = lamv;
-    const double p = 2.0 * lam + 1.0;
     FinalIn in;
     in.N = n;
     in.lam = lam;
@@ -2780,42 +2993,37 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     in.fs = fs;
     in.fsum = s_fit;
     ScanOut rs{INFINITY, 0x7fffffffffffffffLL, 0, 0, 0.0};
+    __shared__ u64 s_aux[3];
+    const bool small = Wt <= SMALL_C;  // (its rank loop is O(c) per row: 492 rows took 17.6 us)
     if (!fail) {
-        const Cand none{nullptr, nullptr, nullptr, nullptr};
-        rs = lds_sort_scan<CAP, true, true>(none, (unsigned)Wt, K0, S0, in, sm, scr);
+        if (small) {
+            rs = win_scan_small((unsigned)Wt, in, lk, lo, lr, (uint16_t *)(sm + LY::POS), scr, s_aux);
+        } else {
+            const Cand none{nullptr, nullptr, nullptr, nullptr};
+            rs = lds_sort_scan<CAP, true, true>(none, (unsigned)Wt, K0, S0, in, sm, scr);
+        }
         fail = rs.bk == 0x7fffffffffffffffLL;
     }
     WINP_T(3);
     // the minimum is global: every coarse bucket's lower bound of h exceeds U
     double U = INFINITY;
     if (!fail) {
-        U = h_of(rs.bk, S0 + lr[rs.bk - K0 - 1], p) + kMarg;  // (lr: prefix sums by position)
+        // S at the minimum: s_aux (small) or lds_sort_scan's prefix sums by position in lr
+        const double Sbk = small ? __longlong_as_double((long long)s_aux[0]) : S0 + lr[rs.bk - K0 - 1];
+        U = h_of(rs.bk, Sbk, p) + kMarg;
         if (t == 0) {
             s_tko[0] = rs.tk;
             s_tko[1] = (u64)rs.to;
         }
     }
-    const double unit = ldexp(1.0, -m.fxs);
-    long long C0 = t < NCB ? (long long)cc : 0;
-    double Pb = (t < NCS) ? (double)cf * unit : 0.0;
-    double Pa = (t >= NCS && t < NCB) ? (double)cf * unit : 0.0;
-    blk_excl_scan3(C0, Pb, Pa, scr);  // (its barriers publish s_tko)
-    bool ok = true;
-    if (!fail && t < NCB) {
-        if (t == NCS - 1 && C0 + (long long)cc != K0) ok = false;  // (a row lost: never)
-        if (cc) {
-            const long long c0 = t < NCS ? C0 : C0 + Wt;  // (C0 counts every row below the window)
-            const double P0 = t < NCS ? Pb : (S0 + rs.total) + Pa;
-            const double lb = block_lb(c0, (long long)cc, P0, lo_r(win_bucket_lo(m, t)), p);
-            ok = lb > U;
-        }
-    }
-    fail = fail || blk_max_ll(ok ? 0 : 1, scr) != 0 || force_retry;
+    const bool ok = lbok && (lbv > U);  // (empty buckets: lbv = inf)
+    fail = fail || blk_max_ll(ok ? 0 : 1, scr) != 0 || force_retry;  // (its barriers publish s_tko)
     WINP_T(4);
 #ifdef FICP_WIN_PROF
     if (t == 0)
-        printf("WINPROF W=%lld K0=%lld fail=%d | b0 load %llu pass %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu (10 ns)\n",
-               Wt, K0, (int)fail, g_winp[1] - g_winp[0], g_winp[2] - g_winp[1], wt_[0] - g_winp[2],
+        printf("WINPROF W=%lld K0=%lld fail=%d | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu (10 ns)\n",
+               Wt, K0, (int)fail, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
+               g_winp[5] - g_winp[4], g_winp[2] - g_winp[5], g_winp[6] - g_winp[2], wt_[0] - g_winp[6],
                wt_[1] - wt_[0], wt_[2] - wt_[1], wt_[3] - wt_[2], wt_[4] - wt_[3]);
 #endif
     if (fail) {
@@ -2832,6 +3040,9 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     if (fs.on) blk_sum8_add(cf8, s_fit, scr);
     if (t == 0) {
         publish(&s_st, in, rs.bf, rs.bk, tk, to);
+        // the next window's smallest half-width from this one's row count (2^lh keys)
+        if (Wt > 384) s_st.wfloor = max(kWinHMinLog, min(s_st.wfloor, m.su + 2) - 1);
+        else if (Wt < 48) s_st.wfloor = min(kWinHStartLog, s_st.wfloor + 1);
         loop_step(&s_st, lc);
         if (fs.on && !s_st.no_fit && s_st.k > 0)
             fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
@@ -2980,7 +3191,7 @@ hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
                              const unsigned long long *range, int64_t range_parts, void *tmp,
                              IterState *st, const LoopCtl &loop, int *host_flag, hipStream_t s,
                              const FitSrc &fit, int fault) {
-    if (n <= 0) return hipErrorInvalidValue;
+    if (n <= 0 || !orig) return hipErrorInvalidValue;  // (the work order's caller indices)
     hipLaunchKernelGGL(k_sel_win, dim3(gather_blocks(n)), dim3(HT), 0, s, r, orig, n, range,
                        range_parts, carve(tmp, n), st, loop, host_flag, fit,
                        (fault & FICP_FAULT_WIN) ? 1 : 0);

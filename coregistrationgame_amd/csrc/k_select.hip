@@ -2436,25 +2436,27 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 //    path decided: both give the first minimum of the same exact curve (S sums differ in
 //    their last bits only: k is pinned where the curve separates by > 1e-9).
 struct WMap {
-    u64 kmin, kmax, wlo, whi;
+    u64 kmin, kmax;  // the call's key range (the last workgroup: from the records)
+    u64 wlo, whi;
     int su;   // coarse unit 2^su keys (H / 4)
-    int fxs;  // fixed point: m = floor(r * 2^fxs), every finite r < 2^(62 - bits(n) - fxs)
+    int fxb;  // fixed point: a row of bucket b adds floor(r * 2^(fxb - e_b)), r < 2^e_b
     int ok;
 };
 
-__device__ __forceinline__ WMap win_map(u64 kmin, u64 kmax, u64 c, u64 tmove, int wfloor,
-                                        int64_t n) {
+// the window [c - H, c + H) (saturated at the key range's ends), H = 2^win_lh; no key
+// range needed: the coarse buckets are measured from the window's edges, and each has its
+// own fixed-point exponent from its highest key
+__device__ __forceinline__ WMap win_map(u64 c, u64 tmove, int wfloor, int64_t n) {
     WMap m{};
-    m.kmin = kmin;
-    m.kmax = kmax;
+    m.kmin = 0;
+    m.kmax = ~0ULL;
     const int lh = win_lh(tmove, wfloor);
     const u64 H = 1ULL << lh;
     m.su = lh - 2;
-    m.wlo = (c > kmin && c - kmin > H) ? c - H : kmin;
-    m.whi = (kmax >= c && kmax - c >= H) ? c + H : kmax + 1ULL;
-    const int ex = (int)((kmax >> 52) & 0x7ffULL);  // d_max < 2^(ex - 1022): r < 2^(2 ex - 2044)
-    m.ok = (kmax >> 63) && ex < 0x7ff && kmax != ~0ULL && lh <= kWinHMaxLog;
-    m.fxs = (62 - bits_of((u64)max<int64_t>(n, 1))) - (2 * ex - 2044);
+    m.wlo = c > H ? c - H : 0ULL;
+    m.whi = c < ~0ULL - H ? c + H : ~0ULL;
+    m.ok = lh <= kWinHMaxLog;
+    m.fxb = 62 - bits_of((u64)max<int64_t>(n, 1));
     return m;
 }
 
@@ -2485,6 +2487,32 @@ __device__ __forceinline__ u64 win_bucket_lo(const WMap &m, int b) {
     if (q >= (1ULL << (64 - m.su))) return m.kmax;
     const u64 d = q << m.su;
     return d > m.kmax - m.whi ? m.kmax : m.whi + d;
+}
+
+// highest key any row of coarse bucket b can have (0: the bucket cannot hold a row)
+__device__ __forceinline__ u64 win_bucket_hi(const WMap &m, int b) {
+    if (b < NCS) {
+        const int j = NCS - 1 - b;  // highest key = wlo - 1 - (lo(j) << su)
+        const u64 q = win_cq_lo(j);
+        if (q >= (1ULL << (64 - m.su))) return 0ULL;
+        const u64 d = q << m.su;
+        return (m.wlo == 0ULL || d > m.wlo - 1ULL) ? 0ULL : m.wlo - 1ULL - d;
+    }
+    const int j = b - NCS;
+    if (j + 1 >= NCS) return ~0ULL;
+    const u64 q = win_cq_lo(j + 1);
+    if (q >= (1ULL << (64 - m.su))) return ~0ULL;
+    const u64 d = q << m.su;
+    return d - 1ULL > ~0ULL - m.whi ? ~0ULL : m.whi + (d - 1ULL);
+}
+
+// e with r < 2^e for every row of coarse bucket b (bucket_exp's rule; 1024: the bucket may
+// hold inf / NaN, those rows fail the window path anyway)
+__device__ __forceinline__ int win_bucket_exp(const WMap &m, int b) {
+    const u64 khi = win_bucket_hi(m, b);
+    if (!(khi >> 63)) return 0;
+    const int ex = (int)((khi >> 52) & 0x7ffULL);
+    return min(2 * ex - 2044, 1024);
 }
 
 __device__ __forceinline__ void win_retry(IterState *st, int *host_flag) {
@@ -2588,19 +2616,6 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     const long long kprev = st->k;
     const u64 tkey = st->tkey, tmove = st->tmove;
     const double lamv = st->lam_cur;
-    // the range parts issue first (PU per thread: the NN's 3,907 parts at 1M rows) and are
-    // reduced after the rows' loads have issued: the reduction waits for them alone
-    constexpr int PU = 8;
-    u64 ka = nparts > 0 ? 0ULL : range[0], kb = nparts > 0 ? 0ULL : range[1];  // (~kmin, kmax)
-    // (every load unconditional, its index clamped: a branch around a load made the
-    // compiler wait for it at the join, which serialised every load of this kernel)
-    ulonglong2 pv[PU];
-    const int64_t plast = max<int64_t>(nparts - 1, 0);
-#pragma unroll
-    for (int u = 0; u < PU; ++u) {
-        const int64_t q = min<int64_t>(t + (int64_t)u * HT, plast);  // (a repeat: max unchanged)
-        pv[u] = *reinterpret_cast<const ulonglong2 *>(range + 2 + 2 * q);
-    }
     // row q of this thread: pairs of consecutive rows per lane, so that every load is 16 B
     // (8-B lanes stream at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md)
     const int64_t base = (int64_t)blockIdx.x * (HT * WI) + 2 * t;
@@ -2625,16 +2640,6 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
         yt[q] = e.x, yt[q + 1] = e.y;
         oo[q] = o.x, oo[q + 1] = o.y;
     }
-#pragma unroll
-    for (int u = 0; u < PU; ++u) {
-        ka = max(ka, pv[u].x);
-        kb = max(kb, pv[u].y);
-    }
-    for (int64_t q = t + (int64_t)PU * HT; q < nparts; q += HT) {  // (more than PU x HT parts)
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(range + 2 + 2 * q);
-        ka = max(ka, v.x);
-        kb = max(kb, v.y);
-    }
     if (sk) {  // the run is over: the flag as k_sel_final's no-op
         if (blockIdx.x == 0 && t == 0 && host_flag)
             __hip_atomic_store(host_flag, kFlagDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2644,36 +2649,21 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
         s_cc[b] = 0u;
         s_cf[b] = 0ULL;
     }
-    {
-        // block max of (~kmin, kmax) with an LDS-only barrier: __syncthreads() would also
-        // wait for every row's load (vmcnt(0)); this way the rows are classified as their
-        // loads land
-#define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
-        wave_range_reduce(ka, kb);
-        if (lane == 63) {
-            scr.u[wave] = ka;
-            scr.v[wave] = kb;
-        }
-        LDS_BARRIER();
-        u64 a = scr.u[0], b = scr.v[0];
-#pragma unroll
-        for (int q = 1; q < NWAVE; ++q) {
-            a = max(a, scr.u[q]);
-            b = max(b, scr.v[q]);
-        }
-        ka = ~a;
-        kb = b;
-#undef LDS_BARRIER
-    }
-    const WMap m = win_map(ka, kb, tkey, tmove, wfl, n);
+    const WMap m0 = win_map(tkey, tmove, wfl, n);
+    __shared__ int s_ce[NCB];  // each coarse bucket's fixed-point exponent
+    if (t < NCB) s_ce[t] = win_bucket_exp(m0, t);
     // (uniform over the launch: every workgroup decides the same way, none arrives)
-    if (!(ph == PH_LOOP && itv >= 1 && kprev > 0 && 2.0 * lamv + 1.0 >= 1.0 && m.ok)) {
+    if (!(ph == PH_LOOP && itv >= 1 && kprev > 0 && 2.0 * lamv + 1.0 >= 1.0 && m0.ok)) {
         if (blockIdx.x == 0 && t == 0) win_retry(st, host_flag);
         return;
     }
+    // an LDS-only barrier: __syncthreads() would also wait for every row's load
+    // (vmcnt(0)); this way the rows are classified as their loads land
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     WINP_B(1);
     // classify the rows
     unsigned nbel = 0, nbad = 0;
+    u64 kmn = ~0ULL, kmx = 0ULL;  // the finite rows' key range (the last workgroup's kmin)
     double sb = 0.0, swn = 0.0;
     double c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     u64 kk[WI];
@@ -2692,21 +2682,24 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
             }
             const u64 k = key_of_r(v);
             kk[q] = k;
-            const u64 fx = (u64)ldexp(v, m.fxs);
-            if (k < m.wlo) {
+            kmn = min(kmn, k);
+            kmx = max(kmx, k);
+            if (k < m0.wlo) {
                 ++nbel;
                 sb = sb + v;
                 fit_add(c8, xs[q], ys[q], xt[q], yt[q], fs.px, fs.py);
-                const int b = NCS - 1 - win_cq((m.wlo - 1ULL - k) >> m.su);
+                const int b = NCS - 1 - win_cq((m0.wlo - 1ULL - k) >> m0.su);
+                const int e = s_ce[b];
                 atomicAdd(&my_cc[b], 1u);
-                atomicAdd(&my_cf[b], fx);
-            } else if (k < m.whi) {
+                atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
+            } else if (k < m0.whi) {
                 inw |= 1u << q;
                 swn = swn + v;
             } else {
-                const int b = NCS + win_cq((k - m.whi) >> m.su);
+                const int b = NCS + win_cq((k - m0.whi) >> m0.su);
+                const int e = s_ce[b];
                 atomicAdd(&my_cc[b], 1u);
-                atomicAdd(&my_cf[b], fx);
+                atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
             }
         }
     }
@@ -2726,6 +2719,13 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
 #pragma unroll
     for (int e = 0; e < 8; ++e) c8[e] = wave_sum63(c8[e]);
     const u64 cnt = wave_sum63_u64((u64)nbel | ((u64)nbad << 32));
+    u64 pka = ~kmn, pkb = kmx;
+    wave_range_reduce(pka, pkb);  // (max of ~kmin and of kmax, lane 63)
+    __shared__ u64 s_kr[NWAVE][2];
+    if (lane == 63) {
+        s_kr[wave][0] = pka;
+        s_kr[wave][1] = pkb;
+    }
     if (lane == 63) {
         s_red[wave][0] = sb;
 #pragma unroll
@@ -2770,6 +2770,15 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
             }
             wpos += (unsigned)__popcll(masks[q]);
         }
+    }
+    if (t == HT - 12) {  // the record's key range words: max(~key), max(key)
+        u64 a = s_kr[0][0], b = s_kr[0][1];
+        for (int q = 1; q < NWAVE; ++q) {
+            a = max(a, s_kr[q][0]);
+            b = max(b, s_kr[q][1]);
+        }
+        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 13], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 14], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t >= HT - 11) {  // the record (the last wave: wave 0 flushed the buckets): count
                          // below, window rows, bad rows, sum of r below, fit sums, window r
@@ -2837,16 +2846,19 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     long long nb_t = 0, nw_t = 0, bad_t = nwb > W_MAXWG ? 1 : 0;
     long long nwg[GMAX];
     double sb_t = 0.0, sw_t = 0.0, f8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 kra_t = 0ULL, krb_t = 0ULL;  // max(~key), max(key) over this thread's records
 #pragma unroll
     for (int q = 0; q < GMAX; ++q) {
         const int g = g0 + q;
         nwg[q] = 0;
         if (g < g1) {
             const u64 *rec = w.wrec + (int64_t)g * WREC;
-            u64 v[13];
+            u64 v[15];
 #pragma unroll
-            for (int e = 0; e < 13; ++e) v[e] = __hip_atomic_load(&rec[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int e = 0; e < 15; ++e) v[e] = __hip_atomic_load(&rec[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sw_t = sw_t + __longlong_as_double((long long)v[12]);
+            kra_t = max(kra_t, v[13]);
+            krb_t = max(krb_t, v[14]);
             nb_t += (long long)v[0];
             nwg[q] = (long long)v[1];
             nw_t += (long long)v[1];
@@ -2859,11 +2871,12 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     // one reduction for all of them (one barrier): DPP wave sums / the window rows' wave
     // scan, lane 63's totals in LDS, the waves added in order (the same fixed trees as
     // blk_sum and blk_sum8_add)
-    __shared__ double s_rr[NWAVE][12];
+    __shared__ double s_rr[NWAVE][14];
     {
         const long long nwi = wave_incl_scan_ll(nw_t);
         const double sbw = wave_sum63(sb_t);
         const double sww = wave_sum63(sw_t);
+        wave_range_reduce(kra_t, krb_t);
         const u64 cnt = wave_sum63_u64((u64)nb_t | ((u64)min(bad_t, 1LL) << 40));
 #pragma unroll
         for (int e = 0; e < 8; ++e) f8[e] = wave_sum63(f8[e]);
@@ -2874,12 +2887,15 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
 #pragma unroll
             for (int e = 0; e < 8; ++e) s_rr[wave][3 + e] = f8[e];
             s_rr[wave][11] = sww;
+            s_rr[wave][12] = __longlong_as_double((long long)kra_t);
+            s_rr[wave][13] = __longlong_as_double((long long)krb_t);
         }
         nw_t = nwi - nw_t;  // exclusive inside the wave
     }
     __syncthreads();
     long long K0 = 0, Wt = 0, woff = nw_t, bad = 0;
     double S0 = 0.0, Swin = 0.0;
+    u64 kra = 0ULL, krb = 0ULL;
 #pragma unroll
     for (int q = 0; q < NWAVE; ++q) {
         const u64 cq = (u64)__double_as_longlong(s_rr[q][0]);
@@ -2890,7 +2906,12 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
         Wt += wq;
         S0 = S0 + s_rr[q][2];
         Swin = Swin + s_rr[q][11];
+        kra = max(kra, (u64)__double_as_longlong(s_rr[q][12]));
+        krb = max(krb, (u64)__double_as_longlong(s_rr[q][13]));
     }
+    WMap m = m0;  // with the call's key range (the lowest coarse bucket's lowest r)
+    m.kmin = ~kra;
+    m.kmax = krb;
     if (t < 8) {
         double v = 0.0;
         for (int q = 0; q < NWAVE; ++q) v = v + s_rr[q][3 + t];
@@ -2905,10 +2926,11 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     double lbv = INFINITY;
     bool lbok = true;
     {
-        const double unit = ldexp(1.0, -m.fxs);
+        const int eb = t < NCB ? win_bucket_exp(m, t) : 0;
+        const double lo_sum = eb < 1024 ? ldexp((double)cf, eb - m.fxb) : 0.0;  // (exact)
         long long C0 = t < NCB ? (long long)cc : 0;
-        double Pb = (t < NCS) ? (double)cf * unit : 0.0;
-        double Pa = (t >= NCS && t < NCB) ? (double)cf * unit : 0.0;
+        double Pb = (t < NCS) ? lo_sum : 0.0;
+        double Pa = (t >= NCS && t < NCB) ? lo_sum : 0.0;
         blk_excl_scan3(C0, Pb, Pa, scr);
         if (t < NCB) {
             if (t == NCS - 1 && C0 + (long long)cc != K0) lbok = false;  // (a row lost: never)

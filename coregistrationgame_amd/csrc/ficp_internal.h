@@ -367,7 +367,8 @@ struct alignas(16) IterState {
                            // nn_reuse so the queued NN launch is a no-op, and the full
                            // selection of the same call (k_sel_final) clears both
     int wfloor;            // log2 of the window path's smallest half-width (keys): adapted
-                           // by each window call to keep its window at ~48-384 rows
+                           // by each window call to keep its window at ~48-384 rows (0:
+                           // not yet, win_start_log)
     int pad3;
 };
 
@@ -380,7 +381,19 @@ constexpr int kFlagDone = 1, kFlagWinNext = 2, kFlagRetry = 4;
 // lh = max(wfloor, bits(tmove) + 1): at least twice the last move (C3's moves shrink
 // ~3-10x per call); wfloor starts at 2^40 (C3 stage 1: ~40-160 rows) and follows the
 // window's row count (stage 2's density put ~1,000 rows into 2^40)
-constexpr int kWinHMinLog = 36, kWinHStartLog = 40, kWinHMaxLog = 44;
+// The floor starts at 2^(60 - bits(N)) keys (C3, 1M rows: 2^40; a 10k-row plot of C4 has
+// 100x fewer rows per key: 2^46) and may grow 4 doublings above that (win_hmax_log).
+// wfloor == 0: not adapted yet (the start).
+constexpr int kWinHMinLog = 36, kWinHStartLog = 40;
+__host__ __device__ __forceinline__ int win_start_log(long long n) {
+    const int b = n > 0 ? 64 - __builtin_clzll((unsigned long long)n) : 0;
+    const int v = 60 - b;
+    return v < kWinHMinLog ? kWinHMinLog : (v > 48 ? 48 : v);
+}
+__host__ __device__ __forceinline__ int win_hmax_log(long long n) { return win_start_log(n) + 4; }
+__host__ __device__ __forceinline__ int win_floor(int wfloor, long long n) {
+    return wfloor > 0 ? wfloor : win_start_log(n);
+}
 __host__ __device__ __forceinline__ int win_lh(unsigned long long tmove, int wfloor) {
     const int b = tmove ? 64 - __builtin_clzll(tmove) : 0;
     return b + 1 > wfloor ? b + 1 : wfloor;
@@ -391,7 +404,8 @@ __host__ __device__ __forceinline__ int win_lh(unsigned long long tmove, int wfl
 // threshold moved less than 2^43 keys, p = 2 lambda + 1 >= 1 (the bounds' quasi-concavity)
 __device__ __forceinline__ bool win_ok(const IterState &s) {
     return s.phase == PH_LOOP && !s.done && s.it >= 1 && s.k > 0 &&
-           win_lh(s.tmove, s.wfloor) <= kWinHMaxLog && 2.0 * s.lam_cur + 1.0 >= 1.0;
+           win_lh(s.tmove, win_floor(s.wfloor, s.n_src)) <= win_hmax_log(s.n_src) &&
+           2.0 * s.lam_cur + 1.0 >= 1.0;
 }
 
 // FRMSD(k) = (1 / (k/N)**lambda) * sqrt(S_k / k), in the reference's operation order
@@ -881,6 +895,9 @@ struct alignas(16) PlotState {
     int n_nn, n_fit, iters0, iters1;
     unsigned long long tkey;  // selection threshold: rows with (key, row) <= (tkey, trow)
     long long trow;           // (global row index) are the k selected ones
+    unsigned long long tmove; // |tkey - previous tkey| between two loop-body calls (else 0)
+    int wfloor;               // the window path's smallest half-width, log2 keys (adapted)
+    int pad;
 };
 
 // per-plot bbox of the CHM layer: bb[4p..4p+3] = xmin, xmax, ymin, ymax

@@ -8,6 +8,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdint.h>
+
+#include "ficp_internal.h"
 
 namespace ficp {
 namespace fb {
@@ -48,6 +51,92 @@ __device__ __forceinline__ double block_lb(long long C0, long long c, double P0,
     const double a = h_of(C0 + 1, P0 + lo, p);
     const double b = h_of(C0 + c, P0 + (double)c * lo, p);
     return fmin(a, b) - kMarg;
+}
+
+// ---- the window paths (k_select.hip k_sel_win, k_batch.hip k_batch_select): a key
+// window [wlo, whi) around the previous threshold key and kWinNCS coarse buckets on each
+// side whose widths grow with their distance from it (win_lh: ficp_internal.h)
+constexpr int kWinNCS = 128;
+typedef unsigned long long u64;
+
+struct WMap {
+    u64 kmin, kmax;  // the call's key range (the last workgroup: from the records)
+    u64 wlo, whi;
+    int su;   // coarse unit 2^su keys (H / 4)
+    int fxb;  // fixed point: a row of bucket b adds floor(r * 2^(fxb - e_b)), r < 2^e_b
+    int ok;
+};
+
+// the window [c - H, c + H) (saturated at the key range's ends), H = 2^win_lh; no key
+// range needed: the coarse buckets are measured from the window's edges, and each has its
+// own fixed-point exponent from its highest key
+__device__ __forceinline__ WMap win_map(u64 c, u64 tmove, int wfloor, int64_t n) {
+    WMap m{};
+    m.kmin = 0;
+    m.kmax = ~0ULL;
+    const int lh = win_lh(tmove, win_floor(wfloor, n));
+    const u64 H = 1ULL << lh;
+    m.su = lh - 2;
+    m.wlo = c > H ? c - H : 0ULL;
+    m.whi = c < ~0ULL - H ? c + H : ~0ULL;
+    m.ok = lh <= win_hmax_log(n);
+    m.fxb = 62 - bits_of((u64)max<int64_t>(n, 1));
+    return m;
+}
+
+// coarse bucket of a distance of q units from the window edge (0..3: one unit each, then 4
+// per octave) and the smallest q of bucket j
+__device__ __forceinline__ int win_cq(u64 q) {
+    if (q < 4) return (int)q;
+    const int e = 63 - __clzll((long long)q);
+    return min(4 * (e - 1) + (int)((q >> (e - 2)) & 3ULL), kWinNCS - 1);
+}
+__device__ __forceinline__ u64 win_cq_lo(int j) {
+    if (j < 4) return (u64)j;
+    return (u64)(4 + (j & 3)) << (j / 4 - 1);
+}
+
+// lowest key any row of coarse bucket b (key order: b < kWinNCS below the window, kWinNCS - 1 the
+// nearest; b >= kWinNCS above it, kWinNCS the nearest) can have
+__device__ __forceinline__ u64 win_bucket_lo(const WMap &m, int b) {
+    if (b < kWinNCS) {
+        const int j = kWinNCS - 1 - b;  // rows with (wlo - 1 - key) >> su in [lo(j), lo(j + 1))
+        if (j + 1 >= kWinNCS) return m.kmin;
+        const u64 q = win_cq_lo(j + 1);
+        if (q >= (1ULL << (64 - m.su))) return m.kmin;
+        const u64 d = q << m.su;  // lowest key = wlo - d
+        return d >= m.wlo - m.kmin ? m.kmin : m.wlo - d;
+    }
+    const u64 q = win_cq_lo(b - kWinNCS);
+    if (q >= (1ULL << (64 - m.su))) return m.kmax;
+    const u64 d = q << m.su;
+    return d > m.kmax - m.whi ? m.kmax : m.whi + d;
+}
+
+// highest key any row of coarse bucket b can have (0: the bucket cannot hold a row)
+__device__ __forceinline__ u64 win_bucket_hi(const WMap &m, int b) {
+    if (b < kWinNCS) {
+        const int j = kWinNCS - 1 - b;  // highest key = wlo - 1 - (lo(j) << su)
+        const u64 q = win_cq_lo(j);
+        if (q >= (1ULL << (64 - m.su))) return 0ULL;
+        const u64 d = q << m.su;
+        return (m.wlo == 0ULL || d > m.wlo - 1ULL) ? 0ULL : m.wlo - 1ULL - d;
+    }
+    const int j = b - kWinNCS;
+    if (j + 1 >= kWinNCS) return ~0ULL;
+    const u64 q = win_cq_lo(j + 1);
+    if (q >= (1ULL << (64 - m.su))) return ~0ULL;
+    const u64 d = q << m.su;
+    return d - 1ULL > ~0ULL - m.whi ? ~0ULL : m.whi + (d - 1ULL);
+}
+
+// e with r < 2^e for every row of coarse bucket b (bucket_exp's rule; 1024: the bucket may
+// hold inf / NaN, those rows fail the window path anyway)
+__device__ __forceinline__ int win_bucket_exp(const WMap &m, int b) {
+    const u64 khi = win_bucket_hi(m, b);
+    if (!(khi >> 63)) return 0;
+    const int ex = (int)((khi >> 52) & 0x7ffULL);
+    return min(2 * ex - 2044, 1024);
 }
 
 }  // namespace fb

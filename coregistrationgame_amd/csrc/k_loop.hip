@@ -26,7 +26,7 @@ __device__ void loop_init(IterState *st, const LoopCtl &c) {
     s.n_nn = s.n_fit = 0;
     s.n_reuse = 0;
     s.win_fail = 0;
-    s.wfloor = kWinHStartLog;
+    s.wfloor = 0;  // (win_start_log of the plot's rows)
     s.iters[0] = s.iters[1] = 0;
     s.phase = c.nstages > 0 ? PH_HEAD : PH_DONE;
     s.lam_cur = c.nstages > 0 ? lam_of(c, 0) : 0.0;

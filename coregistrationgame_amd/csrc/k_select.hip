@@ -101,7 +101,7 @@ constexpr int MAXLEV = 4;
 // window path (k_sel_win): rows a workgroup may hand over, coarse buckets per side of the
 // window (4 per octave of distance), record words per workgroup, arrival counter stride
 constexpr int WSLOT = 64;
-constexpr int NCS = 128;
+constexpr int NCS = fb::kWinNCS;
 constexpr int NCB = 2 * NCS;
 constexpr int WREC = 16;
 constexpr int WCTR = 64;
@@ -2435,85 +2435,13 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 //    then enqueues launch_select for the same call.  The result never depends on which
 //    path decided: both give the first minimum of the same exact curve (S sums differ in
 //    their last bits only: k is pinned where the curve separates by > 1e-9).
-struct WMap {
-    u64 kmin, kmax;  // the call's key range (the last workgroup: from the records)
-    u64 wlo, whi;
-    int su;   // coarse unit 2^su keys (H / 4)
-    int fxb;  // fixed point: a row of bucket b adds floor(r * 2^(fxb - e_b)), r < 2^e_b
-    int ok;
-};
-
-// the window [c - H, c + H) (saturated at the key range's ends), H = 2^win_lh; no key
-// range needed: the coarse buckets are measured from the window's edges, and each has its
-// own fixed-point exponent from its highest key
-__device__ __forceinline__ WMap win_map(u64 c, u64 tmove, int wfloor, int64_t n) {
-    WMap m{};
-    m.kmin = 0;
-    m.kmax = ~0ULL;
-    const int lh = win_lh(tmove, wfloor);
-    const u64 H = 1ULL << lh;
-    m.su = lh - 2;
-    m.wlo = c > H ? c - H : 0ULL;
-    m.whi = c < ~0ULL - H ? c + H : ~0ULL;
-    m.ok = lh <= kWinHMaxLog;
-    m.fxb = 62 - bits_of((u64)max<int64_t>(n, 1));
-    return m;
-}
-
-// coarse bucket of a distance of q units from the window edge (0..3: one unit each, then 4
-// per octave) and the smallest q of bucket j
-__device__ __forceinline__ int win_cq(u64 q) {
-    if (q < 4) return (int)q;
-    const int e = 63 - __clzll((long long)q);
-    return min(4 * (e - 1) + (int)((q >> (e - 2)) & 3ULL), NCS - 1);
-}
-__device__ __forceinline__ u64 win_cq_lo(int j) {
-    if (j < 4) return (u64)j;
-    return (u64)(4 + (j & 3)) << (j / 4 - 1);
-}
-
-// lowest key any row of coarse bucket b (key order: b < NCS below the window, NCS - 1 the
-// nearest; b >= NCS above it, NCS the nearest) can have
-__device__ __forceinline__ u64 win_bucket_lo(const WMap &m, int b) {
-    if (b < NCS) {
-        const int j = NCS - 1 - b;  // rows with (wlo - 1 - key) >> su in [lo(j), lo(j + 1))
-        if (j + 1 >= NCS) return m.kmin;
-        const u64 q = win_cq_lo(j + 1);
-        if (q >= (1ULL << (64 - m.su))) return m.kmin;
-        const u64 d = q << m.su;  // lowest key = wlo - d
-        return d >= m.wlo - m.kmin ? m.kmin : m.wlo - d;
-    }
-    const u64 q = win_cq_lo(b - NCS);
-    if (q >= (1ULL << (64 - m.su))) return m.kmax;
-    const u64 d = q << m.su;
-    return d > m.kmax - m.whi ? m.kmax : m.whi + d;
-}
-
-// highest key any row of coarse bucket b can have (0: the bucket cannot hold a row)
-__device__ __forceinline__ u64 win_bucket_hi(const WMap &m, int b) {
-    if (b < NCS) {
-        const int j = NCS - 1 - b;  // highest key = wlo - 1 - (lo(j) << su)
-        const u64 q = win_cq_lo(j);
-        if (q >= (1ULL << (64 - m.su))) return 0ULL;
-        const u64 d = q << m.su;
-        return (m.wlo == 0ULL || d > m.wlo - 1ULL) ? 0ULL : m.wlo - 1ULL - d;
-    }
-    const int j = b - NCS;
-    if (j + 1 >= NCS) return ~0ULL;
-    const u64 q = win_cq_lo(j + 1);
-    if (q >= (1ULL << (64 - m.su))) return ~0ULL;
-    const u64 d = q << m.su;
-    return d - 1ULL > ~0ULL - m.whi ? ~0ULL : m.whi + (d - 1ULL);
-}
-
-// e with r < 2^e for every row of coarse bucket b (bucket_exp's rule; 1024: the bucket may
-// hold inf / NaN, those rows fail the window path anyway)
-__device__ __forceinline__ int win_bucket_exp(const WMap &m, int b) {
-    const u64 khi = win_bucket_hi(m, b);
-    if (!(khi >> 63)) return 0;
-    const int ex = (int)((khi >> 52) & 0x7ffULL);
-    return min(2 * ex - 2044, 1024);
-}
+using fb::WMap;
+using fb::win_map;
+using fb::win_cq;
+using fb::win_cq_lo;
+using fb::win_bucket_lo;
+using fb::win_bucket_hi;
+using fb::win_bucket_exp;
 
 __device__ __forceinline__ void win_retry(IterState *st, int *host_flag) {
     st->nn_reuse = 1;  // the NN launch queued behind this one keeps the current outputs
@@ -3063,8 +2991,11 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     if (t == 0) {
         publish(&s_st, in, rs.bf, rs.bk, tk, to);
         // the next window's smallest half-width from this one's row count (2^lh keys)
-        if (Wt > 384) s_st.wfloor = max(kWinHMinLog, min(s_st.wfloor, m.su + 2) - 1);
-        else if (Wt < 48) s_st.wfloor = min(kWinHStartLog, s_st.wfloor + 1);
+        {
+            const int f = win_floor(s_st.wfloor, n);
+            if (Wt > 384) s_st.wfloor = max(kWinHMinLog, min(f, m.su + 2) - 1);
+            else if (Wt < 48) s_st.wfloor = min(win_start_log(n), f + 1);
+        }
         loop_step(&s_st, lc);
         if (fs.on && !s_st.no_fit && s_st.k > 0)
             fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);

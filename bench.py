@@ -421,6 +421,7 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
     # stream, inside the timed region.  Each timed dispatch leaves ~5 us of idle queue
     # around it, so by default only the first timed step carries them.
     ctx.profile_enable(_lib.PROF_NN if args.nn_timing != "none" else 0)
+    ps0 = ctx.path_stats()
     barrier()
     t0 = time.perf_counter()
     fits = calls = timed_calls = 0
@@ -436,6 +437,7 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
             ctx.profile_enable(0)
     barrier()
     dt = time.perf_counter() - t0
+    ps1 = ctx.path_stats()
     ctx.profile_enable(0)
     prof = json.loads(ctx.profile_report())
     dt_max, fits_all, calls_all = dt, fits, calls
@@ -465,6 +467,11 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
             "iterations_per_step": fits_all / steps / world,
             "nn_calls_per_step": calls_all / steps / world,
             "correspondences_per_s": calls_all * n / dt_max,
+            # fraction calls per run decided by the one-launch window path
+            # and those that fell back to the full selection
+            "selection_paths": {"fraction_calls_per_run": calls / steps,
+                                "window_calls_per_run": (ps1["win_calls"] - ps0["win_calls"]) / steps,
+                                "window_fallbacks_per_run": (ps1["win_retries"] - ps0["win_retries"]) / steps},
             "roofline": roofline(achieved, traffic, {
                 "kernel": "k_nn_grid (fused apply + exact 1-NN)", "avg_launch_us": avg_ms * 1e3,
                 "launches": timed_calls, "timed_launches_incl_noop": nn["count"],

@@ -719,7 +719,7 @@ def bench_dry(args, wl, rank, world, D, steps, warmup):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)  # (C3: ~1.2 ms per step; 10 were noisy)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: c3 at 1 GPU, batch at more")

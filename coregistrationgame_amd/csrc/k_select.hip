@@ -2540,7 +2540,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     WINP_B(0);
     // every independent load first: the state's window inputs, the rows, the range parts
     const int sk = st->done;
-    const int ph = st->phase, itv = st->it, wfl = st->wfloor;
+    const int ph = st->phase, itv = st->it, stg = st->stage, wfl = st->wfloor;
     const long long kprev = st->k;
     const u64 tkey = st->tkey, tmove = st->tmove;
     const double lamv = st->lam_cur;
@@ -2581,7 +2581,8 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     __shared__ int s_ce[NCB];  // each coarse bucket's fixed-point exponent
     if (t < NCB) s_ce[t] = win_bucket_exp(m0, t);
     // (uniform over the launch: every workgroup decides the same way, none arrives)
-    if (!(ph == PH_LOOP && itv >= 1 && kprev > 0 && 2.0 * lamv + 1.0 >= 1.0 && m0.ok)) {
+    if (!(ph == PH_LOOP && (itv >= 1 || win_first_body(itv, stg, tmove)) && kprev > 0 &&
+          2.0 * lamv + 1.0 >= 1.0 && m0.ok)) {
         if (blockIdx.x == 0 && t == 0) win_retry(st, host_flag);
         return;
     }

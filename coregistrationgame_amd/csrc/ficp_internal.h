@@ -394,16 +394,17 @@ __host__ __device__ __forceinline__ int win_hmax_log(long long n) { return win_s
 __host__ __device__ __forceinline__ int win_floor(int wfloor, long long n) {
     return wfloor > 0 ? wfloor : win_start_log(n);
 }
-// (tmove 0, no move known: the first loop body of a later stage, 4x the floor)
+// (tmove 0, no move known: the first loop body of a later stage, 2x the floor; C3's 73-row
+// move there is ~2^39.6 keys)
 __host__ __device__ __forceinline__ int win_lh(unsigned long long tmove, int wfloor) {
-    if (!tmove) return wfloor + 2;
+    if (!tmove) return wfloor + 1;
     const int b = 64 - __builtin_clzll(tmove);
     return b + 1 > wfloor ? b + 1 : wfloor;
 }
 // the next fraction call may take the window path: a loop body follows a loop body of the
 // same stage (tkey and tmove from loop-body calls), or it is the first body of a later
 // stage, whose head ran on the previous stage's converged source (C3: 73 rows moved there,
-// inside 4x the floor; stage 1's first body moved 4,228 rows), the threshold moved less
+// inside 2x the floor; stage 1's first body moved 4,228 rows), the threshold moved less
 // than 2^(win_hmax_log - 1) keys, p = 2 lambda + 1 >= 1 (the bounds' quasi-concavity)
 __device__ __forceinline__ bool win_first_body(int it, int stage, unsigned long long tmove) {
     return it == 0 && stage >= 1 && tmove == 0;

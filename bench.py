@@ -700,18 +700,35 @@ def bench_dry(args, wl, rank, world, D, steps, warmup):
     dt = max(time.perf_counter() - t0, 1e-9)
     dt_max = D.max([dt])[0] if D is not None else dt
     counts = D.sum([len(mine)]) if D is not None else [len(mine)]
+    per_rank = [len(mine)]
+    gather_ok = True
     if D is not None:
+        # every rank's plot count, and its plot ids' sum, as one SUM of one-hot vectors
+        oh = [0.0] * (2 * world)
+        oh[rank], oh[world + rank] = float(len(mine)), float(np.sum(mine))
+        red = D.sum(oh)
+        per_rank = [int(v) for v in red[:world]]
+        id_sums = [int(v) for v in red[world:]]
+        assert sum(id_sums) == nplots * (nplots - 1) // 2  # every plot id dealt exactly once
+        # the end-of-run all-gather of the per-plot records, back in batch order
         rec = np.zeros(len(mine), _lib.PLOT_STATS_DTYPE)
         rec["k_last"] = mine
+        rec["n_nn_calls"] = rank
         allrec = shard.gather_plot_stats(deal, rec, rank, device=D.dev)
-        assert np.array_equal(allrec["k_last"], np.arange(nplots))
+        owner = np.empty(nplots, np.int64)
+        for r_, ids in enumerate(deal):
+            owner[ids] = r_
+        gather_ok = bool(np.array_equal(allrec["k_last"], np.arange(nplots))
+                         and np.array_equal(allrec["n_nn_calls"], owner))
+        assert gather_ok
     if rank != 0:
         return None
     return {"metric": METRIC, "value": 0.0, "unit": "iterations/s", "n_gpus": world, "steps": steps,
             "warmup": warmup, "ms_per_step": 1e3 * dt_max / max(steps, 1), "higher_is_better": True,
             "scaling": "strong" if wl == "batch" else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "none (dry run)", "dry_run": True,
-            "config": {"workload": wl, "plots": nplots, "plots_dealt": int(counts[0])},
+            "config": {"workload": wl, "plots": nplots, "plots_dealt": int(counts[0]),
+                       "plots_per_rank": per_rank, "gather_in_order": gather_ok},
             "roofline": None, "cpu_baseline": None}
 
 

@@ -587,7 +587,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // flag carried kFlagWinNext; FICP_SEL_WIN=0 turns it off
     const char *wv = getenv("FICP_SEL_WIN");
     // (the work-order arrays: library buffers, 16-B aligned for the window pass's loads)
-    const bool use_win = fused && fuse_fit && keys_from_r && worig && !(wv && atoi(wv) == 0);
+    const bool use_win = fused && fuse_fit && keys_from_r && worig && select_win_fits(n) &&
+                         !(wv && atoi(wv) == 0);
     auto enq_b = [&](int64_t i, bool win) -> int {
         const int slot = (int)(i % kLoopRing);
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
@@ -1146,6 +1147,7 @@ int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
             stats->host_ms[0] = ms(t0, t1);
             stats->host_ms[1] = ms(t1, t2);
             stats->host_ms[2] = ms(t2, clk::now());
+            stats->host_ms[3] = 0.0;
         }
         return FICP_OK;
     }

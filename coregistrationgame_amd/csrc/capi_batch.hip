@@ -256,7 +256,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // From 64 plots on: two sub-batches, each on its own stream, so one half's
         // latency-bound selection (one workgroup per plot) runs beside the other half's
         // NN.  The plots are independent (app.py:658-660), so the split changes no result.
-        // Measured with the fused step (tools/r3_iter6.sh, plot-it/s): 128 plots 846k vs
+        // Measured with the fused step (tools/batch_ab.sh, plot-it/s): 128 plots 846k vs
         // 834k, 512 1,082k vs 1,019k, 1024 1,119k vs 1,061k.  FICP_BATCH_STREAMS=1..4
         // forces the count.
         int nsub = nplots >= 64 ? 2 : 1;
@@ -265,6 +265,22 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // resets its own); zeroed here, before the fork, so an earlier failed run leaves none
         CHK(b.arrive.ensure(kMaxSub * 8));
         HIPCHK(hipMemsetAsync(b.arrive.p, 0, kMaxSub * 8, c->stream));
+        // Joins the sub-batch streams back into the context's stream on EVERY exit of this
+        // scope, error returns included: kernels still queued on a sub-stream must finish
+        // before the next run's uploads and memsets on c->stream reuse their buffers.
+        struct JoinGuard {
+            BatchBufs &b;
+            hipStream_t main;
+            int forked = 0;  // sub-streams 1 .. forked-1 wait on the fork
+            ~JoinGuard() {
+                for (int q = 1; q < forked; ++q) {
+                    if (b.join[q] && hipEventRecord(b.join[q], b.ss[q]) == hipSuccess &&
+                        hipStreamWaitEvent(main, b.join[q], 0) == hipSuccess)
+                        continue;
+                    (void)hipStreamSynchronize(b.ss[q]);  // cannot join by event: drain it
+                }
+            }
+        } joins{b, c->stream};
         if (nsub > 1) {
             if (!b.fork) HIPCHK(hipEventCreateWithFlags(&b.fork, hipEventDisableTiming));
             HIPCHK(hipEventRecord(b.fork, c->stream));  // the grids, states and offsets are ready
@@ -272,6 +288,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                 if (!b.ss[q]) HIPCHK(hipStreamCreateWithFlags(&b.ss[q], hipStreamNonBlocking));
                 if (!b.join[q]) HIPCHK(hipEventCreateWithFlags(&b.join[q], hipEventDisableTiming));
                 HIPCHK(hipStreamWaitEvent(b.ss[q], b.fork, 0));
+                joins.forked = q + 1;
             }
         }
         struct Sub {
@@ -333,7 +350,8 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                                             b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
                                             md, u.s));
             }
-            BatchStepArgs su_step = step;  // this sub-batch's counter and flag
+            BatchStepArgs su_step = step;  // this sub-batch's grids, counter and flag
+            su_step.grids = gu;  // indexed by the plot within the sub-batch (fit pivot)
             su_step.arrive = b.arrive.as<unsigned long long>() + (&u - subs);
             su_step.flag = flag;
             {
@@ -365,12 +383,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         }
         for (int q = 0; q < nsub; ++q)
             if (!subs[q].finished) return fail(FICP_EHIP, "batch did not converge within its bound");
-        for (int q = 1; q < nsub; ++q) {
-            HIPCHK(hipEventRecord(b.join[q], b.ss[q]));
-            HIPCHK(hipStreamWaitEvent(c->stream, b.join[q], 0));
-        }
-
-    }
+    }  // JoinGuard: the sub-streams join c->stream here
     // one report kernel copies the plot states into coherent pinned memory and raises a
     // flag the host polls (a pageable D2H copy + stream sync left ~40 us of idle device)
     const size_t sbytes = (size_t)nplots * sizeof(PlotState);

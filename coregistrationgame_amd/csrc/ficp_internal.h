@@ -792,6 +792,9 @@ hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
                              const unsigned long long *range, int64_t range_parts, void *tmp,
                              IterState *st, const LoopCtl &loop, int *host_flag, hipStream_t s,
                              const FitSrc &fit, int fault = 0);
+// whether one k_sel_win launch can decide n rows (its records hold <= W_MAXWG workgroups;
+// larger layers would fail every window call and pay a retry round trip)
+bool select_win_fits(int64_t n);
 // test-only fault injection (ficp_set_fault): block 0 of k_sel_bounds_gather publishes a
 // wrong token, so every gather block times out (ERR_SPIN)
 constexpr int FICP_FAULT_SPIN = 1;

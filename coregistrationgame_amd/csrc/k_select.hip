@@ -186,7 +186,7 @@ inline int gather_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + GT *
 // wave-instruction per ~50 ns per CU (MI355X_MICROARCH.md, global atomics), so flushing
 // 8192 buckets with atomics cost ~15 us and reading + resetting them from one CU ~25 us.
 #ifndef FICP_HIST_ROWS
-#define FICP_HIST_ROWS 4096  // 256 x 4096 rows: +0.5 % at C3 over 128 x 8192 (tools/r3_iter23.sh)
+#define FICP_HIST_ROWS 4096  // 256 x 4096 rows: +0.5 % at C3 over 128 x 8192 (tools/ab_bench.sh, round 3)
 #endif
 #ifndef FICP_HBMAX
 #define FICP_HBMAX 256
@@ -1075,7 +1075,7 @@ __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
     // FICP_BOUNDS_PRELOAD=1: every thread loads its 16 buckets with the chunk totals (one
     // round of loads, 160 KB) instead of only the active chunks after U1 (a second,
     // dependent round): 136 VGPRs for the gather blocks too, measured 4-5 % slower at C3
-    // (8,140 vs 8,486-8,555 it/s, tools/r3_iter18.sh)
+    // (8,140 vs 8,486-8,555 it/s, tools/ab_bench.sh, round 3)
     auto load_buckets = [&]() {
 #pragma unroll
         for (int j = 0; j < PER; j += 4) {
@@ -3141,6 +3141,8 @@ hipError_t launch_select_dist_final(const long long *packs, int world, int capd,
     return hipGetLastError();
 }
 
+bool select_win_fits(int64_t n) { return n > 0 && gather_blocks(n) <= W_MAXWG; }
+
 hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
                              const unsigned long long *range, int64_t range_parts, void *tmp,
                              IterState *st, const LoopCtl &loop, int *host_flag, hipStream_t s,
@@ -3183,7 +3185,7 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     //  * FICP_SEL_RB=1: k_sel_reduce_bounds -- the bounds spread over the reduce's
     //    workgroups (each waits only for the totals of the workgroups dispatched before
     //    it), the gather reads [b0, b1] (runs of 4 buckets) at its start.  Measured 2 %
-    //    slower at C3 (8,296-8,319 vs 8,456-8,476 it/s, tools/r3_iter13.sh): the gather's
+    //    slower at C3 (8,296-8,319 vs 8,456-8,476 it/s, tools/ab_bench.sh FICP_SEL_RB=1): the gather's
     //    row loads take as long as the one-workgroup bounds, which they hid, and the
     //    reduce grew by its exchange;
     //  * FICP_SEL_SPLIT=1: k_sel_bounds + k_sel_gather, no in-launch hand-off at all.

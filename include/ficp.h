@@ -41,7 +41,10 @@ extern "C" {
 
 typedef struct ficp_ctx ficp_ctx;
 
-/* Per-run statistics and optional traces (caller-owned arrays, nullable). */
+/* Per-run statistics and optional traces (caller-owned arrays, nullable).
+ * The caller must zero-initialise the struct (`ficp_stats st = {0};` / ctypes default)
+ * and then set the "in" fields: max_trace, the trace pointers and max_trace_idx are read
+ * by every run, and garbage there truncates or overruns the traces. */
 typedef struct ficp_stats {
     int32_t n_nn_calls;      /* out: NN correspondence calls (both stages)            */
     int32_t n_fits;          /* out: fits applied = ICP loop bodies (ficp.py:132-145) */

@@ -36,6 +36,38 @@ def test_launcher_spawns_two_ranks_one_line():
     assert d["config"]["plots_dealt"] == 37   # every plot dealt to exactly one rank
 
 
+def test_eight_rank_rehearsal_1024_plots():
+    """The driver's N=8 launch of the C4 line, rehearsed with gloo: 8 ranks form the
+    process group, the 1024 plots are dealt once each in the serpentine (128 per rank),
+    and the end-of-run all-gather returns all 1024 records in batch order."""
+    r = _run(["--gpus", "8", "--dry-run", "--workload", "batch", "--plots", "1024", "--steps", "2",
+              "--warmup", "0"], timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == d["ranks_seen"] == 8
+    assert d["config"]["plots_dealt"] == 1024
+    assert d["config"]["plots_per_rank"] == [128] * 8
+    assert d["config"]["gather_in_order"] is True
+
+
+def test_serpentine_deal_balances_ragged_plots():
+    """shard.deal_plots on ragged N*M: every plot once, each rank's work within the
+    largest plot of the mean, ids ascending per rank."""
+    import numpy as np
+    from coregistrationgame_amd import shard
+    rng = np.random.default_rng(0)
+    work = rng.integers(1, 10_000, 1024).astype(float) * rng.integers(1, 10_000, 1024)
+    deal = shard.deal_plots(work, 8)
+    ids = np.sort(np.concatenate(deal))
+    assert np.array_equal(ids, np.arange(1024))
+    loads = np.array([work[d].sum() for d in deal])
+    assert loads.max() - loads.min() <= work.max()
+    assert all(np.all(np.diff(d) > 0) for d in deal)
+    assert sorted(len(d) for d in deal) == [128] * 8
+
+
 def test_default_workload_is_batch_above_one_gpu():
     r = _run(["--gpus", "3", "--dry-run", "--steps", "1", "--warmup", "0", "--plots", "10"])
     assert r.returncode == 0, r.stderr[-2000:]

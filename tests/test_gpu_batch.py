@@ -95,6 +95,52 @@ def test_batch_vs_oracle_mixed(oracle, knobs, monkeypatch):
         assert b.stats[p]["k_last"] == otr["k"][-1], p
 
 
+def _far_apart_batch(n_plots=80):
+    """Plots at distinct geo offsets ~km apart (each plot's own CHM bbox centre is its fit
+    pivot), with empty CHM layers in the first sub-batch (pivot (0, 0))."""
+    from coregistrationgame_amd import synth
+    srcs, tgts = [], []
+    for p in range(n_plots):
+        pl = synth.make_plot(600, 900, 0.8, seed=40_000 + p, md=3)
+        shift = np.array([3_000.0 * (p % 9), 7_000.0 * (p // 9)])
+        s, t = pl.source.copy(), pl.target.copy()
+        s[:, :2] += shift
+        t[:, :2] += shift
+        srcs.append(s)
+        tgts.append(t)
+    for p in (2, 11):  # empty CHM layers in the first half
+        tgts[p] = tgts[p][:0]
+    return srcs, tgts
+
+
+def test_batch_sub_batches_far_apart_bit_identical(oracle, monkeypatch):
+    """with two sub-batches, the fused selection's fit must use the
+    pivot of its own plot, not of the plot at the same position in the first sub-batch.
+    One stream vs two streams must be bit-identical; the fused step and the separate
+    fit/update launches (FICP_BATCH_FUSE=0) must take the same NN calls and k; a sample
+    of plots in the second sub-batch equals the oracle."""
+    from coregistrationgame_amd import FractionalICPBatch
+    srcs, tgts = _far_apart_batch()
+    outs = {}
+    for name, knobs in (("two", {"FICP_BATCH_STREAMS": "2"}), ("one", {"FICP_BATCH_STREAMS": "1"}),
+                        ("unfused", {"FICP_BATCH_STREAMS": "2", "FICP_BATCH_FUSE": "0"})):
+        for k, v in knobs.items():
+            monkeypatch.setenv(k, v)
+        b = FractionalICPBatch(srcs, tgts)
+        outs[name] = (b.run(), b.stats)
+        monkeypatch.delenv("FICP_BATCH_FUSE", raising=False)
+    (f2, s2), (f1, s1), (fu, su) = outs["two"], outs["one"], outs["unfused"]
+    for p in range(len(srcs)):
+        np.testing.assert_array_equal(bits(f2[p]), bits(f1[p]), err_msg=str(p))
+        assert s2[p]["n_nn_calls"] == su[p]["n_nn_calls"], p
+        assert s2[p]["k_last"] == su[p]["k_last"], p
+        np.testing.assert_allclose(f2[p][:, :2], fu[p][:, :2], atol=1e-6, rtol=0, err_msg=str(p))
+    for p in (40, 42, 51, 79):
+        ofinal, otr = oracle.run(srcs[p], tgts[p], nthreads=8)
+        np.testing.assert_allclose(f2[p][:, :2], ofinal[:, :2], atol=1e-6, rtol=0, err_msg=str(p))
+        assert s2[p]["n_nn_calls"] == len(otr["k"]), p
+
+
 def test_batch_matches_single_runs():
     """Batch == one FractionalICP per plot on the GPU (same NN calls, same k, same XY)."""
     from coregistrationgame_amd import FractionalICP, FractionalICPBatch, synth

@@ -38,6 +38,12 @@ def load_run(name):
     return {k: z[k] for k in z.files}
 
 
+def allow_refl(run):
+    """The run fixture's allow_reflection kwarg (ficp.py:13); fixtures from before round 4
+    have none and ran with the default False."""
+    return bool(int(run.get("kwargs_allow_reflection", 0)))
+
+
 RUN_FIXTURES = sorted(p.stem[4:] for p in GOLDEN.glob("run_*.npz") if p.stem != "run_real_stand10")
 
 # k parity is pinnable only where the reference's own FRMSD curve separates the best k

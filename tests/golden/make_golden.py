@@ -19,6 +19,7 @@ Fixture families:
   apply.npz   apply_transform_2d_xy_only (ficp.py:112-119), D = 2, 3, 5
   run_*.npz   FractionalICP.run() (ficp.py:149-154) per-NN-call traces: lambda, k,
               frac, FRMSD-curve gap, NN idx, T of every fit, final source
+              (run_refl_*: allow_reflection=True, reflected fits included)
   empty.npz   the empty-input contracts (ficp.py:56-57, 66-68, 75-77, 125-126)
 """
 from __future__ import annotations
@@ -302,6 +303,7 @@ def save_run(name, src, tgt, **kw):
         lambda_final=np.float64(icp.lambda_val),
         kwargs_threshold=np.float64(kw.get("threshold", 1e-6)),
         kwargs_max_iterations=np.int64(kw.get("max_iterations", 1000)),
+        kwargs_allow_reflection=np.int64(bool(kw.get("allow_reflection", False))),
     )
     np.savez_compressed(HERE / f"run_{name}.npz", **d)
     print(f"run {name}: n={len(src)} m={len(tgt)} md={icp.match_dims} calls={n_calls} "
@@ -350,6 +352,43 @@ def make_runs():
     print(f"real plots: {len(plots)} plots vs {len(tgt)} CHM stems")
 
 
+def mirrored_strip(n, md, seed, geo):
+    """CHM stems along a narrow strip (x within +-0.6 m, y over 400 m) and a tree layer
+    that is their mirror image in x, slightly rotated and shifted: the trees' nearest
+    stems are mostly their own originals, so the SVD of the cross-covariance returns a
+    reflection (det(Vt^T U^T) < 0, ficp.py:99-103)."""
+    rng = np.random.default_rng(seed)
+    tgt = np.column_stack([rng.uniform(-0.6, 0.6, n), np.sort(rng.uniform(0, 400, n)),
+                           rng.uniform(5, 30, n)])[:, :md]
+    src = tgt.copy()
+    src[:, 0] = -src[:, 0]
+    th = 0.004
+    R = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+    c = np.array([0.0, 200.0])
+    src[:, :2] = (src[:, :2] - c) @ R.T + c + [0.15, -0.1] + rng.normal(0, 0.03, (n, 2))
+    if geo:
+        src[:, :2] += synth.GEO_OFFSET
+        tgt[:, :2] += synth.GEO_OFFSET
+    return src, tgt
+
+
+def make_refl_runs():
+    """run() with allow_reflection=True (ficp.py:13, 101-103): two mirrored strips whose
+    fits are reflections, and a regular plot (rotations) under the same flag."""
+    cases = []
+    s, t = mirrored_strip(160, 3, 61, geo=False)
+    cases.append(("refl_strip3", s, t))
+    s, t = mirrored_strip(220, 2, 62, geo=True)
+    cases.append(("refl_strip2_geo", s, t))
+    p = synth.make_plot(n=500, m=600, f=0.8, seed=63, md=3, geo=True)
+    cases.append(("refl_allow_plot3", p.source, p.target))
+    for name, s, t in cases:
+        icp = trace_run(s, t, allow_reflection=True)
+        dets = [float(np.linalg.det(T[:2, :2])) for T in icp.tr_T]
+        print(f"  {name}: fits with det < 0: {sum(d < 0 for d in dets)} of {len(dets)}")
+        save_run(name, s, t, allow_reflection=True)
+
+
 def make_empty():
     out = {}
     src = synth.make_cloud(n=5, seed=42)
@@ -369,7 +408,7 @@ def make_empty():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["nn", "frac", "fit", "apply", "runs", "empty"]
+    which = sys.argv[1:] or ["nn", "frac", "fit", "apply", "runs", "refl", "empty"]
     for w in which:
         {"nn": make_nn, "frac": make_frac, "fit": make_fit, "apply": make_apply,
-         "runs": make_runs, "empty": make_empty}[w]()
+         "runs": make_runs, "refl": make_refl_runs, "empty": make_empty}[w]()

@@ -4,7 +4,7 @@ FractionalICP(source, target).run() ends (ficp.py:122-154)."""
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, K_GAP_PIN, RUN_FIXTURES, load_run, pinned_prefix
+from conftest import GOLDEN, K_GAP_PIN, RUN_FIXTURES, allow_refl, load_run, pinned_prefix
 
 pytestmark = pytest.mark.gpu
 
@@ -20,11 +20,11 @@ def test_batch_golden_runs():
     runs = {name: load_run(name) for name in RUN_FIXTURES}
     groups = {}
     for name, r in runs.items():
-        key = (float(r["kwargs_threshold"]), int(r["kwargs_max_iterations"]))
+        key = (float(r["kwargs_threshold"]), int(r["kwargs_max_iterations"]), allow_refl(r))
         groups.setdefault(key, []).append(name)
-    for (thr, mx), names in groups.items():
+    for (thr, mx, refl), names in groups.items():
         b = FractionalICPBatch([runs[n]["src"] for n in names], [runs[n]["tgt"] for n in names],
-                               threshold=thr, max_iterations=mx)
+                               threshold=thr, max_iterations=mx, allow_reflection=refl)
         finals = b.run()
         for j, name in enumerate(names):
             r = runs[name]

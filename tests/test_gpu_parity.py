@@ -9,7 +9,7 @@ final XY within 1e-6 abs (north star); Z and extra columns bit-identical.
 import numpy as np
 import pytest
 
-from conftest import (K_GAP_PIN, RUN_FIXTURES, assert_T_close, load_cases, load_run,
+from conftest import (K_GAP_PIN, RUN_FIXTURES, allow_refl, assert_T_close, load_cases, load_run,
                       pinned_prefix)
 
 pytestmark = pytest.mark.gpu
@@ -155,6 +155,39 @@ def test_selection_selfcheck():
         assert r.returncode == 0, r.stdout + r.stderr
 
 
+WINCHECK_CASES = [("1000000", "0", "3.0"), ("1000000", "0", "0.95"), ("1000000", "0", "1.3"),
+                  ("100000", "1", "3.0"), ("200000", "2", "3.0"), ("300000", "3", "0.95"),
+                  ("1000000", "4", "3.0"), ("1000000", "5", "3.0"), ("3000", "0", "3.0"),
+                  ("8000000", "0", "3.0"), ("1000000", "6", "3.0"), ("1000000", "7", "3.0"),
+                  ("1000000", "8", "0.95")]
+
+
+def test_window_selection_selfcheck():
+    """tools/wincheck: the one-launch window selection (k_select.hip k_sel_win) on the ten
+    residual distributions of tools/selcheck plus non-finite rows, hundreds of window rows
+    in one workgroup and exact ties on a grid, for 5 window sizes x 7 placements of the
+    previous threshold (at the true one, just inside / outside both window edges, 512
+    widths away): every launch either decides k, FRMSD, the threshold pair and the fused
+    fit equal to a CPU stable sort + scan and to the full path, or falls back leaving the
+    state untouched, after which the full path's result is bit-identical (ficp.py:73-86)."""
+    import re
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "tools" / "wincheck"
+    if not exe.exists():
+        pytest.skip("tools/wincheck not built (make -C coregistrationgame_amd/csrc wincheck)")
+    decided = 0
+    for args in WINCHECK_CASES:
+        r = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout[-4000:] + r.stderr
+        m = re.search(r"window=(\d+) fallback=(\d+) bad=0", r.stdout)
+        assert m, r.stdout[-2000:]
+        decided += int(m.group(1))
+        if args[1] == "0" and args[0] == "1000000":
+            assert int(m.group(1)) >= 3, r.stdout  # the checker reaches the window's proof
+    assert decided >= 20
+
+
 # ------------------------------------------------------------------ sort / fraction
 def test_argsort_stable(ctx):
     rng = np.random.default_rng(3)
@@ -257,7 +290,8 @@ def test_run_trace(name, nn_mode, monkeypatch):
     if nn_mode == "auto_loop":
         monkeypatch.setenv("FICP_SMALL", "0")
     icp = FractionalICP(r["src"], r["tgt"], threshold=float(r["kwargs_threshold"]),
-                        max_iterations=int(r["kwargs_max_iterations"]), nn_mode=nn_mode.split("_")[0])
+                        max_iterations=int(r["kwargs_max_iterations"]), nn_mode=nn_mode.split("_")[0],
+                        allow_reflection=allow_refl(r))
     final = icp.run(trace=True, trace_idx=True)
     tr = icp.last_stats
     fits = len(r["src"]) <= 1024 and len(r["tgt"]) <= 4096 and len(r["src"]) * len(r["tgt"]) <= 1 << 18
@@ -671,3 +705,109 @@ def test_join_stand_real_vs_oracle(oracle):
             alive.remove(r)
         assert records[int(pid)]["flip"] is False
     assert sorted(t.tree_id for t in chm.trees) == alive
+
+
+# ------------------------------------------------------------------ allow_reflection=True
+REFL_FIXTURES = [n for n in RUN_FIXTURES if n.startswith("refl_")]
+
+
+@pytest.mark.parametrize("knobs", [{}, {"FICP_SMALL": "0"}, {"FICP_SMALL": "0", "FICP_FUSE_FIT": "0"},
+                                   {"FICP_SMALL": "0", "FICP_SEL_WIN": "0"}],
+                         ids=["small", "loop", "loop_fit_pass", "loop_no_window"])
+@pytest.mark.parametrize("name", REFL_FIXTURES)
+def test_run_allow_reflection_golden(name, knobs, monkeypatch):
+    """run(allow_reflection=True) (ficp.py:13, 101-103) against the reference's own runs:
+    mirrored strips whose first fit is a reflection (det R = -1) and a regular plot under
+    the flag.  One-workgroup kernel, multi-kernel loop (fused fit, separate fit pass,
+    window selection off).  Per pinned call k and NN idx exact, T within 1e-6 in action,
+    final XY within 1e-6."""
+    from coregistrationgame_amd import FractionalICP
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    r = load_run(name)
+    assert allow_refl(r)
+    icp = FractionalICP(r["src"], r["tgt"], allow_reflection=True)
+    final = icp.run(trace=True, trace_idx=True)
+    tr = icp.last_stats
+    fits = len(r["src"]) <= 1024 and len(r["tgt"]) <= 4096 and len(r["src"]) * len(r["tgt"]) <= 1 << 18
+    assert tr["path"] == ("small" if fits and not knobs else "loop")
+    np.testing.assert_allclose(final[:, :2], r["final"][:, :2], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(bits(final[:, 2:]), bits(r["final"][:, 2:]))
+    scale = 1.0 + np.abs(r["src"][:, :2]).max()
+    first = pinned_prefix(r["gap"], r["frmsd"], scale)
+    np.testing.assert_array_equal(tr["k"][:first], r["k"][:first])
+    np.testing.assert_array_equal(tr["idx"][:first], r["idx"][:first])
+    nf = min(first, len(r["T"]))
+    assert_T_close(tr["T"][:nf], r["T"][:nf], r["src"], msg=name)
+    ref_dets = np.linalg.det(r["T"][:nf, :2, :2])
+    np.testing.assert_array_equal(np.sign(np.linalg.det(np.asarray(tr["T"]).reshape(-1, 3, 3)[:nf, :2, :2])), np.sign(ref_dets))
+    if name.startswith("refl_strip"):
+        assert ref_dets[0] < 0  # the fixture really exercises the reflection branch
+
+
+def _mirrored_strip(n, seed, th, noise, fout, md=3):
+    """n CHM stems on a 1.2 m-wide strip (4 m apart on average along it) and a tree layer
+    that is their mirror image in x, rotated by th about the strip's centre, shifted, with
+    noise and a fraction fout of outliers pushed sideways: the first fit is a reflection."""
+    rng = np.random.default_rng(seed)
+    L = 4.0 * n
+    tgt = np.column_stack([rng.uniform(-0.6, 0.6, n), rng.uniform(0, L, n), rng.uniform(5, 30, n)])[:, :md]
+    src = tgt.copy()
+    src[:, 0] = -src[:, 0]
+    c = np.array([0.0, L / 2])
+    R = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+    src[:, :2] = (src[:, :2] - c) @ R.T + c + [0.15, -0.1] + rng.normal(0, noise, (n, 2))
+    k = int(fout * n)
+    src[:k, 0] += rng.uniform(-20, 20, k)
+    src[:, :2] += [5.0e5, 6.5e6]
+    tgt[:, :2] += [5.0e5, 6.5e6]
+    return src, tgt
+
+
+@pytest.mark.parametrize("case", ["strip3_200k", "strip2_200k", "plot3_300k"])
+def test_run_allow_reflection_large_vs_oracle(case, oracle, monkeypatch):
+    """run(allow_reflection=True) on the production loop at sizes where the half-step
+    lookahead and the window selection run (>= 64k rows), vs the pinned oracle (whose
+    reflection branch the run_refl_* fixtures pin): the NN-call count, k of every call the
+    oracle's curve separates (conftest.K_GAP_PIN_LARGE), the sign of det R of every fit,
+    final XY within 1e-6.  The fused fit and the separate fit pass both."""
+    from conftest import K_GAP_PIN_LARGE
+    from coregistrationgame_amd import FractionalICP, _lib, synth
+    if case == "plot3_300k":
+        p = synth.make_plot(300_000, 300_000, 0.7, seed=300_001, md=3)
+        src, tgt = p.source, p.target
+    else:
+        src, tgt = _mirrored_strip(200_000, 5, 2e-7, 0.05, 0.2, md=3 if case[5] == "3" else 2)
+    ofinal, otr = oracle.run(src, tgt, allow_reflection=True, nthreads=16)
+    odet = np.sign(np.linalg.det(np.asarray(otr["T"]).reshape(-1, 3, 3)[:, :2, :2]))
+    if case != "plot3_300k":
+        assert odet[0] < 0
+    pinned = otr["gap"] > K_GAP_PIN_LARGE
+    for knobs in ({}, {"FICP_FUSE_FIT": "0"}):
+        monkeypatch.delenv("FICP_FUSE_FIT", raising=False)
+        for k, v in knobs.items():
+            monkeypatch.setenv(k, v)
+        icp = FractionalICP(src, tgt, allow_reflection=True)
+        final = icp.run(trace=True)
+        st = icp.last_stats
+        assert st["n_nn_calls"] == otr["n_calls"], knobs
+        np.testing.assert_array_equal(np.asarray(st["k"])[pinned], otr["k"][pinned])
+        np.testing.assert_array_equal(np.sign(np.linalg.det(np.asarray(st["T"]).reshape(-1, 3, 3)[:, :2, :2])), odet)
+        np.testing.assert_allclose(final[:, :2], ofinal[:, :2], atol=1e-6, rtol=0, err_msg=str(knobs))
+    # the untraced production loop (fused selection, window path where eligible)
+    monkeypatch.delenv("FICP_FUSE_FIT", raising=False)
+    ctx = _lib.Context(0, _lib.NN_GRID)
+    try:
+        md = 3 if src.shape[1] >= 3 and tgt.shape[1] >= 3 else 2
+        ctx.set_target(tgt, md)
+        out = np.array(src)
+        st = ctx.run(out, [3.0, 0.95 if md == 3 else 1.3], 1e-6, 1000, True)
+        ps = ctx.path_stats()
+    finally:
+        ctx.close()
+    assert st["n_nn_calls"] == otr["n_calls"]
+    assert st["k_last"] == otr["k"][-1]
+    np.testing.assert_allclose(out[:, :2], ofinal[:, :2], atol=1e-6, rtol=0)
+    print(f"{case}: window calls {ps['win_calls']}, retries {ps['win_retries']}")
+    if case == "plot3_300k":
+        assert ps["win_calls"] >= 1, ps

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import conftest
-from conftest import K_GAP_PIN, RUN_FIXTURES, load_cases, load_run, pinned_prefix, assert_T_close
+from conftest import K_GAP_PIN, RUN_FIXTURES, allow_refl, load_cases, load_run, pinned_prefix, assert_T_close
 
 
 @pytest.mark.parametrize("method", ["brute", "kdtree"])
@@ -64,7 +64,8 @@ def test_apply_bit_exact(oracle):
 def test_run_trace(oracle, name):
     r = load_run(name)
     final, tr = oracle.run(r["src"], r["tgt"], threshold=float(r["kwargs_threshold"]),
-                           max_iterations=int(r["kwargs_max_iterations"]), trace_idx=True)
+                           max_iterations=int(r["kwargs_max_iterations"]), trace_idx=True,
+                           allow_reflection=allow_refl(r))
     # final XY within 1e-6 abs (north star), every other column bit-identical
     np.testing.assert_allclose(final[:, :2], r["final"][:, :2], atol=1e-6, rtol=0)
     np.testing.assert_array_equal(final[:, 2:], r["final"][:, 2:])

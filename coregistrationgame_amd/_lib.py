@@ -135,6 +135,8 @@ def lib():
         "ficp_apply_xy": ([_vp, _dp, _i64, _i64, _dp, _dp], C.c_int),
         "ficp_run": ([_vp, _dp, _i64, _i64, _i32, _dp, C.c_double, _i32, _i32, C.POINTER(Stats)],
                      C.c_int),
+        "ficp_run_into": ([_vp, _dp, _dp, _i64, _i64, _i32, _dp, C.c_double, _i32, _i32,
+                           C.POINTER(Stats)], C.c_int),
         "ficp_run_device": ([_vp, _vp, _vp, _vp, _i64, _i32, _dp, C.c_double, _i32, _i32,
                              C.POINTER(Stats)], C.c_int),
         "ficp_run_batch": ([_vp, _i32, _ip64, _dp, _i64, _ip64, _dp, _i64, _i32, _i32, _dp, C.c_double,
@@ -329,6 +331,21 @@ class Context:
         _check(lib().ficp_run(self.h, _p(src_inout), len(src_inout), src_inout.shape[1], len(lam), _p(lam),
                               float(threshold), int(max_iterations), int(bool(allow_reflection)), C.byref(st)))
         return _stats_dict(st, keep, len(src_inout))
+
+    def run_into(self, src: np.ndarray, out: np.ndarray, lambdas, threshold: float, max_iterations: int,
+                 allow_reflection: bool, trace: bool = False, trace_idx: bool = False, max_trace: int = 4096):
+        """Runs the stages on C-contiguous float64 (n, ld) rows `src` into `out` (same shape;
+        src is not written).  A pooled pinned `out` (host_array) takes the result in one
+        direct device-to-host copy."""
+        for a in (src, out):
+            assert a.dtype == np.float64 and a.flags.c_contiguous and a.ndim == 2
+        assert src.shape == out.shape
+        lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+        st, keep = _make_stats(len(src), trace, trace_idx, max_trace)
+        _check(lib().ficp_run_into(self.h, _p(src), _p(out), len(src), src.shape[1], len(lam), _p(lam),
+                                   float(threshold), int(max_iterations), int(bool(allow_reflection)),
+                                   C.byref(st)))
+        return _stats_dict(st, keep, len(src))
 
     def run_device(self, x_ptr: int, y_ptr: int, z_ptr: int, n: int, lambdas, threshold: float,
                    max_iterations: int, allow_reflection: bool = False):

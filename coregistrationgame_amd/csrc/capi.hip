@@ -221,8 +221,10 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             bool want_keys, int warm = 0, const int *skip = nullptr,
             const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true,
             const int *reuse = nullptr, bool store_key = true, bool multi = false,
-            const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr) {
+            const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr,
+            const NNWin *win = nullptr) {
     NNArgs a{};
+    if (win) a.win = *win;  // k_nn_grid_q: the window selection's fused pass
     a.fin_orig = fin_orig;
     a.fin_x = fin_x;
     a.fin_y = fin_y;
@@ -570,6 +572,26 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // part A of iteration i: the fit and the NN call; part B: the selection (and, not
     // fused, the loop step and the flag copy)
     int64_t last_a = -1;  // the last iteration whose fit + NN were enqueued
+    // the window path (k_sel_win, one launch instead of four) for the calls whose previous
+    // flag carried kFlagWinNext; FICP_SEL_WIN=0 turns it off
+    const char *wv = getenv("FICP_SEL_WIN");
+    // (the work-order arrays: library buffers, 16-B aligned for the window pass's loads)
+    const bool use_win = fused && fuse_fit && keys_from_r && worig && select_win_fits(n) &&
+                         !(wv && atoi(wv) == 0);
+    // ... and its pass fused into the certified NN kernel of the same call (k_nn_grid_q,
+    // calls >= nn_multi_from): the NN workgroups classify their rows as they write them
+    // and one workgroup decides (k_sel_win_tail).  FICP_WIN_NN=0: k_sel_win's own pass.
+    const char *wn = getenv("FICP_WIN_NN");
+    const bool win_nn = use_win && use_grid(c, n) && select_win_nn_blocks(n) > 0 && !(wn && atoi(wn) == 0);
+    const int64_t win_nn_from = std::max<int64_t>(nn_multi_from, 1);
+    NNWin nnw{};
+    if (win_nn) {
+        nnw.st = dst;
+        nnw.orig = worig;
+        nnw.o = select_win_out(c->sel_tmp.p, n);
+        nnw.px = c->pivot_x;
+        nnw.py = c->pivot_y;
+    }
     auto enq_a = [&](int64_t i) -> int {
         if (!(fused && fuse_fit)) {
             ProfScope ps(c, P_FIT, "fit");
@@ -579,19 +601,19 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         // (a launch queued behind the loop's end writes the caller-order XY: fin_*)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
                     false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from,
-                    worig, sx, sy));
+                    worig, sx, sy, (win_nn && i >= win_nn_from) ? &nnw : nullptr));
         last_a = i;
         return FICP_OK;
     };
-    // the window path (k_sel_win, one launch instead of four) for the calls whose previous
-    // flag carried kFlagWinNext; FICP_SEL_WIN=0 turns it off
-    const char *wv = getenv("FICP_SEL_WIN");
-    // (the work-order arrays: library buffers, 16-B aligned for the window pass's loads)
-    const bool use_win = fused && fuse_fit && keys_from_r && worig && select_win_fits(n) &&
-                         !(wv && atoi(wv) == 0);
     auto enq_b = [&](int64_t i, bool win) -> int {
         const int slot = (int)(i % kLoopRing);
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
+        if (win && win_nn && i >= win_nn_from) {  // call i's NN ran the pass
+            ProfScope ps(c, P_SORT, "select");
+            HIPCHK(launch_select_win_tail(n, c->sel_tmp.p, dst, lc, &c->h_flags[slot], c->stream, fsrc,
+                                          c->fault));
+            return FICP_OK;
+        }
         if (win) {
             ProfScope ps(c, P_SORT, "select");
             HIPCHK(launch_select_win(c->r.as<double>(), worig, n, range_ptr(c),
@@ -1117,13 +1139,25 @@ int ficp_apply_xy(ficp_ctx *c, const double *pts, int64_t n, int64_t ld, const d
 int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
              const double *lambdas, double threshold, int32_t max_iterations,
              int32_t allow_reflection, ficp_stats *stats) {
+    return ficp_run_into(c, src, src, n, ld, nstages, lambdas, threshold, max_iterations,
+                         allow_reflection, stats);
+}
+
+int ficp_run_into(ficp_ctx *c, const double *src, double *out, int64_t n, int64_t ld,
+                  int32_t nstages, const double *lambdas, double threshold,
+                  int32_t max_iterations, int32_t allow_reflection, ficp_stats *stats) {
     CHK(check_ctx(c));
     if (!c->has_target) return fail(FICP_ESTATE, "no target set");
-    if (n < 0 || (n > 0 && (!src || ld < c->md)) || nstages < 0 || (nstages > 0 && !lambdas))
+    if (n < 0 || (n > 0 && (!src || !out || ld < c->md)) || nstages < 0 || (nstages > 0 && !lambdas))
         return fail(FICP_EINVAL, "bad arguments");
-    if (n == 0 || c->m == 0)
+    auto copy_rows = [&]() {  // out = src: the columns the run leaves alone
+        if (out != src) ficp_host_copy(out, src, n * ld * 8);
+    };
+    if (n == 0 || c->m == 0) {
+        copy_rows();
         return run_core(c, nullptr, nullptr, nullptr, 0, nstages, lambdas, threshold,
                         max_iterations, allow_reflection, stats);
+    }
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::time_point a, clk::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
@@ -1139,9 +1173,10 @@ int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
         CHK(run_small(c, c->stage.as<double>(), ld, nullptr, nullptr, nullptr, n, nstages, lambdas,
                       threshold, max_iterations, allow_reflection, stats, &xy));
         const auto t2 = clk::now();
+        copy_rows();
         for (int64_t i = 0; i < n; ++i) {  // columns 0, 1 only (ficp.py:114-118)
-            src[i * ld] = xy[2 * i];
-            src[i * ld + 1] = xy[2 * i + 1];
+            out[i * ld] = xy[2 * i];
+            out[i * ld + 1] = xy[2 * i + 1];
         }
         if (stats) {
             stats->host_ms[0] = ms(t0, t1);
@@ -1151,16 +1186,25 @@ int ficp_run(ficp_ctx *c, double *src, int64_t n, int64_t ld, int32_t nstages,
         }
         return FICP_OK;
     }
+    // the rows stay in c->stage (upload_rows) for the whole run: at the end the moved XY
+    // replace their columns 0, 1 there and the rows come back in one D2H, straight into
+    // `out` when it is page-locked (the library's pooled blocks) -- no host-side column
+    // write-back, and the caller needs no copy of the rows for the run to move
     CHK(upload_rows(c, src, n, ld, c->md, c->sx, c->sy, &c->sz));
     const auto t1 = clk::now();
     CHK(run_core(c, c->sx.as<double>(), c->sy.as<double>(),
                  c->md == 3 ? c->sz.as<double>() : nullptr, n, nstages, lambdas, threshold,
                  max_iterations, allow_reflection, stats));
     const auto t2 = clk::now();
-    CHK(c->stage2.ensure(n * 16));
-    HIPCHK(launch_interleave_xy(c->sx.as<double>(), c->sy.as<double>(), n, c->stage2.as<double>(),
-                                c->stream));
-    CHK(d2h_xy_columns(c, c->stage2.as<double>(), n, src, ld));
+    HIPCHK(launch_put_xy_rows(c->sx.as<double>(), c->sy.as<double>(), n, ld, c->stage.as<double>(),
+                              c->stream));
+    const size_t bytes = (size_t)n * (size_t)ld * 8;
+    if (host_pinned(out)) {
+        HIPCHK(hipMemcpyAsync(out, c->stage.p, bytes, hipMemcpyDeviceToHost, c->stream));
+        CHK(sync(c));
+    } else {
+        CHK(d2h_staged(c, out, c->stage.p, bytes));
+    }
     if (stats) {
         stats->host_ms[0] = ms(t0, t1);
         stats->host_ms[1] = ms(t1, t2);

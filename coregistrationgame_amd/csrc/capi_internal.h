@@ -12,7 +12,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -301,23 +305,110 @@ inline int upload_rows(ficp_ctx *c, const double *rows, int64_t n, int64_t ld, i
                                c1.as<double>(), c2 ? c2->as<double>() : nullptr, c->stream));
     return FICP_OK;
 }
-// f(i0, i1) over [0, n) on up to 8 host threads (large host-side copies of results)
+// f(i0, i1) over [0, n) on the caller and a persistent pool of host threads (large host
+// copies: the constructor's layer copies, staged results).  Spawning threads per call cost
+// ~20-40 us each; the pool's workers sleep on a condition variable between calls.
+// FICP_HOST_THREADS (default 16, the GPU box's per-job CPU share) caps the threads; a call
+// made while another one owns the pool runs on its caller alone.
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool *p = new HostPool();  // never destroyed: workers outlive exit paths
+        return *p;
+    }
+    int threads() const { return nthreads_; }
+    // false: the pool is busy (run serially)
+    bool run(int parts, const std::function<void(int)> &job) {
+        std::unique_lock<std::mutex> own(busy_, std::try_to_lock);
+        if (!own.owns_lock()) return false;
+        unsigned long long gen;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &job;
+            parts_ = parts;
+            left_ = parts;
+            gen = ++gen_;
+            claim_.store((gen & 0xffffffffULL) << 32);  // (generation, next part): a late worker claims nothing
+        }
+        cv_.notify_all();
+        work(&job, gen, parts);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [&] { return left_ == 0; });
+        job_ = nullptr;
+        return true;
+    }
+
+  private:
+    HostPool() {
+        const char *e = getenv("FICP_HOST_THREADS");
+        nthreads_ = std::max(1, std::min(64, e ? atoi(e) : 16));
+        for (int t = 1; t < nthreads_; ++t) std::thread([this] { loop(); }).detach();
+    }
+    // claims parts of generation gen until none is left (or a newer generation began)
+    void work(const std::function<void(int)> *j, unsigned long long gen, int parts) {
+        for (;;) {
+            unsigned long long c = claim_.load();
+            int i;
+            do {
+                if ((c >> 32) != (gen & 0xffffffffULL) || (int)(c & 0xffffffffULL) >= parts) return;
+                i = (int)(c & 0xffffffffULL);
+            } while (!claim_.compare_exchange_weak(c, c + 1));
+            (*j)(i);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_all();
+        }
+    }
+    void loop() {
+        unsigned long long seen = 0;
+        for (;;) {
+            const std::function<void(int)> *j;
+            unsigned long long gen;
+            int parts;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen && job_ != nullptr; });
+                seen = gen = gen_;
+                j = job_;
+                parts = parts_;
+            }
+            work(j, gen, parts);
+        }
+    }
+    int nthreads_ = 1;
+    std::mutex busy_, m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    int parts_ = 0, left_ = 0;
+    std::atomic<unsigned long long> claim_{0};
+    unsigned long long gen_ = 0;
+};
+
 template <typename F>
 inline void host_parallel(int64_t n, F f) {
     const int64_t per_min = 1 << 17;
-    const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, n / per_min));
+    HostPool &hp = HostPool::get();
+    const int nt = (int)std::min<int64_t>(hp.threads(), std::max<int64_t>(1, n / per_min));
     if (nt <= 1) {
         f((int64_t)0, n);
         return;
     }
-    std::vector<std::thread> th;
     const int64_t per = (n + nt - 1) / nt;
-    for (int t = 1; t < nt; ++t) {
+    const std::function<void(int)> job = [&](int t) {
         const int64_t a = std::min(n, t * per), b = std::min(n, a + per);
-        th.emplace_back([=]() { f(a, b); });
+        if (b > a) f(a, b);
+    };
+    if (!hp.run(nt, job)) f((int64_t)0, n);
+}
+
+// page-locked host memory the DMA engines reach directly (hipHostMalloc'd blocks, e.g.
+// the Python host pool's); pageable memory is reported as not pinned
+inline bool host_pinned(const void *p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
     }
-    f(0, std::min(n, per));
-    for (auto &x : th) x.join();
+    return at.type == hipMemoryTypeHost;
 }
 
 // device bytes -> the caller's host memory through the pinned staging buffer

@@ -275,6 +275,30 @@ struct GridView {
 typedef float gap_t;
 
 // Per-launch NN arguments.
+// The window selection's per-workgroup outputs (k_select.hip SelWS's window part): each
+// pass workgroup's record (kWinRec words), its window rows (at most kWinSlot: key, r, caller
+// index, work row) and the coarse buckets (agent-scope atomics, read and zeroed by the tail).
+constexpr int kWinSlot = 64, kWinRec = 16;
+struct WinPassOut {
+    unsigned long long *wrec;
+    unsigned long long *wsk;
+    double *wsr;
+    uint32_t *wso, *wsp;
+    unsigned *gcc;
+    unsigned long long *gcf;
+};
+struct IterState;
+// The window pass fused into the certified NN kernel (k_grid_nn.hip nn_win_pass): when the
+// loop state allows the window path (win_ok), each k_nn_grid_q workgroup classifies its own
+// kWinNNRows rows right after writing them, and k_sel_win_tail (one workgroup) decides.
+constexpr int kWinNNRows = 1024;
+struct NNWin {
+    const IterState *st;        // nullable: no fused pass
+    const uint32_t *orig;       // caller index per work row (the selection's tie-break)
+    WinPassOut o;
+    double px, py;              // fit pivot
+};
+
 struct NNArgs {
     double *sx;                 // source x (updated in place when T != nullptr)
     double *sy;
@@ -313,6 +337,7 @@ struct NNArgs {
     // fin_x[fin_orig[p]] = sx[p] (k_scatter_xy's work, no launch or host round trip of its own)
     const uint32_t *fin_orig;
     double *fin_x, *fin_y;
+    NNWin win;                  // k_nn_grid_q: the fused window pass (win.st nullable)
 };
 
 // k_scatter_xy's work for rows [p0, p0 + cnt) of the work order
@@ -672,6 +697,8 @@ hipError_t launch_nn_brute(const NNArgs &a, const double *tx, const double *ty,
                            int32_t *part_idx, hipStream_t s, bool reduce_range = true);
 hipError_t launch_deinterleave(const double *rows, int64_t n, int64_t ld, int ncols,
                                double *c0, double *c1, double *c2, hipStream_t s);
+hipError_t launch_put_xy_rows(const double *x, const double *y, int64_t n, int64_t ld, double *rows,
+                              hipStream_t s);
 hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, double *out_xy,
                                 hipStream_t s);
 // Two-level bucket sort of points by a grid key (k_bsort.hip).  mode 0: key = cell id
@@ -795,6 +822,13 @@ hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
 // whether one k_sel_win launch can decide n rows (its records hold <= W_MAXWG workgroups;
 // larger layers would fail every window call and pay a retry round trip)
 bool select_win_fits(int64_t n);
+// the fused form (k_grid_nn.hip nn_win_pass + k_sel_win_tail): NN workgroups of n rows
+// (0: too many for one tail), the pass's output arrays inside the selection workspace, and
+// the tail's launch (the same outputs, flags and fallback as launch_select_win)
+int select_win_nn_blocks(int64_t n);
+WinPassOut select_win_out(void *tmp, int64_t n);
+hipError_t launch_select_win_tail(int64_t n, void *tmp, IterState *st, const LoopCtl &loop,
+                                  int *host_flag, hipStream_t s, const FitSrc &fit, int fault = 0);
 // test-only fault injection (ficp_set_fault): block 0 of k_sel_bounds_gather publishes a
 // wrong token, so every gather block times out (ERR_SPIN)
 constexpr int FICP_FAULT_SPIN = 1;

@@ -19,6 +19,7 @@
 // Both fuse the pending rigid transform of the previous fit (ficp.py:135) into the
 // source load, and write idx, dist, d2, the sort key, and the matched stem's XY.
 #include "ficp_internal.h"
+#include "win_pass.h"
 
 #include <hip/hip_ext.h>
 
@@ -909,6 +910,8 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
     return pend;
 }
 
+static_assert(kWinNNRows == 256 * QPT, "the fused window pass classifies one k_nn_grid_q workgroup");
+
 template <int MD, bool APPLY, int Q>
 __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g) {
     // the three flags load together (the apply flag's load used to wait for the other two)
@@ -961,6 +964,8 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g)
             for (int e = t; e < tot; e += 256)
                 cert_scan<MD>(a, g, S, i0 + s_list[e], true, cert_pad(g, s_mv[e]), kmin_c, kmax);
         }
+        // the window selection's pass on this workgroup's rows (uniform: the loop state)
+        if (Q == QPT && a.win.st && win_ok(*a.win.st)) nn_win_pass<Q>(a, i0, i0 / (256 * Q));
     } else {
         const Stems S = stems_of(g.pts, g.m);
         for (int q = 0; q < Q; ++q) {
@@ -1470,6 +1475,15 @@ __global__ __launch_bounds__(256) void k_interleave_xy(const double *x, const do
     out[2 * i + 1] = y[i];
 }
 
+// the moved XY into columns 0, 1 of the uploaded (n x ld) rows (ficp_run_into's result)
+__global__ __launch_bounds__(256) void k_put_xy_rows(const double *x, const double *y, int64_t n,
+                                                     int64_t ld, double *rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    rows[i * ld] = x[i];
+    rows[i * ld + 1] = y[i];
+}
+
 // empty shard: +inf distance, an index no real stem has (never chosen by the merge)
 __global__ __launch_bounds__(256) void k_fill_inf(double *d2, int32_t *idx, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1641,6 +1655,13 @@ hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, dou
                                 hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_interleave_xy, dim3(nblk(n)), dim3(256), 0, s, x, y, n, out_xy);
+    return hipGetLastError();
+}
+
+hipError_t launch_put_xy_rows(const double *x, const double *y, int64_t n, int64_t ld, double *rows,
+                              hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_put_xy_rows, dim3(nblk(n)), dim3(256), 0, s, x, y, n, ld, rows);
     return hipGetLastError();
 }
 

@@ -100,10 +100,10 @@ constexpr int NS_LOG = 12;
 constexpr int MAXLEV = 4;
 // window path (k_sel_win): rows a workgroup may hand over, coarse buckets per side of the
 // window (4 per octave of distance), record words per workgroup, arrival counter stride
-constexpr int WSLOT = 64;
+constexpr int WSLOT = kWinSlot;
 constexpr int NCS = fb::kWinNCS;
 constexpr int NCB = 2 * NCS;
-constexpr int WREC = 16;
+constexpr int WREC = kWinRec;
 constexpr int WCTR = 64;
 constexpr int SMALL_C = 160;  // final_small: above it the binned sort ranks faster (390: 5.8 vs 3.4 us)
 #ifndef FICP_GT
@@ -231,6 +231,11 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.ahi = (double *)take(NB / 16 * 8);
     x.ppk = (u64 *)take((int64_t)HBMAX * NB * 8);
     x.ctl = (SelCtl *)take(256);
+    // the words kept zero by the kernels themselves (zeroed once, k_sel_init) sit at offsets
+    // that do not depend on n: a context's workspace serves later runs of any smaller n
+    x.gcc = (unsigned *)take(NCB * 4);
+    x.gcf = (u64 *)take(NCB * 8);
+    x.wctr = (unsigned *)take(9 * WCTR * 4);
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
     x.fparts = (double *)take((int64_t)gather_blocks(n) * 64);
     x.ka = (u64 *)take(nn * 8);
@@ -246,15 +251,13 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.sblb = (double *)take(NB / 4 * 8);
     x.sbcb = (long long *)take(NB / 4 * 8);
     x.fpre = (double *)take(SMALL_C * 32);
-    const int64_t gbw = gather_blocks(n);
+    // (k_sel_win's workgroups or the fused pass's NN workgroups, whichever are more)
+    const int64_t gbw = std::max<int64_t>(gather_blocks(n), (nn + kWinNNRows - 1) / kWinNNRows);
     x.wrec = (u64 *)take(gbw * WREC * 8);
     x.wsk = (u64 *)take(gbw * WSLOT * 8);
     x.wsr = (double *)take(gbw * WSLOT * 8);
     x.wso = (uint32_t *)take(gbw * WSLOT * 4);
     x.wsp = (uint32_t *)take(gbw * WSLOT * 4);
-    x.gcc = (unsigned *)take(NCB * 4);
-    x.gcf = (u64 *)take(NCB * 8);
-    x.wctr = (unsigned *)take(9 * WCTR * 4);
     if (w) *w = x;
     return (int64_t)(p - p0) + 256;
 }
@@ -2520,238 +2523,13 @@ __device__ unsigned long long g_winp[8];
     } while (0)
 #endif
 
-__global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t *orig, int64_t n,
-                                               const u64 *range, int64_t nparts, SelWS w,
-                                               IterState *st, LoopCtl lc, int *host_flag,
-                                               FitSrc fs, int force_retry) {
-    constexpr int WI = GI;  // rows per thread (stride HT)
-    static_assert(GT == HT, "k_sel_win: gather's workgroup shape");
+// The window path's decision (k_sel_win's last workgroup, or k_sel_win_tail after the NN's
+// fused pass, k_grid_nn.hip nn_win_pass): the coarse buckets (read and zeroed), the records
+// of the nwb pass workgroups
+__device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap &m0, double lamv,
+                                         IterState *st, const LoopCtl &lc, int *host_flag,
+                                         const FitSrc &fs, int force_retry, Scr &scr) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    __shared__ Scr scr;
-    // coarse buckets in LDS, WREP copies by lane % WREP (most rows of a wave fall into a
-    // few coarse buckets: one copy serialised up to 64 lanes per atomic), rows padded so
-    // that a bucket's copies sit in different banks
-    constexpr int WREP = 8, WRS = NCB + 1;
-    __shared__ unsigned s_cc[WREP * WRS];
-    __shared__ u64 s_cf[WREP * WRS];
-    __shared__ double s_red[NWAVE][11];
-    __shared__ unsigned s_wc[NWAVE];
-    __shared__ int s_last;
-    WINP_B(0);
-    // every independent load first: the state's window inputs, the rows, the range parts
-    const int sk = st->done;
-    const int ph = st->phase, itv = st->it, stg = st->stage, wfl = st->wfloor;
-    const long long kprev = st->k;
-    const u64 tkey = st->tkey, tmove = st->tmove;
-    const double lamv = st->lam_cur;
-    // row q of this thread: pairs of consecutive rows per lane, so that every load is 16 B
-    // (8-B lanes stream at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md)
-    const int64_t base = (int64_t)blockIdx.x * (HT * WI) + 2 * t;
-    auto row_of = [&](int q) -> int64_t { return base + (int64_t)(q >> 1) * (2 * HT) + (q & 1); };
-    double rr[WI], xs[WI], ys[WI], xt[WI], yt[WI];
-    uint32_t oo[WI];
-#pragma unroll
-    for (int q = 0; q < WI; q += 2) {
-        // (i is even; the buffers hold n + 1 rows, so the pair of row n - 1 is readable; a
-        // pair at or past n reads pair 0, whose values the row tests below ignore)
-        const int64_t i = row_of(q) < n ? row_of(q) : 0;
-        const double2 a = *reinterpret_cast<const double2 *>(r + i);
-        const double2 b = *reinterpret_cast<const double2 *>(fs.sx + i);
-        const double2 c = *reinterpret_cast<const double2 *>(fs.sy + i);
-        const double2 d = *reinterpret_cast<const double2 *>(fs.cx + i);
-        const double2 e = *reinterpret_cast<const double2 *>(fs.cy + i);
-        const uint2 o = *reinterpret_cast<const uint2 *>(orig + i);
-        rr[q] = a.x, rr[q + 1] = a.y;
-        xs[q] = b.x, xs[q + 1] = b.y;
-        ys[q] = c.x, ys[q + 1] = c.y;
-        xt[q] = d.x, xt[q + 1] = d.y;
-        yt[q] = e.x, yt[q + 1] = e.y;
-        oo[q] = o.x, oo[q + 1] = o.y;
-    }
-    if (sk) {  // the run is over: the flag as k_sel_final's no-op
-        if (blockIdx.x == 0 && t == 0 && host_flag)
-            __hip_atomic_store(host_flag, kFlagDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-    }
-    for (int b = t; b < WREP * WRS; b += HT) {
-        s_cc[b] = 0u;
-        s_cf[b] = 0ULL;
-    }
-    const WMap m0 = win_map(tkey, tmove, wfl, n);
-    __shared__ int s_ce[NCB];  // each coarse bucket's fixed-point exponent
-    if (t < NCB) s_ce[t] = win_bucket_exp(m0, t);
-    // (uniform over the launch: every workgroup decides the same way, none arrives)
-    if (!(ph == PH_LOOP && (itv >= 1 || win_first_body(itv, stg, tmove)) && kprev > 0 &&
-          2.0 * lamv + 1.0 >= 1.0 && m0.ok)) {
-        if (blockIdx.x == 0 && t == 0) win_retry(st, host_flag);
-        return;
-    }
-    // an LDS-only barrier: __syncthreads() would also wait for every row's load
-    // (vmcnt(0)); this way the rows are classified as their loads land
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    WINP_B(1);
-    // classify the rows
-    unsigned nbel = 0, nbad = 0;
-    u64 kmn = ~0ULL, kmx = 0ULL;  // the finite rows' key range (the last workgroup's kmin)
-    double sb = 0.0, swn = 0.0;
-    double c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    u64 kk[WI];
-    unsigned inw = 0;
-    unsigned *my_cc = s_cc + (lane % WREP) * WRS;
-    u64 *my_cf = s_cf + (lane % WREP) * WRS;
-#pragma unroll
-    for (int q = 0; q < WI; ++q) {
-        const int64_t i = row_of(q);
-        kk[q] = 0ULL;
-        if (i < n) {
-            const double v = rr[q];
-            if (!(v < INFINITY)) {  // inf / NaN: the full selection's special cases
-                ++nbad;
-                continue;
-            }
-            const u64 k = key_of_r(v);
-            kk[q] = k;
-            kmn = min(kmn, k);
-            kmx = max(kmx, k);
-            if (k < m0.wlo) {
-                ++nbel;
-                sb = sb + v;
-                fit_add(c8, xs[q], ys[q], xt[q], yt[q], fs.px, fs.py);
-                const int b = NCS - 1 - win_cq((m0.wlo - 1ULL - k) >> m0.su);
-                const int e = s_ce[b];
-                atomicAdd(&my_cc[b], 1u);
-                atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
-            } else if (k < m0.whi) {
-                inw |= 1u << q;
-                swn = swn + v;
-            } else {
-                const int b = NCS + win_cq((k - m0.whi) >> m0.su);
-                const int e = s_ce[b];
-                atomicAdd(&my_cc[b], 1u);
-                atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
-            }
-        }
-    }
-    WINP_B(3);
-    // window rows handed over in row order (wave, then row slot, then lane): deterministic
-    u64 masks[WI];
-    unsigned wtot = 0;
-#pragma unroll
-    for (int q = 0; q < WI; ++q) {
-        masks[q] = __ballot((inw >> q) & 1u);
-        wtot += (unsigned)__popcll(masks[q]);
-    }
-    if (lane == 0) s_wc[wave] = wtot;
-    // the workgroup's sums (fixed trees: DPP wave sums, then the waves in order)
-    sb = wave_sum63(sb);
-    swn = wave_sum63(swn);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) c8[e] = wave_sum63(c8[e]);
-    const u64 cnt = wave_sum63_u64((u64)nbel | ((u64)nbad << 32));
-    u64 pka = ~kmn, pkb = kmx;
-    wave_range_reduce(pka, pkb);  // (max of ~kmin and of kmax, lane 63)
-    __shared__ u64 s_kr[NWAVE][2];
-    if (lane == 63) {
-        s_kr[wave][0] = pka;
-        s_kr[wave][1] = pkb;
-    }
-    if (lane == 63) {
-        s_red[wave][0] = sb;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s_red[wave][1 + e] = c8[e];
-        s_red[wave][9] = __longlong_as_double((long long)cnt);
-        s_red[wave][10] = swn;
-    }
-    __syncthreads();  // (the LDS atomics, the wave counts and sums are complete)
-    WINP_B(4);
-    // the coarse buckets first: their atomics complete while the rest is stored
-    if (t < NCB) {
-        unsigned c = 0;
-        u64 f = 0;
-#pragma unroll
-        for (int q = 0; q < WREP; ++q) {
-            c += s_cc[q * WRS + t];
-            f += s_cf[q * WRS + t];
-        }
-        if (c) {
-            __hip_atomic_fetch_add(&w.gcc[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&w.gcf[t], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    unsigned wpos = 0, wall = 0;
-#pragma unroll
-    for (int q = 0; q < NWAVE; ++q) {
-        wpos += q < wave ? s_wc[q] : 0u;
-        wall += s_wc[q];
-    }
-    const int blk = blockIdx.x;
-    if (wtot && wall <= (unsigned)WSLOT) {
-        const u64 lt = (1ULL << lane) - 1ULL;
-#pragma unroll
-        for (int q = 0; q < WI; ++q) {
-            if ((inw >> q) & 1u) {
-                const int64_t slot = (int64_t)blk * WSLOT + wpos + (unsigned)__popcll(masks[q] & lt);
-                __hip_atomic_store(&w.wsk[slot], kk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&w.wsr[slot], rr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&w.wso[slot], oo[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&w.wsp[slot], (uint32_t)row_of(q), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-            wpos += (unsigned)__popcll(masks[q]);
-        }
-    }
-    if (t == HT - 12) {  // the record's key range words: max(~key), max(key)
-        u64 a = s_kr[0][0], b = s_kr[0][1];
-        for (int q = 1; q < NWAVE; ++q) {
-            a = max(a, s_kr[q][0]);
-            b = max(b, s_kr[q][1]);
-        }
-        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 13], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 14], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (t >= HT - 11) {  // the record (the last wave: wave 0 flushed the buckets): count
-                         // below, window rows, bad rows, sum of r below, fit sums, window r
-        const int f = t - (HT - 11);
-        double v = s_red[0][f];
-        u64 cv = (u64)__double_as_longlong(s_red[0][9]);
-        for (int q = 1; q < NWAVE; ++q) {
-            v = v + s_red[q][f];
-            cv += (u64)__double_as_longlong(s_red[q][9]);
-        }
-        u64 *rec = w.wrec + (int64_t)blk * WREC;
-        if (f == 9) {
-            const u64 bad = (cv >> 32) + (wall > (unsigned)WSLOT ? 1ULL : 0ULL);
-            __hip_atomic_store(&rec[0], cv & 0xffffffffULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&rec[1], (u64)wall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&rec[2], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&rec[f < 9 ? 3 + f : 12], (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    WINP_B(5);
-    WINP_B(2);
-    // hand-off (k_fit_sums' form): every storing wave waits for its stores and atomics,
-    // then one lane arrives at its group counter and the group's last at the top counter
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    WINP_B(6);
-    if (t == 0) {
-        const unsigned grp = blockIdx.x & 7u, ng = min(gridDim.x, 8u);
-        const unsigned gsz = (gridDim.x - grp + 7u) / 8u;
-        unsigned *gc = w.wctr + WCTR * (1 + grp);
-        bool last = false;
-        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
-            __hip_atomic_exchange(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = __hip_atomic_fetch_add(w.wctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-            if (last) __hip_atomic_exchange(w.wctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-
-    // ---- the last workgroup: the coarse buckets (read and zeroed), the records
 #ifdef FICP_WIN_PROF
     unsigned long long wt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -2768,7 +2546,6 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     }
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
-    const int nwb = gridDim.x;
     const int G = (nwb + HT - 1) / HT;  // this thread's records: [g0, g1) (in order)
     const int g0 = min(nwb, t * G), g1 = min(nwb, g0 + G);
     constexpr int GMAX = 8;  // records per thread (nwb <= W_MAXWG)
@@ -3008,6 +2785,265 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t *orig, int64_t n,
+                                               const u64 *range, int64_t nparts, SelWS w,
+                                               IterState *st, LoopCtl lc, int *host_flag,
+                                               FitSrc fs, int force_retry) {
+    constexpr int WI = GI;  // rows per thread (stride HT)
+    static_assert(GT == HT, "k_sel_win: gather's workgroup shape");
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    __shared__ Scr scr;
+    // coarse buckets in LDS, WREP copies by lane % WREP (most rows of a wave fall into a
+    // few coarse buckets: one copy serialised up to 64 lanes per atomic), rows padded so
+    // that a bucket's copies sit in different banks
+    constexpr int WREP = 8, WRS = NCB + 1;
+    __shared__ unsigned s_cc[WREP * WRS];
+    __shared__ u64 s_cf[WREP * WRS];
+    __shared__ double s_red[NWAVE][11];
+    __shared__ unsigned s_wc[NWAVE];
+    __shared__ int s_last;
+    WINP_B(0);
+    // every independent load first: the state's window inputs, the rows, the range parts
+    const int sk = st->done;
+    const int ph = st->phase, itv = st->it, stg = st->stage, wfl = st->wfloor;
+    const long long kprev = st->k;
+    const u64 tkey = st->tkey, tmove = st->tmove;
+    const double lamv = st->lam_cur;
+    // row q of this thread: pairs of consecutive rows per lane, so that every load is 16 B
+    // (8-B lanes stream at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md)
+    const int64_t base = (int64_t)blockIdx.x * (HT * WI) + 2 * t;
+    auto row_of = [&](int q) -> int64_t { return base + (int64_t)(q >> 1) * (2 * HT) + (q & 1); };
+    double rr[WI], xs[WI], ys[WI], xt[WI], yt[WI];
+    uint32_t oo[WI];
+#pragma unroll
+    for (int q = 0; q < WI; q += 2) {
+        // (i is even; the buffers hold n + 1 rows, so the pair of row n - 1 is readable; a
+        // pair at or past n reads pair 0, whose values the row tests below ignore)
+        const int64_t i = row_of(q) < n ? row_of(q) : 0;
+        const double2 a = *reinterpret_cast<const double2 *>(r + i);
+        const double2 b = *reinterpret_cast<const double2 *>(fs.sx + i);
+        const double2 c = *reinterpret_cast<const double2 *>(fs.sy + i);
+        const double2 d = *reinterpret_cast<const double2 *>(fs.cx + i);
+        const double2 e = *reinterpret_cast<const double2 *>(fs.cy + i);
+        const uint2 o = *reinterpret_cast<const uint2 *>(orig + i);
+        rr[q] = a.x, rr[q + 1] = a.y;
+        xs[q] = b.x, xs[q + 1] = b.y;
+        ys[q] = c.x, ys[q + 1] = c.y;
+        xt[q] = d.x, xt[q + 1] = d.y;
+        yt[q] = e.x, yt[q + 1] = e.y;
+        oo[q] = o.x, oo[q + 1] = o.y;
+    }
+    if (sk) {  // the run is over: the flag as k_sel_final's no-op
+        if (blockIdx.x == 0 && t == 0 && host_flag)
+            __hip_atomic_store(host_flag, kFlagDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    for (int b = t; b < WREP * WRS; b += HT) {
+        s_cc[b] = 0u;
+        s_cf[b] = 0ULL;
+    }
+    const WMap m0 = win_map(tkey, tmove, wfl, n);
+    __shared__ int s_ce[NCB];  // each coarse bucket's fixed-point exponent
+    if (t < NCB) s_ce[t] = win_bucket_exp(m0, t);
+    // (uniform over the launch: every workgroup decides the same way, none arrives)
+    if (!(ph == PH_LOOP && (itv >= 1 || win_first_body(itv, stg, tmove)) && kprev > 0 &&
+          2.0 * lamv + 1.0 >= 1.0 && m0.ok)) {
+        if (blockIdx.x == 0 && t == 0) win_retry(st, host_flag);
+        return;
+    }
+    // an LDS-only barrier: __syncthreads() would also wait for every row's load
+    // (vmcnt(0)); this way the rows are classified as their loads land
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    WINP_B(1);
+    // classify the rows
+    unsigned nbel = 0, nbad = 0;
+    u64 kmn = ~0ULL, kmx = 0ULL;  // the finite rows' key range (the last workgroup's kmin)
+    double sb = 0.0, swn = 0.0;
+    double c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 kk[WI];
+    unsigned inw = 0;
+    unsigned *my_cc = s_cc + (lane % WREP) * WRS;
+    u64 *my_cf = s_cf + (lane % WREP) * WRS;
+#pragma unroll
+    for (int q = 0; q < WI; ++q) {
+        const int64_t i = row_of(q);
+        kk[q] = 0ULL;
+        if (i < n) {
+            const double v = rr[q];
+            if (!(v < INFINITY)) {  // inf / NaN: the full selection's special cases
+                ++nbad;
+                continue;
+            }
+            const u64 k = key_of_r(v);
+            kk[q] = k;
+            kmn = min(kmn, k);
+            kmx = max(kmx, k);
+            if (k < m0.wlo) {
+                ++nbel;
+                sb = sb + v;
+                fit_add(c8, xs[q], ys[q], xt[q], yt[q], fs.px, fs.py);
+                const int b = NCS - 1 - win_cq((m0.wlo - 1ULL - k) >> m0.su);
+                const int e = s_ce[b];
+                atomicAdd(&my_cc[b], 1u);
+                atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
+            } else if (k < m0.whi) {
+                inw |= 1u << q;
+                swn = swn + v;
+            } else {
+                const int b = NCS + win_cq((k - m0.whi) >> m0.su);
+                const int e = s_ce[b];
+                atomicAdd(&my_cc[b], 1u);
+                atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
+            }
+        }
+    }
+    WINP_B(3);
+    // window rows handed over in row order (wave, then row slot, then lane): deterministic
+    u64 masks[WI];
+    unsigned wtot = 0;
+#pragma unroll
+    for (int q = 0; q < WI; ++q) {
+        masks[q] = __ballot((inw >> q) & 1u);
+        wtot += (unsigned)__popcll(masks[q]);
+    }
+    if (lane == 0) s_wc[wave] = wtot;
+    // the workgroup's sums (fixed trees: DPP wave sums, then the waves in order)
+    sb = wave_sum63(sb);
+    swn = wave_sum63(swn);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) c8[e] = wave_sum63(c8[e]);
+    const u64 cnt = wave_sum63_u64((u64)nbel | ((u64)nbad << 32));
+    u64 pka = ~kmn, pkb = kmx;
+    wave_range_reduce(pka, pkb);  // (max of ~kmin and of kmax, lane 63)
+    __shared__ u64 s_kr[NWAVE][2];
+    if (lane == 63) {
+        s_kr[wave][0] = pka;
+        s_kr[wave][1] = pkb;
+    }
+    if (lane == 63) {
+        s_red[wave][0] = sb;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s_red[wave][1 + e] = c8[e];
+        s_red[wave][9] = __longlong_as_double((long long)cnt);
+        s_red[wave][10] = swn;
+    }
+    __syncthreads();  // (the LDS atomics, the wave counts and sums are complete)
+    WINP_B(4);
+    // the coarse buckets first: their atomics complete while the rest is stored
+    if (t < NCB) {
+        unsigned c = 0;
+        u64 f = 0;
+#pragma unroll
+        for (int q = 0; q < WREP; ++q) {
+            c += s_cc[q * WRS + t];
+            f += s_cf[q * WRS + t];
+        }
+        if (c) {
+            __hip_atomic_fetch_add(&w.gcc[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&w.gcf[t], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    unsigned wpos = 0, wall = 0;
+#pragma unroll
+    for (int q = 0; q < NWAVE; ++q) {
+        wpos += q < wave ? s_wc[q] : 0u;
+        wall += s_wc[q];
+    }
+    const int blk = blockIdx.x;
+    if (wtot && wall <= (unsigned)WSLOT) {
+        const u64 lt = (1ULL << lane) - 1ULL;
+#pragma unroll
+        for (int q = 0; q < WI; ++q) {
+            if ((inw >> q) & 1u) {
+                const int64_t slot = (int64_t)blk * WSLOT + wpos + (unsigned)__popcll(masks[q] & lt);
+                __hip_atomic_store(&w.wsk[slot], kk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&w.wsr[slot], rr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&w.wso[slot], oo[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&w.wsp[slot], (uint32_t)row_of(q), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            wpos += (unsigned)__popcll(masks[q]);
+        }
+    }
+    if (t == HT - 12) {  // the record's key range words: max(~key), max(key)
+        u64 a = s_kr[0][0], b = s_kr[0][1];
+        for (int q = 1; q < NWAVE; ++q) {
+            a = max(a, s_kr[q][0]);
+            b = max(b, s_kr[q][1]);
+        }
+        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 13], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 14], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t >= HT - 11) {  // the record (the last wave: wave 0 flushed the buckets): count
+                         // below, window rows, bad rows, sum of r below, fit sums, window r
+        const int f = t - (HT - 11);
+        double v = s_red[0][f];
+        u64 cv = (u64)__double_as_longlong(s_red[0][9]);
+        for (int q = 1; q < NWAVE; ++q) {
+            v = v + s_red[q][f];
+            cv += (u64)__double_as_longlong(s_red[q][9]);
+        }
+        u64 *rec = w.wrec + (int64_t)blk * WREC;
+        if (f == 9) {
+            const u64 bad = (cv >> 32) + (wall > (unsigned)WSLOT ? 1ULL : 0ULL);
+            __hip_atomic_store(&rec[0], cv & 0xffffffffULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rec[1], (u64)wall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&rec[2], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&rec[f < 9 ? 3 + f : 12], (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    WINP_B(5);
+    WINP_B(2);
+    // hand-off (k_fit_sums' form): every storing wave waits for its stores and atomics,
+    // then one lane arrives at its group counter and the group's last at the top counter
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    WINP_B(6);
+    if (t == 0) {
+        const unsigned grp = blockIdx.x & 7u, ng = min(gridDim.x, 8u);
+        const unsigned gsz = (gridDim.x - grp + 7u) / 8u;
+        unsigned *gc = w.wctr + WCTR * (1 + grp);
+        bool last = false;
+        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
+            __hip_atomic_exchange(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = __hip_atomic_fetch_add(w.wctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+            if (last) __hip_atomic_exchange(w.wctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    win_tail(w, (int)gridDim.x, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
+}
+
+// The decision after the NN's fused window pass (k_grid_nn.hip nn_win_pass): one workgroup
+// reads the nwb NN workgroups' records, slots and coarse buckets and runs win_tail.  Its
+// state test is k_sel_win's, the one the NN kernel took (win_ok) on the same state.
+__global__ __launch_bounds__(HT) void k_sel_win_tail(int nwb, int64_t n, SelWS w, IterState *st,
+                                                    LoopCtl lc, int *host_flag, FitSrc fs,
+                                                    int force_retry) {
+    __shared__ Scr scr;
+    const int sk = st->done;
+    const int ph = st->phase, itv = st->it, stg = st->stage, wfl = st->wfloor;
+    const long long kprev = st->k;
+    const u64 tkey = st->tkey, tmove = st->tmove;
+    const double lamv = st->lam_cur;
+    if (sk) {  // the run is over: the flag as k_sel_final's no-op
+        if (threadIdx.x == 0 && host_flag)
+            __hip_atomic_store(host_flag, kFlagDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    const WMap m0 = win_map(tkey, tmove, wfl, n);
+    if (!(ph == PH_LOOP && (itv >= 1 || win_first_body(itv, stg, tmove)) && kprev > 0 &&
+          2.0 * lamv + 1.0 >= 1.0 && m0.ok)) {  // (never: the NN pass took the same test)
+        if (threadIdx.x == 0) win_retry(st, host_flag);
+        return;
+    }
+    win_tail(w, nwb, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
+}
+
 __global__ void k_sel_init(SelWS w) {
     if (threadIdx.x == 0) {
         __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3142,6 +3178,25 @@ hipError_t launch_select_dist_final(const long long *packs, int world, int capd,
 }
 
 bool select_win_fits(int64_t n) { return n > 0 && gather_blocks(n) <= W_MAXWG; }
+
+int select_win_nn_blocks(int64_t n) {
+    const int64_t b = (n + kWinNNRows - 1) / kWinNNRows;
+    return (n > 0 && b <= W_MAXWG) ? (int)b : 0;
+}
+
+WinPassOut select_win_out(void *tmp, int64_t n) {
+    const SelWS w = carve(tmp, n);
+    return WinPassOut{w.wrec, w.wsk, w.wsr, w.wso, w.wsp, w.gcc, w.gcf};
+}
+
+hipError_t launch_select_win_tail(int64_t n, void *tmp, IterState *st, const LoopCtl &loop,
+                                  int *host_flag, hipStream_t s, const FitSrc &fit, int fault) {
+    const int nwb = select_win_nn_blocks(n);
+    if (nwb <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_sel_win_tail, dim3(1), dim3(HT), 0, s, nwb, n, carve(tmp, n), st, loop,
+                       host_flag, fit, (fault & FICP_FAULT_WIN) ? 1 : 0);
+    return hipGetLastError();
+}
 
 hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
                              const unsigned long long *range, int64_t range_parts, void *tmp,

@@ -169,18 +169,20 @@ class FractionalICP:
         if len(self.source) == 0 or len(self.target) == 0:
             self.last_stats = dict(n_nn_calls=0, n_fits=0, iters=(0, 0))
             return self.source
-        # the run moves a fresh array (ficp.py:114,135 replace self.source; the array the
-        # constructor made is never written), columns 0-1 only
+        # the run moves into a fresh array (ficp.py:114,135 replace self.source; the array
+        # the constructor made is never written): the library reads self.source and writes
+        # every column of `src` (0-1 moved), into a pooled pinned block in one D2H
         t0 = time.perf_counter()
-        src = _lib.copy_array(np.ascontiguousarray(self.source, dtype=np.float64))
+        rows = np.ascontiguousarray(self.source, dtype=np.float64)
+        src = _lib.host_array(rows.shape)
         t1 = time.perf_counter()
         with self._borrow() as ctx:
             t2 = time.perf_counter()
             # the CHM rows go over with their leading dimension (no column-slice copy)
             ctx.set_target(np.ascontiguousarray(self.target, dtype=np.float64), self.match_dims)
             t3 = time.perf_counter()
-            st = ctx.run(src, lambdas, self.threshold, self.max_iterations, self.allow_reflection,
-                         trace=trace, trace_idx=trace_idx)
+            st = ctx.run_into(rows, src, lambdas, self.threshold, self.max_iterations,
+                              self.allow_reflection, trace=trace, trace_idx=trace_idx)
             t4 = time.perf_counter()
         t5 = time.perf_counter()
         # where the call's host time went (ms): the constructor's copies, this copy, the

@@ -131,6 +131,13 @@ int ficp_apply_xy(ficp_ctx *ctx, const double *pts, int64_t n, int64_t ld, const
 int ficp_run(ficp_ctx *ctx, double *src, int64_t n, int64_t ld, int32_t nstages,
              const double *lambdas, double threshold, int32_t max_iterations,
              int32_t allow_reflection, ficp_stats *stats);
+/* ficp_run with separate input and output rows: `out` (n x ld) receives `src` with
+ * columns 0, 1 moved (out may alias src: that is ficp_run).  Replaces the copy the caller
+ * needs for ficp.py:114,135 (`self.source` is replaced by a new array, the constructor's
+ * is never written); when `out` is page-locked the rows come back in one direct D2H. */
+int ficp_run_into(ficp_ctx *ctx, const double *src, double *out, int64_t n, int64_t ld,
+                  int32_t nstages, const double *lambdas, double threshold,
+                  int32_t max_iterations, int32_t allow_reflection, ficp_stats *stats);
 /* Same on device-resident SoA source; x, y updated in place. */
 int ficp_run_device(ficp_ctx *ctx, double *x, double *y, const double *z, int64_t n,
                     int32_t nstages, const double *lambdas, double threshold,

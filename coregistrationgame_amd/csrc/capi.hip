@@ -224,7 +224,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr,
             const NNWin *win = nullptr) {
     NNArgs a{};
-    if (win) a.win = *win;  // k_nn_grid_q: the window selection's fused pass
+    a.win = win;  // k_nn_grid_q: the window selection's fused pass (device-side inputs)
     a.fin_orig = fin_orig;
     a.fin_x = fin_x;
     a.fin_y = fin_y;
@@ -520,8 +520,44 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
             tidx = c->tr_idx.as<int32_t>();
         }
     }
+    // selection path without traces: the selection's last kernel also runs the loop step
+    // and stores the done flag straight into the pinned ring (and, fuse_fit, the rigid fit
+    // of the next iteration: gather + final, no k_fit_sums pass).
+    const bool fused = !tidx;
+    // the rigid fit fused into the selection (gather: the rows below the candidates, their
+    // pairs loaded before the bounds wait; final: the selected candidates, prefetched in its
+    // prologue) instead of a k_fit_sums pass: +1.5-2.5 % at C3 (tools/ab_bench.sh, 2 x 40
+    // steps: 8,067 / 8,140 vs 7,965 / 7,933 it/s).  FICP_FUSE_FIT=0: the separate pass.
+    const char *ff = getenv("FICP_FUSE_FIT");
+    const bool fuse_fit = !(ff && atoi(ff) == 0);
+    // with the fused loop and fit every consumer of the sort key (histogram, gather) derives
+    // it from r (key_of_r): the NN stores 8 B per row less.  FICP_NN_KEYS=1: stored keys.
+    const char *nk = getenv("FICP_NN_KEYS");
+    const bool keys_from_r = fused && fuse_fit && !(nk && atoi(nk) != 0);
+    // the window path (k_sel_win, one launch instead of four) for the calls whose previous
+    // flag carried kFlagWinNext; FICP_SEL_WIN=0 turns it off.  It needs the work order (its
+    // arrays: library buffers, 16-B aligned for the window pass's loads).
+    const char *wv = getenv("FICP_SEL_WIN");
+    const bool use_win = fused && fuse_fit && keys_from_r && use_grid(c, n) && select_win_fits(n) &&
+                         !(wv && atoi(wv) == 0);
+    // ... and its pass fused into the certified NN kernel of the same call (k_nn_grid_q):
+    // the NN workgroups classify their rows as they write them and one workgroup decides
+    // (k_sel_win_tail).  FICP_WIN_NN=0: k_sel_win's own pass.
+    const char *wn = getenv("FICP_WIN_NN");
+    const bool win_nn = FICP_WIN_NN_BUILD && use_win && select_win_nn_blocks(n) > 0 && !(wn && atoi(wn) == 0);
+    NNWin nnw{};
+    NNWin *nnw_dev = nullptr;
+    if (win_nn) {
+        CHK(c->worig.ensure((n + 1) * 4));  // (build_work_order's buffer, allocated here first)
+        nnw.st = dst;
+        nnw.orig = c->worig.as<uint32_t>();
+        nnw.o = select_win_out(c->sel_tmp.p, n);
+        nnw.px = c->pivot_x;
+        nnw.py = c->pivot_y;
+        nnw_dev = select_win_desc(c->sel_tmp.p);
+    }
     HIPCHK(launch_run_start(tflag, &c->h_rep->t[0], c->stream, sel_err_word(c->sel_tmp.p, n), dst,
-                            &lc));
+                            &lc, nnw_dev, win_nn ? &nnw : nullptr));
     double *wx = sx, *wy = sy;
     const double *wz = sz;
     const uint32_t *worig = nullptr;
@@ -541,12 +577,6 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
              nullptr, worig, n, c->pivot_x, c->pivot_y, dst};
     const FitSrc fsrc{wx, wy, c->ccx.as<double>(), c->ccy.as<double>(), c->pivot_x, c->pivot_y, 1,
                       allow_refl};
-    // the rigid fit fused into the selection (gather: the rows below the candidates, their
-    // pairs loaded before the bounds wait; final: the selected candidates, prefetched in its
-    // prologue) instead of a k_fit_sums pass: +1.5-2.5 % at C3 (tools/ab_bench.sh, 2 x 40
-    // steps: 8,067 / 8,140 vs 7,965 / 7,933 it/s).  FICP_FUSE_FIT=0: the separate pass.
-    const char *ff = getenv("FICP_FUSE_FIT");
-    const bool fuse_fit = !(ff && atoi(ff) == 0);
     // Iterations are enqueued `la` ahead of the one whose done flag the host reads, so
     // the device never waits for the host; the iterations enqueued past the end are
     // no-ops (every kernel tests the flags k_loop_update set).  la = 1 with the fused
@@ -557,14 +587,6 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     const int64_t cap = (int64_t)nstages * ((int64_t)std::max(max_iter, 0) + 1);
     int64_t j = 0;
     bool finished = nstages <= 0;
-    // selection path without traces: the selection's last kernel also runs the loop step
-    // and stores the done flag straight into the pinned ring (and, fuse_fit, the rigid fit
-    // of the next iteration: gather + final, no k_fit_sums pass).
-    const bool fused = !tidx;
-    // with the fused loop and fit every consumer of the sort key (histogram, gather) derives
-    // it from r (key_of_r): the NN stores 8 B per row less.  FICP_NN_KEYS=1: stored keys.
-    const char *nk = getenv("FICP_NN_KEYS");
-    const bool keys_from_r = fused && fuse_fit && !(nk && atoi(nk) != 0);
     // the calls from this index on take k_nn_grid_q (mostly certified queries);
     // FICP_NN_QPT_FROM overrides (a large value: never)
     const char *qf = getenv("FICP_NN_QPT_FROM");
@@ -572,26 +594,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // part A of iteration i: the fit and the NN call; part B: the selection (and, not
     // fused, the loop step and the flag copy)
     int64_t last_a = -1;  // the last iteration whose fit + NN were enqueued
-    // the window path (k_sel_win, one launch instead of four) for the calls whose previous
-    // flag carried kFlagWinNext; FICP_SEL_WIN=0 turns it off
-    const char *wv = getenv("FICP_SEL_WIN");
-    // (the work-order arrays: library buffers, 16-B aligned for the window pass's loads)
-    const bool use_win = fused && fuse_fit && keys_from_r && worig && select_win_fits(n) &&
-                         !(wv && atoi(wv) == 0);
-    // ... and its pass fused into the certified NN kernel of the same call (k_nn_grid_q,
-    // calls >= nn_multi_from): the NN workgroups classify their rows as they write them
-    // and one workgroup decides (k_sel_win_tail).  FICP_WIN_NN=0: k_sel_win's own pass.
-    const char *wn = getenv("FICP_WIN_NN");
-    const bool win_nn = use_win && use_grid(c, n) && select_win_nn_blocks(n) > 0 && !(wn && atoi(wn) == 0);
     const int64_t win_nn_from = std::max<int64_t>(nn_multi_from, 1);
-    NNWin nnw{};
-    if (win_nn) {
-        nnw.st = dst;
-        nnw.orig = worig;
-        nnw.o = select_win_out(c->sel_tmp.p, n);
-        nnw.px = c->pivot_x;
-        nnw.py = c->pivot_y;
-    }
     auto enq_a = [&](int64_t i) -> int {
         if (!(fused && fuse_fit)) {
             ProfScope ps(c, P_FIT, "fit");
@@ -601,7 +604,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         // (a launch queued behind the loop's end writes the caller-order XY: fin_*)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
                     false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from,
-                    worig, sx, sy, (win_nn && i >= win_nn_from) ? &nnw : nullptr));
+                    worig, sx, sy, (win_nn && i >= win_nn_from) ? nnw_dev : nullptr));
         last_a = i;
         return FICP_OK;
     };

@@ -279,6 +279,9 @@ typedef float gap_t;
 // pass workgroup's record (kWinRec words), its window rows (at most kWinSlot: key, r, caller
 // index, work row) and the coarse buckets (agent-scope atomics, read and zeroed by the tail).
 constexpr int kWinSlot = 64, kWinRec = 16;
+// copies of the coarse buckets, one per XCD (blockIdx % 8): memory-side atomics on one word
+// serialise (~88 per us), and 977 NN workgroups on 256 words took ~11 us
+constexpr int kWinCopies = 8;
 struct WinPassOut {
     unsigned long long *wrec;
     unsigned long long *wsk;
@@ -292,6 +295,11 @@ struct IterState;
 // loop state allows the window path (win_ok), each k_nn_grid_q workgroup classifies its own
 // kWinNNRows rows right after writing them, and k_sel_win_tail (one workgroup) decides.
 constexpr int kWinNNRows = 1024;
+// -DFICP_WIN_NN_BUILD=0: a library without the fused pass (A/B of its register cost in the
+// NN kernel; the host then runs k_sel_win's own pass)
+#ifndef FICP_WIN_NN_BUILD
+#define FICP_WIN_NN_BUILD 1
+#endif
 struct NNWin {
     const IterState *st;        // nullable: no fused pass
     const uint32_t *orig;       // caller index per work row (the selection's tie-break)
@@ -337,7 +345,8 @@ struct NNArgs {
     // fin_x[fin_orig[p]] = sx[p] (k_scatter_xy's work, no launch or host round trip of its own)
     const uint32_t *fin_orig;
     double *fin_x, *fin_y;
-    NNWin win;                  // k_nn_grid_q: the fused window pass (win.st nullable)
+    const NNWin *win;           // k_nn_grid_q: the fused window pass's inputs (device memory,
+                                // written by k_run_start; nullable: no pass)
 };
 
 // k_scatter_xy's work for rows [p0, p0 + cnt) of the work order
@@ -415,7 +424,12 @@ __host__ __device__ __forceinline__ int win_start_log(long long n) {
     const int v = 60 - b;
     return v < kWinHMinLog ? kWinHMinLog : (v > 48 ? 48 : v);
 }
-__host__ __device__ __forceinline__ int win_hmax_log(long long n) { return win_start_log(n) + 4; }
+#ifndef FICP_WIN_HMAX_EXTRA
+#define FICP_WIN_HMAX_EXTRA 4  // doublings of the window above its start (tools/build_variant.sh A/B)
+#endif
+__host__ __device__ __forceinline__ int win_hmax_log(long long n) {
+    return win_start_log(n) + FICP_WIN_HMAX_EXTRA;
+}
 __host__ __device__ __forceinline__ int win_floor(int wfloor, long long n) {
     return wfloor > 0 ? wfloor : win_start_log(n);
 }
@@ -667,7 +681,8 @@ hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg
 // also initialise the loop state *st (the work of launch_loop_init, one launch less)
 hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s,
                             unsigned *selerr = nullptr, IterState *st = nullptr,
-                            const LoopCtl *lc = nullptr);
+                            const LoopCtl *lc = nullptr, NNWin *win_dst = nullptr,
+                            const NNWin *win_val = nullptr);
 
 // grid build (k_grid_nn.hip)
 // bbox of (x, y) -> out4 {xmin, xmax, ymin, ymax}; with ox, also copies x, y (z) there
@@ -827,6 +842,7 @@ bool select_win_fits(int64_t n);
 // the tail's launch (the same outputs, flags and fallback as launch_select_win)
 int select_win_nn_blocks(int64_t n);
 WinPassOut select_win_out(void *tmp, int64_t n);
+NNWin *select_win_desc(void *tmp);  // the NNWin slot of the workspace (n-independent offset)
 hipError_t launch_select_win_tail(int64_t n, void *tmp, IterState *st, const LoopCtl &loop,
                                   int *host_flag, hipStream_t s, const FitSrc &fit, int fault = 0);
 // test-only fault injection (ficp_set_fault): block 0 of k_sel_bounds_gather publishes a

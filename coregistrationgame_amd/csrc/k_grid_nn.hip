@@ -434,6 +434,17 @@ __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t
 
 // Per-query finish: matched slot, correspondence XY, idx/dist/r/key; folds the key into
 // this thread's range accumulator.
+// A warm scan that ends on the stem it matched before leaves (cx, cy, dz2, bp) as they are
+// -- they describe that stem already -- and writes only r / key / idx: 28 B per query less
+// written and no record reload, for one more load (the previous slot) before the scan.  The
+// batch kernels take it (C4 1024 plots: +2 %, 1.222M vs 1.200M plot-it/s); the single-plot
+// ones do not (C3 cover scans: -1.2 %, 8,470 vs 8,575 it/s).  FICP_NN_SKIP_SAME=0: never.
+#ifndef FICP_NN_SKIP_SAME
+#define FICP_NN_SKIP_SAME 1
+#endif
+__device__ __forceinline__ void finish_same(const NNArgs &a, int64_t i, const Best &b,
+                                            unsigned long long &kmin_c, unsigned long long &kmax);
+
 __device__ __forceinline__ void finish(const NNArgs &a, const Stems &S, int64_t i, double qz,
                                        const Best &b,
                                        unsigned long long &kmin_c, unsigned long long &kmax) {
@@ -450,6 +461,13 @@ __device__ __forceinline__ void finish(const NNArgs &a, const Stems &S, int64_t 
             a.dz2[i] = dz * dz;
         }
     }
+    const unsigned long long k = write_out(a, i, b.d2, b.id);
+    kmin_c = max(kmin_c, ~k);
+    kmax = max(kmax, k);
+}
+
+__device__ __forceinline__ void finish_same(const NNArgs &a, int64_t i, const Best &b,
+                                            unsigned long long &kmin_c, unsigned long long &kmax) {
     const unsigned long long k = write_out(a, i, b.d2, b.id);
     kmin_c = max(kmin_c, ~k);
     kmax = max(kmax, k);
@@ -655,7 +673,7 @@ __device__ __forceinline__ void cold_start(const GridView &g, const Stems &S, do
 // Step 2: the full scan of an uncertified query at its (already moved) position: warm
 // bound from the stored match (or the cold 3x3 start), every stem within d + pad
 // evaluated, the new bound G and the match slot stored, outputs written.
-template <int MD>
+template <int MD, bool SKIP = false>
 __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, const Stems &S,
                                           int64_t i, bool warm, double pad,
                                           unsigned long long &kmin_c, unsigned long long &kmax) {
@@ -664,6 +682,7 @@ __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, co
     const double eps = cert_eps(g, qx, qy);
     Best2 b{INFINITY, 0x7fffffff, -1, INFINITY};
     NNST(3);
+    const int pslot = (SKIP && warm) ? a.out_bp[i] : -2;  // the previous match
     if (warm) {
         const double d2w = warm_d2<MD>(a, i, qx, qy);
         if (d2w < INFINITY) b.d2 = d2w;  // a stem's exact d2, its slot unknown (-1)
@@ -689,6 +708,10 @@ __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, co
         gnew = fmin(sqrt(b.s2), rc - mq) - eps;
     }
     a.gap[i] = gap_rd(b.slot >= 0 ? gnew : 0.0);
+    if (b.slot >= 0 && b.slot == pslot) {
+        finish_same(a, i, Best{b.d2, b.id, b.slot}, kmin_c, kmax);
+        return;
+    }
     a.out_bp[i] = b.slot;
     finish(a, S, i, qz, Best{b.d2, b.id, max(b.slot, 0)}, kmin_c, kmax);
 }
@@ -704,7 +727,7 @@ __device__ __forceinline__ void group_eval(const Stems &S, int p0, int p1, int l
     for (int p = p0 + lg; p < p1; p += GS) eval2<MD>(S, p, qx, qy, qz, b);
 }
 
-template <int MD, int GS>
+template <int MD, int GS, bool SKIP = false>
 __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView &g, const Stems &S,
                                                 int64_t i, int lg, double pad,
                                                 unsigned long long &kmin_c, unsigned long long &kmax) {
@@ -717,6 +740,7 @@ __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView 
         return;
     }
     Best2 b{d2w, 0x7fffffff, -1, INFINITY};
+    const int pslot = SKIP ? a.out_bp[i] : -2;  // the previous match
     const int cy = cell_coord(qy, g.y0, g.inv_h, g.gy);
     const double mq = query_margin(g, qx, qy);
     const double rc = sqrt(d2w) + pad;
@@ -762,6 +786,10 @@ __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView 
     }
     const double gnew = fmin(sqrt(b.s2), rc - mq) - eps;
     a.gap[i] = gap_rd(gnew);
+    if (b.slot == pslot) {
+        finish_same(a, i, Best{b.d2, b.id, b.slot}, kmin_c, kmax);
+        return;
+    }
     finish(a, S, i, qz, Best{b.d2, b.id, max(b.slot, 0)}, kmin_c, kmax);
 }
 
@@ -912,15 +940,15 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
 
 static_assert(kWinNNRows == 256 * QPT, "the fused window pass classifies one k_nn_grid_q workgroup");
 
-template <int MD, bool APPLY, int Q>
-__device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g) {
+
+template <int MD, bool APPLY, int Q, bool SKIP = false>
+__device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g, int64_t i0) {
     // the three flags load together (the apply flag's load used to wait for the other two)
     const int sk = a.skip ? *a.skip : 0, ru = a.reuse ? *a.reuse : 0;
     const int ap = (APPLY && a.apply_flag) ? *a.apply_flag : 1;
     if (sk && a.fin_orig) fin_scatter(a, (int64_t)blockIdx.x * (256 * Q), 256 * Q);
     if (sk || ru) return;
     const int t = threadIdx.x;
-    const int64_t i0 = xcd_block(blockIdx.x, gridDim.x) * (256 * Q);
     unsigned long long kmin_c = 0, kmax = 0;
     const double *T = (APPLY && ap) ? a.T : nullptr;
     if (a.cert_block && a.gap && a.warm_c) {
@@ -951,21 +979,23 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g)
         __syncthreads();
         const int tot = s_n;
         if (a.cert_block >= 16 && tot <= 16) {
-            if (t < tot * 16) cert_scan_group<MD, 16>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
+            if (t < tot * 16) cert_scan_group<MD, 16, SKIP>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
         } else if (a.cert_block >= 8 && tot <= 32) {
-            if (t < tot * 8) cert_scan_group<MD, 8>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
+            if (t < tot * 8) cert_scan_group<MD, 8, SKIP>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
         } else if (a.cert_block >= 4 && tot <= 64) {
-            if (t < tot * 4) cert_scan_group<MD, 4>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
+            if (t < tot * 4) cert_scan_group<MD, 4, SKIP>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
         } else if (a.cert_block >= 2 && tot <= 128) {
-            if (t < tot * 2) cert_scan_group<MD, 2>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
+            if (t < tot * 2) cert_scan_group<MD, 2, SKIP>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
         } else if constexpr (Q == 1) {
-            if (t < tot) cert_scan<MD>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
+            if (t < tot) cert_scan<MD, SKIP>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
         } else {
             for (int e = t; e < tot; e += 256)
-                cert_scan<MD>(a, g, S, i0 + s_list[e], true, cert_pad(g, s_mv[e]), kmin_c, kmax);
+                cert_scan<MD, SKIP>(a, g, S, i0 + s_list[e], true, cert_pad(g, s_mv[e]), kmin_c, kmax);
         }
         // the window selection's pass on this workgroup's rows (uniform: the loop state)
-        if (Q == QPT && a.win.st && win_ok(*a.win.st)) nn_win_pass<Q>(a, i0, i0 / (256 * Q));
+#if FICP_WIN_NN_BUILD
+        if (Q == QPT && a.win && win_ok(*a.win->st)) nn_win_pass<Q>(a, i0, i0 / (256 * Q));
+#endif
     } else {
         const Stems S = stems_of(g.pts, g.m);
         for (int q = 0; q < Q; ++q) {
@@ -1078,7 +1108,7 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
 
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) NNQ_WPE void k_nn_grid_q(NNArgs a, GridView g) {
-    nn_grid_body<MD, APPLY, QPT>(a, g);
+    nn_grid_body<MD, APPLY, QPT>(a, g, xcd_block(blockIdx.x, gridDim.x) * (256 * QPT));
 }
 
 // Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against
@@ -1113,12 +1143,11 @@ __device__ __forceinline__ GridView plot_view(const PlotGrid &pg, const TPt *pts
 #define NNB_WPE
 #endif
 template <int MD>
-__global__ __launch_bounds__(256) NNB_WPE void k_nn_grid_batch(NNArgs a, const int32_t *__restrict__ plot_of,
-                                                       const PlotGrid *__restrict__ grids,
-                                                       const TPt *__restrict__ pts, int64_t m,
-                                                       const int32_t *__restrict__ cell_start,
-                                                       const PlotState *__restrict__ st) {
-    const int64_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void nn_batch_rows(const NNArgs &a, const int32_t *__restrict__ plot_of,
+                                              const PlotGrid *__restrict__ grids,
+                                              const TPt *__restrict__ pts, int64_t m,
+                                              const int32_t *__restrict__ cell_start,
+                                              const PlotState *__restrict__ st, int64_t i) {
     unsigned long long kmin_c = 0, kmax = 0;  // (no key range: the batch selection is per plot)
     const Stems S = stems_of(pts, m);
     int p = 0;
@@ -1163,15 +1192,58 @@ __global__ __launch_bounds__(256) NNB_WPE void k_nn_grid_batch(NNArgs a, const i
             const int64_t iq = i0 + s_list[q];
             const GridView gq = plot_view(grids[plot_of[iq]], pts, cell_start, m);
             const double pad = cert_pad(gq, s_mv[q]);
-            if (gs == 8) cert_scan_group<MD, 8>(a, gq, S, iq, t & 7, pad, kmin_c, kmax);
-            else if (gs == 4) cert_scan_group<MD, 4>(a, gq, S, iq, t & 3, pad, kmin_c, kmax);
-            else if (gs == 2) cert_scan_group<MD, 2>(a, gq, S, iq, t & 1, pad, kmin_c, kmax);
-            else cert_scan<MD>(a, gq, S, iq, true, pad, kmin_c, kmax);
+            constexpr bool SK = FICP_NN_SKIP_SAME != 0;
+            if (gs == 8) cert_scan_group<MD, 8, SK>(a, gq, S, iq, t & 7, pad, kmin_c, kmax);
+            else if (gs == 4) cert_scan_group<MD, 4, SK>(a, gq, S, iq, t & 3, pad, kmin_c, kmax);
+            else if (gs == 2) cert_scan_group<MD, 2, SK>(a, gq, S, iq, t & 1, pad, kmin_c, kmax);
+            else cert_scan<MD, SK>(a, gq, S, iq, true, pad, kmin_c, kmax);
         }
     } else if (live) {
         const GridView g = plot_view(grids[p], pts, cell_start, m);
         nn_query<MD>(a, g, S, i, T, kmin_c, kmax);
         if (a.gap) a.gap[i] = 0;  // the cold call stores no certificate (k_nn_grid)
+    }
+}
+
+template <int MD>
+__global__ __launch_bounds__(256) NNB_WPE void k_nn_grid_batch(NNArgs a, const int32_t *__restrict__ plot_of,
+                                                       const PlotGrid *__restrict__ grids,
+                                                       const TPt *__restrict__ pts, int64_t m,
+                                                       const int32_t *__restrict__ cell_start,
+                                                       const PlotState *__restrict__ st) {
+    nn_batch_rows<MD>(a, plot_of, grids, pts, m, cell_start, st,
+                      xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x);
+}
+
+// Warm batch calls, QPT queries per thread (the single-plot k_nn_grid_q's form): a
+// workgroup takes 256 * QPT consecutive trees.  When they all belong to one plot (10k-tree
+// plots: ~9 in 10 workgroups) the plot's state, transform and grid are uniform and the
+// rows run nn_grid_body against that plot's grid; a workgroup that straddles plots runs
+// k_nn_grid_batch's per-row form on each of its QPT row blocks in turn.
+template <int MD>
+__global__ __launch_bounds__(256) NNQ_WPE void k_nn_grid_batch_q(NNArgs a, const int32_t *__restrict__ plot_of,
+                                                         const PlotGrid *__restrict__ grids,
+                                                         const TPt *__restrict__ pts, int64_t m,
+                                                         const int32_t *__restrict__ cell_start,
+                                                         PlotState *__restrict__ st) {
+    const int64_t i0 = xcd_block(blockIdx.x, gridDim.x) * (256 * QPT);
+    const int64_t ilast = min(i0 + 256 * QPT, a.n) - 1;
+    const int p0 = plot_of[i0], p1 = plot_of[ilast];
+    if (p0 == p1) {  // (uniform)
+        if (st[p0].phase == PH_DONE) return;
+        NNArgs b = a;
+        b.T = st[p0].T;
+        b.apply_flag = &st[p0].apply;
+        b.skip = nullptr;
+        b.reuse = nullptr;
+        nn_grid_body<MD, true, QPT, FICP_NN_SKIP_SAME != 0>(b, plot_view(grids[p0], pts, cell_start, m), i0);
+        return;
+    }
+    for (int q = 0; q < QPT; ++q) {
+        const int64_t r0 = i0 + (int64_t)q * 256;
+        if (r0 >= a.n) break;  // (uniform)
+        nn_batch_rows<MD>(a, plot_of, grids, pts, m, cell_start, st, r0 + threadIdx.x);
+        __syncthreads();  // (the per-row form's LDS list is reused by the next block)
     }
 }
 
@@ -1707,7 +1779,23 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
                                 const TPt *pts, int64_t m, const int32_t *cell_start,
                                 const PlotState *st, int md, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    if (md == 3)
+    // warm calls: QPT queries per thread from FICP_BATCH_QPT_MIN trees per launch on (default
+    // 2M: ~2,000 workgroups of 1024 trees, enough to hide their latency chains; at 128 plots
+    // of 10k, 640k trees per sub-batch, the 1-query form measured 39 vs 55 us per launch,
+    // at 1024 plots the QPT form 264 vs 316 us); FICP_BATCH_QPT=0: never
+    const char *qe = getenv("FICP_BATCH_QPT");
+    const char *qm = getenv("FICP_BATCH_QPT_MIN");
+    const int64_t qpt_min = qm ? atoll(qm) : (int64_t)2000000;
+    if (!(qe && atoi(qe) == 0) && a.n >= qpt_min && a.warm_c && a.gap && a.cert_block) {
+        PlotState *stw = const_cast<PlotState *>(st);
+        const dim3 gq(nblk(a.n, 256 * QPT));
+        if (md == 3)
+            hipLaunchKernelGGL(k_nn_grid_batch_q<3>, gq, dim3(256), 0, s, a, plot_of, grids, pts, m,
+                               cell_start, stw);
+        else
+            hipLaunchKernelGGL(k_nn_grid_batch_q<2>, gq, dim3(256), 0, s, a, plot_of, grids, pts, m,
+                               cell_start, stw);
+    } else if (md == 3)
         hipLaunchKernelGGL(k_nn_grid_batch<3>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
                            pts, m, cell_start, st);
     else

@@ -170,6 +170,7 @@ struct SelWS {
     long long *sbcb; // [NB / 4] rows in the buckets before each run
     double *fpre;    // [SMALL_C][4] fused fit: the pair of pack slots < SMALL_C (gather)
     // the window path (k_sel_win):
+    NNWin *nnwin;    // the fused pass's inputs (k_run_start writes them per run)
     u64 *wrec;       // [gather blocks][WREC] each workgroup's record (sc1 stores)
     u64 *wsk;        // [gather blocks][WSLOT] its window rows: key, r, caller index, work row
     double *wsr;
@@ -233,9 +234,10 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.ctl = (SelCtl *)take(256);
     // the words kept zero by the kernels themselves (zeroed once, k_sel_init) sit at offsets
     // that do not depend on n: a context's workspace serves later runs of any smaller n
-    x.gcc = (unsigned *)take(NCB * 4);
-    x.gcf = (u64 *)take(NCB * 8);
+    x.gcc = (unsigned *)take(kWinCopies * NCB * 4);
+    x.gcf = (u64 *)take(kWinCopies * NCB * 8);
     x.wctr = (unsigned *)take(9 * WCTR * 4);
+    x.nnwin = (NNWin *)take(sizeof(NNWin));
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
     x.fparts = (double *)take((int64_t)gather_blocks(n) * 64);
     x.ka = (u64 *)take(nn * 8);
@@ -2541,8 +2543,18 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     unsigned cc = 0;
     u64 cf = 0;
     if (t < NCB) {
-        cc = __hip_atomic_exchange(&w.gcc[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cf = __hip_atomic_exchange(&w.gcf[t], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned cq[kWinCopies];
+        u64 fq[kWinCopies];
+#pragma unroll
+        for (int q = 0; q < kWinCopies; ++q) {
+            cq[q] = __hip_atomic_exchange(&w.gcc[q * NCB + t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fq[q] = __hip_atomic_exchange(&w.gcf[q * NCB + t], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int q = 0; q < kWinCopies; ++q) {  // (integers: exact in any order)
+            cc += cq[q];
+            cf += fq[q];
+        }
     }
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
@@ -2939,8 +2951,9 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
             f += s_cf[q * WRS + t];
         }
         if (c) {
-            __hip_atomic_fetch_add(&w.gcc[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&w.gcf[t], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int cp = (int)(blockIdx.x % kWinCopies) * NCB + t;  // (the XCD's copy)
+            __hip_atomic_fetch_add(&w.gcc[cp], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&w.gcf[cp], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     unsigned wpos = 0, wall = 0;
@@ -3053,7 +3066,7 @@ __global__ void k_sel_init(SelWS w) {
         __hip_atomic_store(&w.ctl->bpub, (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // the window path's coarse buckets and arrival counters
-    for (int b = threadIdx.x; b < NCB; b += blockDim.x) {
+    for (int b = threadIdx.x; b < kWinCopies * NCB; b += blockDim.x) {
         __hip_atomic_exchange(&w.gcc[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_exchange(&w.gcf[b], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -3183,6 +3196,8 @@ int select_win_nn_blocks(int64_t n) {
     const int64_t b = (n + kWinNNRows - 1) / kWinNNRows;
     return (n > 0 && b <= W_MAXWG) ? (int)b : 0;
 }
+
+NNWin *select_win_desc(void *tmp) { return carve(tmp, 0).nnwin; }
 
 WinPassOut select_win_out(void *tmp, int64_t n) {
     const SelWS w = carve(tmp, n);

@@ -22,7 +22,7 @@ static_assert(kWinNCB == 256, "one coarse bucket per thread of the NN workgroup"
 template <int Q>
 __device__ __forceinline__ void nn_win_pass(const NNArgs &a, int64_t i0, int64_t tile) {
     using fb::u64;
-    const NNWin &W = a.win;
+    const NNWin &W = *a.win;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     constexpr int NCS = fb::kWinNCS, WREP = 2, WRS = kWinNCB + 1;
     __shared__ unsigned s_cc[WREP * WRS];
@@ -123,8 +123,9 @@ __device__ __forceinline__ void nn_win_pass(const NNArgs &a, int64_t i0, int64_t
             f += s_cf[q * WRS + t];
         }
         if (c) {
-            __hip_atomic_fetch_add(&W.o.gcc[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&W.o.gcf[t], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int cp = (int)(blockIdx.x % kWinCopies) * kWinNCB + t;  // (the XCD's copy)
+            __hip_atomic_fetch_add(&W.o.gcc[cp], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&W.o.gcf[cp], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // the window rows: slot of (row slot q, wave, lane) in that order

@@ -302,7 +302,9 @@ int main(int argc, char **argv) {
                     na.sy = dys;
                     na.cx = dxt;
                     na.cy = dyt;
-                    na.win = NNWin{st, dorig, select_win_out(tmp, n), 0.0, 0.0};
+                    const NNWin nw{st, dorig, select_win_out(tmp, n), 0.0, 0.0};
+                    CK(hipMemcpy(select_win_desc(tmp), &nw, sizeof nw, hipMemcpyHostToDevice));
+                    na.win = select_win_desc(tmp);
                     hipLaunchKernelGGL(k_pass_only, dim3((unsigned)select_win_nn_blocks(n)), dim3(256), 0, 0, na);
                 }
                 CK(launch_select_win_tail(n, tmp, st, lc, dflag, 0, fs, 0));

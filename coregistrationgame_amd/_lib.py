@@ -135,6 +135,7 @@ def lib():
         "ficp_apply_xy": ([_vp, _dp, _i64, _i64, _dp, _dp], C.c_int),
         "ficp_run": ([_vp, _dp, _i64, _i64, _i32, _dp, C.c_double, _i32, _i32, C.POINTER(Stats)],
                      C.c_int),
+        "ficp_set_batch_trace": ([_vp, C.POINTER(C.c_int64), _i32], C.c_int),
         "ficp_run_into": ([_vp, _dp, _dp, _i64, _i64, _i32, _dp, C.c_double, _i32, _i32,
                            C.POINTER(Stats)], C.c_int),
         "ficp_run_device": ([_vp, _vp, _vp, _vp, _i64, _i32, _dp, C.c_double, _i32, _i32,
@@ -372,6 +373,15 @@ class Context:
                                     float(threshold), int(max_iterations), int(bool(allow_reflection)),
                                     _vp(out.ctypes.data)))
         return out
+
+    def set_batch_trace(self, trace_k: np.ndarray | None):
+        """Per-call k of every plot of the next batch runs into trace_k (nplots x max_calls
+        int64, -1 past a plot's last call); None turns it off.  Keep the array alive."""
+        if trace_k is None:
+            _check(lib().ficp_set_batch_trace(self.h, None, 0))
+            return
+        assert trace_k.dtype == np.int64 and trace_k.flags.c_contiguous and trace_k.ndim == 2
+        _check(lib().ficp_set_batch_trace(self.h, _p(trace_k, _ip64), trace_k.shape[1]))
 
     def run_batch_device(self, src_off, x_ptr: int, y_ptr: int, z_ptr: int, tgt_off, tx_ptr: int, ty_ptr: int,
                          tz_ptr: int, md: int, lambdas, threshold: float, max_iterations: int,

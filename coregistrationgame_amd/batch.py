@@ -52,9 +52,13 @@ class FractionalICPBatch:
             self._ctx.close()
             self._ctx = None
 
-    def run(self) -> list[np.ndarray]:
-        """Runs every plot; returns (and stores in .sources) the moved source arrays."""
+    def run(self, trace: bool = False, max_trace: int = 256) -> list[np.ndarray]:
+        """Runs every plot; returns (and stores in .sources) the moved source arrays.
+        trace=True also records every plot's k per NN / fraction call in .k_trace (a list of
+        int64 arrays, up to max_trace calls each)."""
         nplots = len(self.sources)
+        self._trace = max_trace if trace else 0
+        self.k_trace = [np.zeros(0, np.int64) for _ in range(nplots)] if trace else None
         stats = np.zeros(nplots, _lib.PLOT_STATS_DTYPE)
         ident = np.eye(3).ravel()
         stats["T_total"] = ident
@@ -77,9 +81,19 @@ class FractionalICPBatch:
         to = np.zeros(len(plots) + 1, np.int64)
         so[1:] = np.cumsum([len(self.sources[p]) for p in plots])
         to[1:] = np.cumsum([len(self.targets[p]) for p in plots])
-        out = self._context().run_batch(so, src, to, tgt, md, stage_lambdas(self.lambda_val, md),
-                                        self.threshold, self.max_iterations, self.allow_reflection)
+        ctx = self._context()
+        tr = np.full((len(plots), self._trace), -1, np.int64) if self._trace else None
+        ctx.set_batch_trace(tr)
+        try:
+            out = ctx.run_batch(so, src, to, tgt, md, stage_lambdas(self.lambda_val, md),
+                                self.threshold, self.max_iterations, self.allow_reflection)
+        finally:
+            if tr is not None:
+                ctx.set_batch_trace(None)
         for j, p in enumerate(plots):
+            if tr is not None:
+                row = tr[j]
+                self.k_trace[p] = row[row >= 0].copy()
             moved = self.sources[p].copy()  # columns 0,1 move; the rest stay bit-identical
             moved[:, :2] = src[so[j]:so[j + 1], :2]
             self.sources[p] = moved

@@ -864,6 +864,7 @@ void ficp_destroy(ficp_ctx *c) {
                       &c->ccx,    &c->ccy,        &c->rs,       &c->range,    &c->wx,
                       &c->wy,     &c->wz,         &c->worig,    &c->tidx,     &c->stage,
                       &c->stage2, &c->cx,         &c->cy,       &c->cz,       &c->state_dev,
+                      &c->btrace,
                       &c->bp,     &c->dz2,        &c->gap,      &c->lams,       &c->tr_k,     &c->tr_f,     &c->tr_l,
                       &c->tr_T,   &c->tr_idx,     &c->sel_tmp,  &c->sel_stats, &c->bs_tmp, &c->bs_tmp2};
     for (DevBuf *b : bufs) b->release();

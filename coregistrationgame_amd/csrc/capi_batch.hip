@@ -315,8 +315,16 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // the separate k_batch_fit and k_batch_update launches.
         const char *bf = getenv("FICP_BATCH_FUSE");
         const bool bfuse = !(bf && atoi(bf) == 0);
-        const BatchStepArgs step{sx, sy, b.ccx.as<double>(), b.ccy.as<double>(), b.grids.as<PlotGrid>(),
-                                 allow_refl, nstages, max_iter, threshold};
+        BatchStepArgs step{sx, sy, b.ccx.as<double>(), b.ccy.as<double>(), b.grids.as<PlotGrid>(),
+                           allow_refl, nstages, max_iter, threshold};
+        long long *trace = nullptr;  // per-call k of every plot (ficp_set_batch_trace), -1 = none
+        if (c->btrace_host && c->btrace_max > 0) {
+            const size_t tb = (size_t)nplots * (size_t)c->btrace_max * 8;
+            CHK(c->btrace.ensure(tb));
+            HIPCHK(hipMemsetAsync(c->btrace.p, 0xff, tb, c->stream));
+            trace = c->btrace.as<long long>();
+            step.max_trace = c->btrace_max;
+        }
         auto enqueue = [&](Sub &u, int64_t bit) -> int {
             int *flag = &u.ring[bit % kBatchRing];
             __atomic_store_n(flag, -1, __ATOMIC_RELEASE);
@@ -350,8 +358,9 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                                             b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
                                             md, u.s));
             }
-            BatchStepArgs su_step = step;  // this sub-batch's grids, counter and flag
+            BatchStepArgs su_step = step;  // this sub-batch's grids, counter, flag and trace
             su_step.grids = gu;  // indexed by the plot within the sub-batch (fit pivot)
+            su_step.trace = trace ? trace + (size_t)u.p0 * (size_t)step.max_trace : nullptr;
             su_step.arrive = b.arrive.as<unsigned long long>() + (&u - subs);
             su_step.flag = flag;
             {
@@ -362,7 +371,9 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             }
             // (fused: the selection's last workgroup stores the live count, k_batch.hip
             // batch_arrive -- the k_batch_live launch cost ~5-8 us per batch iteration)
-            if (!bfuse) HIPCHK(launch_batch_update(u.np, nstages, threshold, max_iter, su, flag, u.s));
+            if (!bfuse)
+                HIPCHK(launch_batch_update(u.np, nstages, threshold, max_iter, su, flag, u.s, su_step.trace,
+                                           step.max_trace));
             return FICP_OK;
         };
         for (int q = 0; q < nsub; ++q)
@@ -396,6 +407,15 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         int v = 0;
         CHK(poll_flag(c, rflag, v));
     }
+    if (c->btrace_host && c->btrace_max > 0) {
+        const size_t tb = (size_t)nplots * (size_t)c->btrace_max * 8;
+        if (n > 0 && m > 0 && nstages > 0) {
+            HIPCHK(hipMemcpyAsync(c->btrace_host, c->btrace.p, tb, hipMemcpyDeviceToHost, c->stream));
+            CHK(sync(c));
+        } else {
+            memset(c->btrace_host, 0xff, tb);  // no call ran
+        }
+    }
     if (per_plot) {
         const PlotState *hs = b.rep.as<const PlotState>();
         for (int32_t p = 0; p < nplots; ++p) {
@@ -424,6 +444,14 @@ int check_batch_args(int32_t nplots, int32_t md, int32_t nstages, const double *
 }  // namespace
 
 extern "C" {
+
+int ficp_set_batch_trace(ficp_ctx *c, int64_t *trace_k, int32_t max_calls) {
+    if (!c) return fail(FICP_EINVAL, "null context");
+    if (max_calls < 0 || (max_calls > 0 && !trace_k)) return fail(FICP_EINVAL, "bad trace arguments");
+    c->btrace_host = max_calls > 0 ? trace_k : nullptr;
+    c->btrace_max = max_calls;
+    return FICP_OK;
+}
 
 int ficp_run_batch(ficp_ctx *c, int32_t nplots, const int64_t *src_off, double *src,
                    int64_t lds, const int64_t *tgt_off, const double *tgt, int64_t ldt,

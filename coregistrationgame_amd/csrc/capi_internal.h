@@ -208,6 +208,10 @@ struct ficp_ctx {
     PinBuf pin_xy{nullptr, 0, hipHostMallocCoherent};  // k_small_run's XY, stored by the kernel
     PinBuf pin_up;             // bounce buffer of small target uploads (ficp_set_target)
     hipEvent_t up_ev = nullptr;  // the last upload from pin_up
+    // per-call k trace of the batch runs (ficp_set_batch_trace): host rows of max_trace
+    int64_t *btrace_host = nullptr;
+    int32_t btrace_max = 0;
+    DevBuf btrace;
 };
 constexpr size_t kBounceBytes = 1 << 20;  // ficp_set_target layers up to 1 MB bounce (no sync)
 

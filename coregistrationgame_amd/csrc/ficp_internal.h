@@ -1005,6 +1005,8 @@ struct BatchStepArgs {
     // (no k_batch_live launch)
     unsigned long long *arrive = nullptr;
     int *flag = nullptr;
+    long long *trace = nullptr;  // per-call k trace rows of this launch's plots (nullable)
+    int max_trace = 0;
 };
 hipError_t launch_batch_live(int nplots, const PlotState *st, int *flag, hipStream_t s);
 hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,
@@ -1013,6 +1015,7 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
                                const BatchStepArgs *step = nullptr);
 // *flag (coherent pinned host memory) <- number of plots still running
 hipError_t launch_batch_update(int nplots, int nstages, double threshold, int max_iter,
-                               PlotState *st, int *flag, hipStream_t s);
+                               PlotState *st, int *flag, hipStream_t s, long long *trace = nullptr,
+                               int max_trace = 0);
 
 }  // namespace ficp

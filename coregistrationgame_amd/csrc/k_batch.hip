@@ -341,9 +341,12 @@ __device__ __forceinline__ void end_stage(PlotState &s, int nstages) {
 // *flag in coherent pinned host memory, which the host polls while the next batch
 // iteration already runs
 constexpr int UT = 1024;
+// trace (nullable): this plot's row of the per-call k trace (ficp_set_batch_trace)
 __device__ __forceinline__ void step_plot(PlotState &s, int nstages, double threshold,
-                                          int max_iter) {
+                                          int max_iter, long long *trace = nullptr,
+                                          int max_trace = 0) {
     if (s.phase != PH_DONE) {
+        if (trace && s.n_nn < max_trace) trace[s.n_nn] = s.k;
         s.n_nn += 1;
         if (s.phase == PH_HEAD) {
             if (s.k == 0) {
@@ -376,10 +379,11 @@ __device__ __forceinline__ void step_plot(PlotState &s, int nstages, double thre
 }
 
 __device__ __forceinline__ bool update_plot(PlotState *st, int p, int nstages, double threshold,
-                                            int max_iter) {
+                                            int max_iter, long long *trace, int max_trace) {
     PlotState s = st[p];
     if (s.phase != PH_DONE) {
-        step_plot(s, nstages, threshold, max_iter);
+        step_plot(s, nstages, threshold, max_iter, trace ? trace + (int64_t)p * max_trace : nullptr,
+                  max_trace);
         st[p] = s;
     }
     return s.phase != PH_DONE;
@@ -401,6 +405,8 @@ struct BatchStep {
     int *flag;                   // the last arrival stores the live count (pinned host word)
     int nplots;
     int win;                     // the window path (FICP_BSEL_WIN=0: off)
+    long long *trace;            // per-call k trace, max_trace per plot of this launch (nullable)
+    int max_trace;
 };
 
 // thread 0 of plot p's workgroup, its state final for this call: one agent-scope atomic
@@ -442,7 +448,8 @@ __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, do
         const int f = win_floor(s.wfloor, nrow);
         if (wrows > 256) s.wfloor = max(kWinHMinLog, f - 1);
         else if (wrows >= 0 && wrows < 16) s.wfloor = min(win_hmax_log(nrow) - 1, f + 1);
-        step_plot(s, bs.nstages, bs.threshold, bs.max_iter);
+        step_plot(s, bs.nstages, bs.threshold, bs.max_iter,
+                  bs.trace ? bs.trace + (int64_t)p * bs.max_trace : nullptr, bs.max_trace);
         s_flag[0] = s.phase == PH_LOOP && s.k > 0;  // a loop body (fit -> apply -> NN) follows
         st[p] = s;
         batch_arrive(bs, s.phase != PH_DONE ? 1 : 0);
@@ -1129,11 +1136,12 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
 }
 
 __global__ __launch_bounds__(UT) void k_batch_update(int nplots, int nstages, double threshold,
-                                                     int max_iter, PlotState *st, int *flag) {
+                                                     int max_iter, PlotState *st, int *flag,
+                                                     long long *trace, int max_trace) {
     __shared__ int s_live[UT / 64];
     int live = 0;
     for (int p = threadIdx.x; p < nplots; p += UT)
-        live += update_plot(st, p, nstages, threshold, max_iter) ? 1 : 0;
+        live += update_plot(st, p, nstages, threshold, max_iter, trace, max_trace) ? 1 : 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o, 64);
     if ((threadIdx.x & 63) == 0) s_live[threadIdx.x >> 6] = live;
@@ -1249,6 +1257,8 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
         bs.arrive = step->arrive;
         bs.flag = step->flag;
         bs.nplots = nplots;
+        bs.trace = step->trace;
+        bs.max_trace = step->max_trace;
         const char *wv = getenv("FICP_BSEL_WIN");
         bs.win = !(wv && atoi(wv) == 0);
     }
@@ -1264,9 +1274,10 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
 }
 
 hipError_t launch_batch_update(int nplots, int nstages, double threshold, int max_iter,
-                               PlotState *st, int *flag, hipStream_t s) {
+                               PlotState *st, int *flag, hipStream_t s, long long *trace,
+                               int max_trace) {
     hipLaunchKernelGGL(k_batch_update, dim3(1), dim3(UT), 0, s, nplots, nstages, threshold,
-                       max_iter, st, flag);
+                       max_iter, st, flag, trace, max_trace);
     return hipGetLastError();
 }
 

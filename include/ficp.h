@@ -161,6 +161,11 @@ typedef struct ficp_plot_stats {
    non-decreasing.  All plots share md, lambdas, threshold, max_iterations and
    allow_reflection; 0 < nplots <= 65535.  Source columns 0,1 are updated in place;
    per_plot (nullable) receives nplots records.  Independent of ficp_set_target. */
+/* Per-call k trace of the next batch runs (no reference counterpart; the batch's analogue
+   of ficp_stats::trace_k, for tests): trace_k[p * max_calls + j] = k of plot p's j-th NN /
+   fraction call (ficp.py:73-86), -1 past its last call; (nullptr, 0) turns it off.  The
+   host array must hold nplots * max_calls entries and outlive the runs. */
+int ficp_set_batch_trace(ficp_ctx *ctx, int64_t *trace_k, int32_t max_calls);
 int ficp_run_batch(ficp_ctx *ctx, int32_t nplots, const int64_t *src_off, double *src,
                    int64_t lds, const int64_t *tgt_off, const double *tgt, int64_t ldt,
                    int32_t md, int32_t nstages, const double *lambdas, double threshold,

@@ -82,17 +82,22 @@ def test_batch_vs_oracle_mixed(oracle, knobs, monkeypatch):
     srcs[5] = srcs[5][:0]            # empty tree layer
     tgts[9] = tgts[9][:0]            # empty CHM layer
     b = FractionalICPBatch(srcs, tgts)
-    finals = b.run()
+    finals = b.run(trace=True)
     for p in range(64):
         if len(srcs[p]) == 0 or len(tgts[p]) == 0:
             np.testing.assert_array_equal(finals[p], srcs[p])
             assert b.stats[p]["n_nn_calls"] == 0
+            assert len(b.k_trace[p]) == 0
             continue
         ofinal, otr = oracle.run(srcs[p], tgts[p], nthreads=8)
         np.testing.assert_allclose(finals[p][:, :2], ofinal[:, :2], atol=1e-6, rtol=0, err_msg=str(p))
         np.testing.assert_array_equal(bits(finals[p][:, 2:]), bits(srcs[p][:, 2:]))
         assert b.stats[p]["n_nn_calls"] == len(otr["k"]), p
         assert b.stats[p]["k_last"] == otr["k"][-1], p
+        # k of every call the oracle's curve pins (per call, not only the last)
+        first = pinned_prefix(otr["gap"], otr["frmsd"], 1.0 + np.abs(srcs[p][:, :2]).max())
+        assert len(b.k_trace[p]) == len(otr["k"]), p
+        np.testing.assert_array_equal(b.k_trace[p][:first], otr["k"][:first], err_msg=str(p))
 
 
 def _far_apart_batch(n_plots=80):
@@ -127,11 +132,13 @@ def test_batch_sub_batches_far_apart_bit_identical(oracle, monkeypatch):
         for k, v in knobs.items():
             monkeypatch.setenv(k, v)
         b = FractionalICPBatch(srcs, tgts)
-        outs[name] = (b.run(), b.stats)
+        outs[name] = (b.run(trace=True), b.stats, b.k_trace)
         monkeypatch.delenv("FICP_BATCH_FUSE", raising=False)
-    (f2, s2), (f1, s1), (fu, su) = outs["two"], outs["one"], outs["unfused"]
+    (f2, s2, k2), (f1, s1, k1), (fu, su, ku) = outs["two"], outs["one"], outs["unfused"]
     for p in range(len(srcs)):
         np.testing.assert_array_equal(bits(f2[p]), bits(f1[p]), err_msg=str(p))
+        np.testing.assert_array_equal(k2[p], k1[p], err_msg=str(p))
+        np.testing.assert_array_equal(k2[p], ku[p], err_msg=str(p))
         assert s2[p]["n_nn_calls"] == su[p]["n_nn_calls"], p
         assert s2[p]["k_last"] == su[p]["k_last"], p
         np.testing.assert_allclose(f2[p][:, :2], fu[p][:, :2], atol=1e-6, rtol=0, err_msg=str(p))

@@ -3,7 +3,8 @@
 # the same command, the PMC passes of the NN kernel (tools/pmc.sh) with the 8-B-per-lane
 # FETCH/WRITE calibration (tools/pmc_calib.py), and the drop-in call under a HIP API
 # trace (tools/host_path_trace.py), all under gpurun_out/<tag>/.
-# tools/make_profiles.py <tag> <prefix> turns them into profiles/<prefix>_*.
+# tools/make_profiles.py <tag> <prefix> turns them into profiles/<prefix>_*, and
+# tools/make_batch_pmc.py gpurun_out/<tag>/pmc_batch <prefix> the batch NN's PMC bytes.
 # usage: tools/round_profile.sh <tag>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 tag=${1:-r3}
@@ -17,6 +18,8 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/
 find "$out/prof" -name '*kernel_stats.csv' -exec cp {} "$out/kernel_stats.csv" \;
 PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|TCC_HIT_sum TCC_MISS_sum TA_TA_BUSY_sum TD_TD_BUSY_sum|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU|SQ_ACTIVE_INST_VMEM SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU SQ_LEVEL_WAVES SQ_INST_LEVEL_VMEM SQ_INSTS_VALU_FLOPS_FP64" \
     bash tools/pmc.sh "$tag/pmc" --no-extra > "$out/pmc.log" 2>&1 || { echo "pmc failed"; tail -5 "$out/pmc.log"; exit 1; }
+PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|TCC_HIT_sum TCC_MISS_sum" \
+    bash tools/pmc.sh "$tag/pmc_batch" --workload batch --no-extra > "$out/pmc_batch.log" 2>&1 || { echo "batch pmc failed"; tail -5 "$out/pmc_batch.log"; exit 1; }
 i=0
 for ctr in FETCH_SIZE WRITE_SIZE; do
   i=$((i + 1))

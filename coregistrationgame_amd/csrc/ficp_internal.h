@@ -295,10 +295,13 @@ struct IterState;
 // loop state allows the window path (win_ok), each k_nn_grid_q workgroup classifies its own
 // kWinNNRows rows right after writing them, and k_sel_win_tail (one workgroup) decides.
 constexpr int kWinNNRows = 1024;
-// -DFICP_WIN_NN_BUILD=0: a library without the fused pass (A/B of its register cost in the
-// NN kernel; the host then runs k_sel_win's own pass)
+// Measured slower than k_sel_win's own pass (C3, 40-step A/B: 9,017-9,114 it/s against
+// 9,196-9,296): the pass adds ~6 us to each certified NN launch (its loads after the
+// workgroup's slowest scan, 96 VGPRs with spills against 87), and the separate tail reads
+// ~1,000 records cold (records phase 12.7 vs 7.1 us).  Built only with
+// -DFICP_WIN_NN_BUILD=1 (then FICP_WIN_NN=0 turns it off at run time).
 #ifndef FICP_WIN_NN_BUILD
-#define FICP_WIN_NN_BUILD 1
+#define FICP_WIN_NN_BUILD 0
 #endif
 struct NNWin {
     const IterState *st;        // nullable: no fused pass

@@ -2531,9 +2531,9 @@ __device__ unsigned long long g_winp[8];
 __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap &m0, double lamv,
                                          IterState *st, const LoopCtl &lc, int *host_flag,
                                          const FitSrc &fs, int force_retry, Scr &scr) {
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int t = threadIdx.x;
 #ifdef FICP_WIN_PROF
-    unsigned long long wt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long wt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (phase stamps, FICP_WIN_PROF)
 #endif
     WINP_T(0);
     __shared__ __align__(16) unsigned char sm[W_SMEM];
@@ -2558,83 +2558,69 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     }
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
-    const int G = (nwb + HT - 1) / HT;  // this thread's records: [g0, g1) (in order)
-    const int g0 = min(nwb, t * G), g1 = min(nwb, g0 + G);
-    constexpr int GMAX = 8;  // records per thread (nwb <= W_MAXWG)
-    long long nb_t = 0, nw_t = 0, bad_t = nwb > W_MAXWG ? 1 : 0;
-    long long nwg[GMAX];
-    double sb_t = 0.0, sw_t = 0.0, f8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    u64 kra_t = 0ULL, krb_t = 0ULL;  // max(~key), max(key) over this thread's records
-#pragma unroll
-    for (int q = 0; q < GMAX; ++q) {
-        const int g = g0 + q;
-        nwg[q] = 0;
-        if (g < g1) {
-            const u64 *rec = w.wrec + (int64_t)g * WREC;
-            u64 v[15];
-#pragma unroll
-            for (int e = 0; e < 15; ++e) v[e] = __hip_atomic_load(&rec[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sw_t = sw_t + __longlong_as_double((long long)v[12]);
-            kra_t = max(kra_t, v[13]);
-            krb_t = max(krb_t, v[14]);
-            nb_t += (long long)v[0];
-            nwg[q] = (long long)v[1];
-            nw_t += (long long)v[1];
-            bad_t += (long long)v[2];
-            sb_t = sb_t + __longlong_as_double((long long)v[3]);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f8[e] = f8[e] + __longlong_as_double((long long)v[4 + e]);
-        }
-    }
-    // one reduction for all of them (one barrier): DPP wave sums / the window rows' wave
-    // scan, lane 63's totals in LDS, the waves added in order (the same fixed trees as
-    // blk_sum and blk_sum8_add)
-    __shared__ double s_rr[NWAVE][14];
+    // The records, read coalesced: 16 lanes per record (lane e reads word e), 32 records per
+    // pass of the workgroup (a record per thread read 15 scattered words: ~9 us for the
+    // fused pass's ~1,000 records).  Thread (e, r0) accumulates word e of records r0, r0 +
+    // 32, ... in that order; the 32 partials of a word are then added in r0 order (a fixed
+    // tree: deterministic), the window-row counts kept per record for their offsets.
+    using LY = LdsLay<CAP, true>;
+    unsigned *s_off = (unsigned *)(sm + LY::BC);  // [nwb + 1] (the sort's bin area, free until it)
+    static_assert(2 * NSB >= W_MAXWG + 1, "workgroup offsets in the bin area");
+    // the 32 partials of each word: in the window rows' key area (free until they load)
+    u64 (*s_part)[HT / 16 + 1] = reinterpret_cast<u64 (*)[HT / 16 + 1]>(sm + LY::K);
+    static_assert(16 * (HT / 16 + 1) * 8 <= CAP * 8, "record partials in the key area");
+    __shared__ u64 s_tot[16];
     {
-        const long long nwi = wave_incl_scan_ll(nw_t);
-        const double sbw = wave_sum63(sb_t);
-        const double sww = wave_sum63(sw_t);
-        wave_range_reduce(kra_t, krb_t);
-        const u64 cnt = wave_sum63_u64((u64)nb_t | ((u64)min(bad_t, 1LL) << 40));
+        const int e = t & 15, r0 = t >> 4;
+        constexpr int RP = HT / 16;
+        u64 iacc = 0ULL;  // e 0-2: integer sums; 13, 14: max
+        double dacc = 0.0;  // e 3-12: fp64 sums in record order
+        // UR records' loads in flight per thread before their first use (a plain loop
+        // waited for each load in turn: ~31 dependent latencies at ~1,000 records)
+        constexpr int UR = 16;
+        for (int rb = r0; rb < nwb; rb += UR * RP) {  // (rb: uniform per 16-lane group)
+            u64 v[UR];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f8[e] = wave_sum63(f8[e]);
-        if (lane == 63) {
-            s_rr[wave][0] = __longlong_as_double((long long)cnt);
-            s_rr[wave][1] = __longlong_as_double(nwi);
-            s_rr[wave][2] = sbw;
+            for (int u = 0; u < UR; ++u) {
+                const int r = rb + u * RP;
+                v[u] = r < nwb ? __hip_atomic_load(&w.wrec[(int64_t)r * WREC + e], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0ULL;
+            }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s_rr[wave][3 + e] = f8[e];
-            s_rr[wave][11] = sww;
-            s_rr[wave][12] = __longlong_as_double((long long)kra_t);
-            s_rr[wave][13] = __longlong_as_double((long long)krb_t);
+            for (int u = 0; u < UR; ++u) {
+                const int r = rb + u * RP;
+                if (r >= nwb) break;
+                if (e == 1) s_off[r] = (unsigned)v[u];  // window rows of record r
+                if (e < 3) iacc += v[u];
+                else if (e < 13) dacc = dacc + __longlong_as_double((long long)v[u]);
+                else if (e < 15) iacc = max(iacc, v[u]);
+            }
         }
-        nw_t = nwi - nw_t;  // exclusive inside the wave
+        s_part[e][r0] = (e >= 3 && e < 13) ? (u64)__double_as_longlong(dacc) : iacc;
+        __syncthreads();
+        if (t < 15) {
+            u64 ia = 0ULL;
+            double da = 0.0;
+            for (int q = 0; q < RP; ++q) {
+                const u64 v = s_part[t][q];
+                if (t < 3) ia += v;
+                else if (t < 13) da = da + __longlong_as_double((long long)v);
+                else ia = max(ia, v);
+            }
+            s_tot[t] = (t >= 3 && t < 13) ? (u64)__double_as_longlong(da) : ia;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    long long K0 = 0, Wt = 0, woff = nw_t, bad = 0;
-    double S0 = 0.0, Swin = 0.0;
-    u64 kra = 0ULL, krb = 0ULL;
-#pragma unroll
-    for (int q = 0; q < NWAVE; ++q) {
-        const u64 cq = (u64)__double_as_longlong(s_rr[q][0]);
-        const long long wq = __double_as_longlong(s_rr[q][1]);
-        K0 += (long long)(cq & ((1ULL << 40) - 1ULL));
-        bad += (long long)(cq >> 40);
-        if (q < wave) woff += wq;
-        Wt += wq;
-        S0 = S0 + s_rr[q][2];
-        Swin = Swin + s_rr[q][11];
-        kra = max(kra, (u64)__double_as_longlong(s_rr[q][12]));
-        krb = max(krb, (u64)__double_as_longlong(s_rr[q][13]));
-    }
+    const long long K0 = (long long)s_tot[0], Wt = (long long)s_tot[1];
+    const long long bad = (long long)s_tot[2] + (nwb > W_MAXWG ? 1 : 0);
+    const double S0 = __longlong_as_double((long long)s_tot[3]);
+    const double Swin = __longlong_as_double((long long)s_tot[12]);
+    const u64 kra = s_tot[13], krb = s_tot[14];
     WMap m = m0;  // with the call's key range (the lowest coarse bucket's lowest r)
     m.kmin = ~kra;
     m.kmax = krb;
-    if (t < 8) {
-        double v = 0.0;
-        for (int q = 0; q < NWAVE; ++q) v = v + s_rr[q][3 + t];
-        s_fit[t] = v;  // (the window rows' part is added after the sort)
-    }
+    if (t < 8) s_fit[t] = __longlong_as_double((long long)s_tot[4 + t]);  // (+ the window rows' part after the sort)
     bool fail = bad != 0 || Wt <= 0 || Wt > CAP;
     const double p = 2.0 * lamv + 1.0;
     // each coarse bucket's lower bound of h (k_sel_bounds' block_lb), before the sort: only
@@ -2661,24 +2647,29 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     }
     WINP_T(1);
     // the window rows into LDS, in workgroup order (lds_sort_scan's layout + work rows)
-    using LY = LdsLay<CAP, true>;
     u64 *lk = (u64 *)(sm + LY::K);
     double *lr = (double *)(sm + LY::R);
     uint32_t *lo = (uint32_t *)(sm + LY::O);
     uint32_t *lrow = (uint32_t *)(sm + W_ROW);
-    // each workgroup's first candidate index (in the sort's bin area, free until the sort),
-    // then every candidate loads its slot: one round of loads (a per-workgroup loop of
-    // dependent loads serialised them)
-    unsigned *s_off = (unsigned *)(sm + LY::BC);  // [nwb + 1]
-    static_assert(2 * NSB >= W_MAXWG + 1, "workgroup offsets in the bin area");
-    if (!fail) {
-#pragma unroll
-        for (int q = 0; q < GMAX; ++q)
-            if (g0 + q < g1) {
-                s_off[g0 + q] = (unsigned)woff;
-                woff += nwg[q];
+    // each workgroup's first candidate index (in the sort's bin area, free until the sort):
+    // an exclusive scan of the records' window-row counts, a contiguous run per thread; then
+    // every candidate loads its slot: one round of loads (a per-workgroup loop of dependent
+    // loads serialised them)
+    {
+        const int G = (nwb + HT - 1) / HT;
+        const int g0 = min(nwb, t * G), g1 = min(nwb, g0 + G);
+        long long loc = 0;
+        for (int g = g0; g < g1; ++g) loc += s_off[g];
+        long long tot_unused;
+        long long off = blk_excl_scan_ll(loc, scr, tot_unused);  // (its barriers: s_off read)
+        if (!fail) {
+            for (int g = g0; g < g1; ++g) {
+                const unsigned c = s_off[g];
+                s_off[g] = (unsigned)off;
+                off += c;
             }
-        if (t == 0) s_off[nwb] = (unsigned)Wt;
+            if (t == 0) s_off[nwb] = (unsigned)Wt;
+        }
     }
     __syncthreads();
     if (!fail) {
@@ -2795,6 +2786,10 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     if (t == 0 && host_flag)
         __hip_atomic_store(host_flag, s_st.done | (win_ok(s_st) ? kFlagWinNext : 0),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef FICP_WIN_PROF
+    WINP_T(5);
+    if (t == 0) printf("WINPROF_END fit+publish %llu (10 ns)\n", wt_[5] - wt_[4]);
+#endif
 }
 
 __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t *orig, int64_t n,
@@ -3038,6 +3033,7 @@ __global__ __launch_bounds__(HT) void k_sel_win_tail(int nwb, int64_t n, SelWS w
                                                     LoopCtl lc, int *host_flag, FitSrc fs,
                                                     int force_retry) {
     __shared__ Scr scr;
+    WINP_B(6);
     const int sk = st->done;
     const int ph = st->phase, itv = st->it, stg = st->stage, wfl = st->wfloor;
     const long long kprev = st->k;

@@ -529,6 +529,18 @@ def borrowed(device: int | None = None, nn_mode: int = NN_AUTO):
         release_context(ctx)
 
 
+@contextlib.contextmanager
+def lent(ctx: Context):
+    """borrowed() for a context acquired elsewhere (the constructor's prefetch)."""
+    try:
+        yield ctx
+    except BaseException:
+        ctx.close()
+        raise
+    else:
+        release_context(ctx)
+
+
 def drain_pool():
     """Destroy every idle pooled context (frees their device and pinned memory)."""
     with _pool_lock:

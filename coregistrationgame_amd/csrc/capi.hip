@@ -1435,10 +1435,16 @@ int ficp_host_copy(void *dst, const void *src, int64_t bytes) {
     if (bytes < 0 || (bytes > 0 && (!dst || !src))) return fail(FICP_EINVAL, "bad arguments");
     char *d = (char *)dst;
     const char *s = (const char *)src;
-    // 2 MiB pieces per thread at least: below that the thread start costs more than it saves
+    // 2 MiB pieces per thread at least (host_parallel); each piece with streaming stores when
+    // the destination is 16-B aligned: a plain memcpy of a ~1.5 MiB piece stays under
+    // glibc's non-temporal threshold and reads every destination line first (FICP_HOST_NT=0:
+    // plain memcpy)
+    static const bool nt = !(getenv("FICP_HOST_NT") && atoi(getenv("FICP_HOST_NT")) == 0);
     host_parallel((bytes + 15) / 16, [&](int64_t a, int64_t b) {
         const int64_t lo = a * 16, hi = std::min<int64_t>(b * 16, bytes);
-        if (hi > lo) memcpy(d + lo, s + lo, (size_t)(hi - lo));
+        if (hi <= lo) return;
+        if (nt) stream_copy(d + lo, s + lo, (size_t)(hi - lo));
+        else memcpy(d + lo, s + lo, (size_t)(hi - lo));
     });
     return FICP_OK;
 }

@@ -4,6 +4,7 @@
 #include "../../include/ficp.h"
 #include "ficp_internal.h"
 
+#include <emmintrin.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -386,6 +387,31 @@ class HostPool {
     std::atomic<unsigned long long> claim_{0};
     unsigned long long gen_ = 0;
 };
+
+// memcpy with non-temporal 16-B stores (SSE2, baseline x86-64) into a 16-B aligned
+// destination: no read-for-ownership of the destination lines, which a large copy into a
+// fresh pinned block would otherwise pay (3 memory transfers per byte instead of 2)
+inline void stream_copy(char *d, const char *s, size_t bytes) {
+    size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+    if (head > bytes) head = bytes;
+    memcpy(d, s, head);
+    d += head;
+    s += head;
+    bytes -= head;
+    const size_t nv = bytes / 64;
+    for (size_t i = 0; i < nv; ++i) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(s + 64 * i));
+        const __m128i b = _mm_loadu_si128((const __m128i *)(s + 64 * i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i *)(s + 64 * i + 32));
+        const __m128i e = _mm_loadu_si128((const __m128i *)(s + 64 * i + 48));
+        _mm_stream_si128((__m128i *)(d + 64 * i), a);
+        _mm_stream_si128((__m128i *)(d + 64 * i + 16), b);
+        _mm_stream_si128((__m128i *)(d + 64 * i + 32), c);
+        _mm_stream_si128((__m128i *)(d + 64 * i + 48), e);
+    }
+    _mm_sfence();
+    memcpy(d + 64 * nv, s + 64 * nv, bytes - 64 * nv);
+}
 
 template <typename F>
 inline void host_parallel(int64_t n, F f) {

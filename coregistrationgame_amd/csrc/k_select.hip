@@ -2590,11 +2590,12 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
 #pragma unroll
             for (int u = 0; u < UR; ++u) {
                 const int r = rb + u * RP;
-                if (r >= nwb) break;
-                if (e == 1) s_off[r] = (unsigned)v[u];  // window rows of record r
-                if (e < 3) iacc += v[u];
-                else if (e < 13) dacc = dacc + __longlong_as_double((long long)v[u]);
-                else if (e < 15) iacc = max(iacc, v[u]);
+                if (r < nwb) {
+                    if (e == 1) s_off[r] = (unsigned)v[u];  // window rows of record r
+                    if (e < 3) iacc += v[u];
+                    else if (e < 13) dacc = dacc + __longlong_as_double((long long)v[u]);
+                    else if (e < 15) iacc = max(iacc, v[u]);
+                }
             }
         }
         s_part[e][r0] = (e >= 3 && e < 13) ? (u64)__double_as_longlong(dacc) : iacc;

@@ -19,11 +19,44 @@ There is no CPU fallback: without the library or a GPU the methods raise.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
 
 from . import _lib
+
+_PREFETCH = None  # worker threads of the constructor's target prefetch (see __init__)
+
+
+def _prefetch_pool():
+    global _PREFETCH
+    if _PREFETCH is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _PREFETCH = ThreadPoolExecutor(max_workers=2, thread_name_prefix="ficp-prefetch")
+    return _PREFETCH
+
+
+def _plain_rows(a) -> bool:
+    """A C-contiguous float64 2-D array large enough for the pinned pool: np.array(a,
+    dtype=float) of it is a plain copy that cannot fail, so copy order is unobservable."""
+    return (isinstance(a, np.ndarray) and a.dtype == np.float64 and a.ndim == 2 and a.flags.c_contiguous
+            and a.nbytes >= _lib.HOST_POOL_MIN)
+
+
+def _prefetch_target(tgt, md, device, nn_mode):
+    ctx = _lib.acquire_context(device, nn_mode)
+    try:
+        ctx.set_target(tgt, md)
+    except BaseException:
+        ctx.close()
+        raise
+    return ctx
+
+
+def _release_done(fut):
+    if not fut.cancelled() and fut.exception() is None:
+        _lib.release_context(fut.result())
 
 
 class FractionalICP:
@@ -50,9 +83,23 @@ class FractionalICP:
         """
         t0 = time.perf_counter()
         # np.array(source, dtype=float) copies (ficp.py:34-35); large layers land in pooled
-        # page-locked blocks (_lib.copy_array): no page faults, unstaged uploads
-        self.source = _lib.copy_array(source)
-        self.target = _lib.copy_array(target)
+        # page-locked blocks (_lib.copy_array): no page faults, unstaged uploads.  When both
+        # copies are plain memcpys (the Join's arrays), the target is copied first and its
+        # upload to a pooled context (+ the grid's inputs) starts on a worker thread while
+        # the source is copied: run() then finds the CHM layer on the device.
+        # FICP_PREFETCH=0: no prefetch.
+        self._prefetch = None
+        if (_plain_rows(source) and _plain_rows(target) and len(source) and len(target)
+                and os.environ.get("FICP_PREFETCH", "1") != "0"):
+            self.target = _lib.copy_array(target)
+            md = 3 if (source.shape[1] >= 3 and target.shape[1] >= 3) else 2
+            mode = {"auto": _lib.NN_AUTO, "brute": _lib.NN_BRUTE, "grid": _lib.NN_GRID}[nn_mode]
+            self._prefetch = (_prefetch_pool().submit(_prefetch_target, self.target, md, device, mode),
+                              self.target, md)
+            self.source = _lib.copy_array(source)
+        else:
+            self.source = _lib.copy_array(source)
+            self.target = _lib.copy_array(target)
         self._ctor_ms = 1e3 * (time.perf_counter() - t0)  # host-path accounting (last_stats)
 
         if self.source.ndim != 2 or self.target.ndim != 2:
@@ -74,8 +121,29 @@ class FractionalICP:
         context creation or device allocation."""
         return _lib.borrowed(self.device, self.nn_mode)
 
+    def _take_prefetch(self):
+        """The pooled context the constructor uploaded self.target to (None: none, or the
+        attribute has been replaced since, or the match dims changed)."""
+        pf, self._prefetch = getattr(self, "_prefetch", None), None
+        if pf is None:
+            return None
+        fut, tgt, md = pf
+        if tgt is not self.target or md != self.match_dims:
+            fut.add_done_callback(_release_done)
+            return None
+        return fut.result()  # (raises what the upload raised: no GPU, bad layer)
+
     def close(self):
-        """Kept for callers that release explicitly; the instance holds nothing."""
+        """Releases the constructor's prefetched context, if run() has not used it."""
+        pf, self._prefetch = getattr(self, "_prefetch", None), None
+        if pf is not None:
+            pf[0].add_done_callback(_release_done)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     # ----------------- helpers (ficp.py:47-51) -----------------
     def _xy(self, pts):
@@ -176,15 +244,19 @@ class FractionalICP:
         rows = np.ascontiguousarray(self.source, dtype=np.float64)
         src = _lib.host_array(rows.shape)
         t1 = time.perf_counter()
-        with self._borrow() as ctx:
+        pre = self._take_prefetch()  # (set_target below: the wait for the prefetch)
+        with (_lib.lent(pre) if pre is not None else self._borrow()) as ctx:
             t2 = time.perf_counter()
             # the CHM rows go over with their leading dimension (no column-slice copy)
-            ctx.set_target(np.ascontiguousarray(self.target, dtype=np.float64), self.match_dims)
+            if pre is None:
+                ctx.set_target(np.ascontiguousarray(self.target, dtype=np.float64), self.match_dims)
             t3 = time.perf_counter()
             st = ctx.run_into(rows, src, lambdas, self.threshold, self.max_iterations,
                               self.allow_reflection, trace=trace, trace_idx=trace_idx)
             t4 = time.perf_counter()
         t5 = time.perf_counter()
+        if pre is not None:  # the prefetch wait belongs to set_target
+            t1, t2 = t1, t1
         # where the call's host time went (ms): the constructor's copies, this copy, the
         # pool, the CHM upload + grid inputs, the library run (its own phases in
         # st["lib_host_ms"], the device loop in st["gpu_ms"]) and the release

@@ -328,12 +328,14 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         auto enqueue = [&](Sub &u, int64_t bit) -> int {
             int *flag = &u.ring[bit % kBatchRing];
             __atomic_store_n(flag, -1, __ATOMIC_RELEASE);
-            const bool prof = u.s == c->stream;  // kernel timing covers the first sub-batch
+            // kernel timing: every sub-batch's launches, with events on its own stream (the
+            // NN roofline divides every plot's NN bytes by the sum of the launch times)
+            const bool prof = true;
             PlotState *su = st + u.p0;
             const int64_t *sou = b.so.as<int64_t>() + u.p0;
             const PlotGrid *gu = b.grids.as<PlotGrid>() + u.p0;
             if (!bfuse) {
-                ProfScope ps(c, prof ? P_FIT : 0, "batch_fit");
+                ProfScope ps(c, prof ? P_FIT : 0, "batch_fit", u.s);
                 HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
                                         b.key.as<unsigned long long>(), sou, gu, u.np, max_rows,
                                         allow_refl, su, b.fpart.as<double>() + (size_t)u.p0 * fch,
@@ -353,7 +355,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             au.gap = a.gap + u.r0;
             au.dz2 = a.dz2 ? a.dz2 + u.r0 : nullptr;
             {
-                ProfScope ps(c, prof ? P_NN : 0, "nn_grid_batch");
+                ProfScope ps(c, prof ? P_NN : 0, "nn_grid_batch", u.s);
                 HIPCHK(launch_nn_grid_batch(au, b.plot_of.as<int32_t>() + u.r0, b.grids.as<PlotGrid>(),
                                             b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
                                             md, u.s));
@@ -364,7 +366,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             su_step.arrive = b.arrive.as<unsigned long long>() + (&u - subs);
             su_step.flag = flag;
             {
-                ProfScope ps(c, prof ? P_FRAC : 0, "batch_select");
+                ProfScope ps(c, prof ? P_FRAC : 0, "batch_select", u.s);
                 HIPCHK(launch_batch_select(b.key.as<unsigned long long>(), b.r.as<double>(), sou, u.np,
                                            max_rows, b.lams.as<double>(), su, ws, u.s,
                                            bfuse ? &su_step : nullptr));

@@ -250,17 +250,20 @@ struct KernelEvents {
 struct ProfScope {
     ficp_ctx *c;
     const char *name;
+    hipStream_t s;
     hipEvent_t a = nullptr;
-    ProfScope(ficp_ctx *c_, int cls, const char *n) : c(c_), name(n) {
+    // (stream: the launches' stream when not the context's, e.g. a batch sub-stream)
+    ProfScope(ficp_ctx *c_, int cls, const char *n, hipStream_t stream = nullptr)
+        : c(c_), name(n), s(stream ? stream : c_->stream) {
         if (c->prof_mask & cls) {
             a = ev_get(c);
-            (void)hipEventRecord(a, c->stream);
+            (void)hipEventRecord(a, s);
         }
     }
     ~ProfScope() {
         if (a) {
             hipEvent_t b = ev_get(c);
-            (void)hipEventRecord(b, c->stream);
+            (void)hipEventRecord(b, s);
             c->recs.push_back({name, a, b});
         }
     }

@@ -281,7 +281,10 @@ typedef float gap_t;
 constexpr int kWinSlot = 64, kWinRec = 16;
 // copies of the coarse buckets, one per XCD (blockIdx % 8): memory-side atomics on one word
 // serialise (~88 per us), and 977 NN workgroups on 256 words took ~11 us
-constexpr int kWinCopies = 8;
+#ifndef FICP_WIN_COPIES
+#define FICP_WIN_COPIES 8
+#endif
+constexpr int kWinCopies = FICP_WIN_COPIES;
 struct WinPassOut {
     unsigned long long *wrec;
     unsigned long long *wsk;

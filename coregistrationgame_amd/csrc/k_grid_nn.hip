@@ -442,6 +442,9 @@ __device__ __forceinline__ unsigned long long write_out(const NNArgs &a, int64_t
 #ifndef FICP_NN_SKIP_SAME
 #define FICP_NN_SKIP_SAME 1
 #endif
+#ifndef FICP_NN_SKIP_SINGLE  // (the single-plot kernels: A/B, tools/build_variant.sh)
+#define FICP_NN_SKIP_SINGLE 0
+#endif
 __device__ __forceinline__ void finish_same(const NNArgs &a, int64_t i, const Best &b,
                                             unsigned long long &kmin_c, unsigned long long &kmax);
 
@@ -938,7 +941,8 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
     return pend;
 }
 
-static_assert(kWinNNRows == 256 * QPT, "the fused window pass classifies one k_nn_grid_q workgroup");
+static_assert(!FICP_WIN_NN_BUILD || kWinNNRows == 256 * QPT,
+              "the fused window pass classifies one k_nn_grid_q workgroup");
 
 
 template <int MD, bool APPLY, int Q, bool SKIP = false>
@@ -1046,6 +1050,7 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g,
 
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
+    constexpr bool SK1 = FICP_NN_SKIP_SINGLE != 0;
     // the three flags load together (the apply flag's load used to wait for the other two)
     const int sk = a.skip ? *a.skip : 0, ru = a.reuse ? *a.reuse : 0;
     const int ap = (APPLY && a.apply_flag) ? *a.apply_flag : 1;
@@ -1080,15 +1085,15 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
         const int64_t i0 = i - threadIdx.x;
         const int t = threadIdx.x;
         if (a.cert_block >= 16 && tot <= 16) {
-            if (t < tot * 16) cert_scan_group<MD, 16>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
+            if (t < tot * 16) cert_scan_group<MD, 16, SK1>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
         } else if (a.cert_block >= 8 && tot <= 32) {
-            if (t < tot * 8) cert_scan_group<MD, 8>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
+            if (t < tot * 8) cert_scan_group<MD, 8, SK1>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
         } else if (a.cert_block >= 4 && tot <= 64) {
-            if (t < tot * 4) cert_scan_group<MD, 4>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
+            if (t < tot * 4) cert_scan_group<MD, 4, SK1>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
         } else if (a.cert_block >= 2 && tot <= 128) {
-            if (t < tot * 2) cert_scan_group<MD, 2>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
+            if (t < tot * 2) cert_scan_group<MD, 2, SK1>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
         } else if (t < tot) {
-            cert_scan<MD>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
+            cert_scan<MD, SK1>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
         }
     } else if (i < a.n) {
         if (a.gap && !a.warm_c) {
@@ -1108,7 +1113,7 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
 
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) NNQ_WPE void k_nn_grid_q(NNArgs a, GridView g) {
-    nn_grid_body<MD, APPLY, QPT>(a, g, xcd_block(blockIdx.x, gridDim.x) * (256 * QPT));
+    nn_grid_body<MD, APPLY, QPT, FICP_NN_SKIP_SINGLE != 0>(a, g, xcd_block(blockIdx.x, gridDim.x) * (256 * QPT));
 }
 
 // Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against

@@ -722,6 +722,8 @@ hipError_t launch_put_xy_rows(const double *x, const double *y, int64_t n, int64
                               hipStream_t s);
 hipError_t launch_interleave_xy(const double *x, const double *y, int64_t n, double *out_xy,
                                 hipStream_t s);
+// n16 16-B words from src to dst (device buffers, 16-B aligned, not overlapping)
+hipError_t launch_copy16(const void *src, void *dst, int64_t n16, hipStream_t s);
 // Two-level bucket sort of points by a grid key (k_bsort.hip).  mode 0: key = cell id
 // cy * gx + cx (grid layout: TPt records + cell_start); mode 1: 8x8-supertile order
 // (work order: SoA coordinates + caller index).  Order: (key, point index).

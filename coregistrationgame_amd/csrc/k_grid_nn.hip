@@ -1561,6 +1561,22 @@ __global__ __launch_bounds__(256) void k_put_xy_rows(const double *x, const doub
     rows[i * ld + 1] = y[i];
 }
 
+// device-to-device copy of n 16-B words (ficp_memcpy_d2d on aligned buffers): four
+// independent loads per thread in flight, a grid that covers the array once
+__global__ __launch_bounds__(256) void k_copy16(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
 // empty shard: +inf distance, an index no real stem has (never chosen by the merge)
 __global__ __launch_bounds__(256) void k_fill_inf(double *d2, int32_t *idx, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1739,6 +1755,15 @@ hipError_t launch_put_xy_rows(const double *x, const double *y, int64_t n, int64
                               hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_put_xy_rows, dim3(nblk(n)), dim3(256), 0, s, x, y, n, ld, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy16(const void *src, void *dst, int64_t n16, hipStream_t s) {
+    if (n16 <= 0) return hipSuccess;
+    // one pass of 4 words per thread: 1M x 16 B (C3's x, y columns) = 1,024 workgroups
+    const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n16 + 1023) / 1024, 1), 8192);
+    hipLaunchKernelGGL(k_copy16, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4 *)src, (uint4 *)dst,
+                       n16);
     return hipGetLastError();
 }
 

@@ -57,3 +57,36 @@ def test_unused_prefetch_is_returned():
     a = icp.run()
     b = FractionalICP(p.source, p.target).run()
     np.testing.assert_array_equal(a, b)
+
+
+def test_memcpy_d2d_copy_kernel_and_fallback():
+    """ficp_memcpy_d2d: the 16-B copy kernel on aligned disjoint ranges, the runtime copy on
+    the rest (odd sizes and offsets); every byte outside the destination range untouched."""
+    import ctypes as C
+    from coregistrationgame_amd import _lib
+    ctx = _lib.Context(0)
+    L = _lib.lib()
+    nb = 1 << 22
+    rng = np.random.default_rng(11)
+    host = rng.integers(0, 256, nb, dtype=np.uint8)
+    bufs = []
+    for _ in range(2):
+        p = C.c_void_p()
+        _lib._check(L.ficp_dev_alloc(ctx.h, nb, C.byref(p)))
+        bufs.append(p.value)
+    a, b = bufs
+    try:
+        _lib._check(L.ficp_memcpy_h2d(ctx.h, C.c_void_p(a), host.ctypes.data_as(C.c_void_p), nb))
+        for (so, do, size) in [(0, 0, nb), (16, 32, 1 << 20), (0, 0, 16), (0, 0, 48), (0, 0, 17),
+                               (8, 0, 4096), (3, 5, 100_003), (16, 16, 3 * (1 << 20) + 16), (0, 0, 0)]:
+            fill = np.full(nb, 0xA5, np.uint8)
+            _lib._check(L.ficp_memcpy_h2d(ctx.h, C.c_void_p(b), fill.ctypes.data_as(C.c_void_p), nb))
+            _lib._check(L.ficp_memcpy_d2d(ctx.h, C.c_void_p(b + do), C.c_void_p(a + so), size))
+            got = np.zeros(nb, np.uint8)
+            _lib._check(L.ficp_memcpy_d2h(ctx.h, got.ctypes.data_as(C.c_void_p), C.c_void_p(b), nb))
+            exp = fill.copy()
+            exp[do:do + size] = host[so:so + size]
+            np.testing.assert_array_equal(got, exp, err_msg=f"src+{so} dst+{do} {size} B")
+    finally:
+        for p in bufs:
+            L.ficp_dev_free(ctx.h, C.c_void_p(p))

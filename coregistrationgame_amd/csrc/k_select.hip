@@ -168,7 +168,7 @@ struct SelWS {
     double *sblb;    // [NB / 4] smallest lower bound of h in each run of 4 buckets (+inf:
                      // empty)
     long long *sbcb; // [NB / 4] rows in the buckets before each run
-    double *fpre;    // [SMALL_C][4] fused fit: the pair of pack slots < SMALL_C (gather)
+    double *fpre;    // [CAP][4] fused fit: the pair of pack slots < CAP (gather)
     // the window path (k_sel_win):
     NNWin *nnwin;    // the fused pass's inputs (k_run_start writes them per run)
     u64 *wrec;       // [gather blocks][WREC] each workgroup's record (sc1 stores)
@@ -252,7 +252,7 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.ublk = (double *)take((NB / 64) * 8);
     x.sblb = (double *)take(NB / 4 * 8);
     x.sbcb = (long long *)take(NB / 4 * 8);
-    x.fpre = (double *)take(SMALL_C * 32);
+    x.fpre = (double *)take(CAP * 32);
     // (k_sel_win's workgroups or the fused pass's NN workgroups, whichever are more)
     const int64_t gbw = std::max<int64_t>(gather_blocks(n), (nn + kWinNNRows - 1) / kWinNNRows);
     x.wrec = (u64 *)take(gbw * WREC * 8);
@@ -1363,7 +1363,7 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
                 w.oa[p] = orig ? orig[i] : (uint32_t)i;
                 w.ra[p] = rr[q];
                 w.pa[p] = (uint32_t)i;
-                if (fs.on && p < (unsigned)SMALL_C) {  // final_small's pairs, no row lookup
+                if (fs.on && p < (unsigned)CAP) {  // the final's pairs, no row lookup
                     w.fpre[4 * p] = fxs[q];
                     w.fpre[4 * p + 1] = fys[q];
                     w.fpre[4 * p + 2] = fxt[q];
@@ -1670,15 +1670,37 @@ __device__ ScanOut lds_sort_scan(const Cand &src, unsigned c, long long K0, doub
 }
 
 // (a) c <= CAPT candidates: one sorted scan, the fused fit's selected candidates, publish
+// fpre (nullable): the pairs the gather stored by pack slot (the candidates not refined):
+// 32 B per candidate from one 128-KB array instead of a work-row lookup and four loads
+// into four 8-MB columns per candidate (C3's stage head, ~2,000 candidates: 10.5 us for
+// the fit after the scan, TLB-bound)
 template <int CAPT, bool RL>
 __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsigned char *sm,
-                          Scr &scr, IterState *st) {
+                          Scr &scr, IterState *st, const double *fpre = nullptr) {
     const ScanOut r = lds_sort_scan<CAPT, RL>(src, c, in.K0, in.S0, in, sm, scr);
     if (in.fs.on && r.bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
         const uint16_t *pos = (const uint16_t *)(sm + LdsLay<CAPT, RL>::POS);
+        const unsigned nsel = (unsigned)(r.bk - in.K0);
         double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (unsigned q = threadIdx.x; q < (unsigned)(r.bk - in.K0); q += HT)
-            fit_row(cf, in.fs, src.p[pos[q]]);
+        if (fpre) {
+            // positions t, t + HT, ... in increasing order, as the row lookup below; four
+            // positions' loads issued together (clamped indices, the sums predicated)
+            for (unsigned q0 = threadIdx.x; q0 < nsel; q0 += 4 * HT) {
+                double2 a[4], b[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const unsigned q = q0 + (unsigned)j * HT;
+                    const unsigned e = pos[q < nsel ? q : q0];
+                    a[j] = *reinterpret_cast<const double2 *>(fpre + 4 * e);
+                    b[j] = *reinterpret_cast<const double2 *>(fpre + 4 * e + 2);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (q0 + (unsigned)j * HT < nsel) fit_add(cf, a[j].x, a[j].y, b[j].x, b[j].y, in.fs.px, in.fs.py);
+            }
+        } else {
+            for (unsigned q = threadIdx.x; q < nsel; q += HT) fit_row(cf, in.fs, src.p[pos[q]]);
+        }
         blk_sum8_add(cf, in.fsum, scr);
     }
     if (threadIdx.x == 0) publish(st, in, r.bf, r.bk, r.tk, r.to);
@@ -2352,7 +2374,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
             }
             final_small(q, c, in, sm, scr, &s_st);
         } else if (c <= (unsigned)CAP) {
-            final_lds<CAP, true>(src, c, in, sm, scr, &s_st);
+            final_lds<CAP, true>(src, c, in, sm, scr, &s_st, (lev == 0 && fs.on) ? w.fpre : nullptr);
         } else if (c <= (unsigned)CAP2) {
             final_lds<CAP2, false>(src, c, in, sm, scr, &s_st);
         } else if (!fs.on && final_chunked(src, dst, c, in, sm, scr, &s_st, s_gbeg)) {
@@ -2408,6 +2430,12 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
                (long long)(g[21] - g[1]), (long long)(g[22] - g[21]), (long long)(g[23] - g[22]),
                (long long)(g[24] - g[23]), (long long)(g[25] - g[24]), (long long)(g[5] - g[25]),
                (long long)(g[6] - g[5]));
+        if (c > (unsigned)SMALL_C)  // the binned LDS sort's phases (lds_sort_scan), then the fit
+            printf("SELPROF_LDS load %lld minmax %lld count %lld scan %lld scatter %lld rank %lld "
+                   "prefix %lld frmsd %lld argmin+fit %lld\n",
+                   (long long)(g[2] - g[1]), (long long)(g[16] - g[2]), (long long)(g[17] - g[16]),
+                   (long long)(g[18] - g[17]), (long long)(g[19] - g[18]), (long long)(g[3] - g[19]),
+                   (long long)(g[20] - g[3]), (long long)(g[4] - g[20]), (long long)(g[5] - g[4]));
     }
 #endif
 }

@@ -2586,6 +2586,7 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     }
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
+    WINP_T(6);
     // The records, read coalesced: 16 lanes per record (lane e reads word e), 32 records per
     // pass of the workgroup (a record per thread read 15 scattered words: ~9 us for the
     // fused pass's ~1,000 records).  Thread (e, r0) accumulates word e of records r0, r0 +
@@ -2628,6 +2629,7 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
         }
         s_part[e][r0] = (e >= 3 && e < 13) ? (u64)__double_as_longlong(dacc) : iacc;
         __syncthreads();
+        WINP_T(7);
         if (t < 15) {
             u64 ia = 0ULL;
             double da = 0.0;
@@ -2780,6 +2782,8 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     fail = fail || blk_max_ll(ok ? 0 : 1, scr) != 0 || force_retry;  // (its barriers publish s_tko)
     WINP_T(4);
 #ifdef FICP_WIN_PROF
+    if (t == 0)
+        printf("WINPROF_REC coarse+state %llu records %llu rest %llu\n", wt_[6] - wt_[0], wt_[7] - wt_[6], wt_[1] - wt_[7]);
     if (t == 0)
         printf("WINPROF W=%lld K0=%lld fail=%d | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu (10 ns)\n",
                Wt, K0, (int)fail, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],

@@ -2631,13 +2631,22 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
         __syncthreads();
         WINP_T(7);
         if (t < 15) {
+            // the 32 partials loaded together, then added in q order (one LDS round trip
+            // instead of 32 dependent ones)
+            u64 pv[RP];
+#pragma unroll
+            for (int q = 0; q < RP; ++q) pv[q] = s_part[t][q];
             u64 ia = 0ULL;
             double da = 0.0;
-            for (int q = 0; q < RP; ++q) {
-                const u64 v = s_part[t][q];
-                if (t < 3) ia += v;
-                else if (t < 13) da = da + __longlong_as_double((long long)v);
-                else ia = max(ia, v);
+            if (t < 3) {
+#pragma unroll
+                for (int q = 0; q < RP; ++q) ia += pv[q];
+            } else if (t < 13) {
+#pragma unroll
+                for (int q = 0; q < RP; ++q) da = da + __longlong_as_double((long long)pv[q]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < RP; ++q) ia = max(ia, pv[q]);
             }
             s_tot[t] = (t >= 3 && t < 13) ? (u64)__double_as_longlong(da) : ia;
         }

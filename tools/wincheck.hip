@@ -235,7 +235,7 @@ int main(int argc, char **argv) {
     // floors: lh = floor + 1 (tmove 0); the last one is past the limit (lh > hmax: the
     // launch must refuse at once)
     const int floors[5] = {std::max(kWinHMinLog, wstart - 3), wstart, wstart + 2, whmax - 1, whmax};
-    int bad = 0, n_win = 0, n_fb = 0, cases = 0;
+    int bad = 0, n_win = 0, n_fb = 0;
     float t_win = 0.f;
     int n_t = 0;
     for (int fl : floors) {
@@ -256,7 +256,6 @@ int main(int argc, char **argv) {
             {"far_below", sat_sub(tk, 512 * H)},
         };
         for (const auto &pl : places) {
-            ++cases;
             IterState s0{};
             s0.phase = PH_LOOP;
             s0.stage = 0;

@@ -2561,7 +2561,7 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
                                          const FitSrc &fs, int force_retry, Scr &scr) {
     const int t = threadIdx.x;
 #ifdef FICP_WIN_PROF
-    unsigned long long wt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (phase stamps, FICP_WIN_PROF)
+    unsigned long long wt_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // (phase stamps, FICP_WIN_PROF)
 #endif
     WINP_T(0);
     __shared__ __align__(16) unsigned char sm[W_SMEM];
@@ -2791,9 +2791,9 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     fail = fail || blk_max_ll(ok ? 0 : 1, scr) != 0 || force_retry;  // (its barriers publish s_tko)
     WINP_T(4);
 #ifdef FICP_WIN_PROF
-    if (t == 0)
+    if (fail && t == 0)
         printf("WINPROF_REC coarse+state %llu records %llu rest %llu\n", wt_[6] - wt_[0], wt_[7] - wt_[6], wt_[1] - wt_[7]);
-    if (t == 0)
+    if (fail && t == 0)
         printf("WINPROF W=%lld K0=%lld fail=%d | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu (10 ns)\n",
                Wt, K0, (int)fail, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
                g_winp[5] - g_winp[4], g_winp[2] - g_winp[5], g_winp[6] - g_winp[2], wt_[0] - g_winp[6],
@@ -2811,6 +2811,7 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
         for (int e = t; e < (int)Wt; e += HT)
             if (!less_ko(tk, to, lk[e], lo[e])) fit_row(cf8, fs, lrow[e]);
     if (fs.on) blk_sum8_add(cf8, s_fit, scr);
+    WINP_T(8);
     if (t == 0) {
         publish(&s_st, in, rs.bf, rs.bk, tk, to);
         // the next window's smallest half-width from this one's row count (2^lh keys)
@@ -2824,13 +2825,22 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
             fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
     }
     __syncthreads();
+    WINP_T(9);
     for (int q = t; q < SW; q += HT) ((uint32_t *)st)[q] = ((const uint32_t *)&s_st)[q];
     if (t == 0 && host_flag)
         __hip_atomic_store(host_flag, s_st.done | (win_ok(s_st) ? kFlagWinNext : 0),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef FICP_WIN_PROF
     WINP_T(5);
-    if (t == 0) printf("WINPROF_END fit+publish %llu (10 ns)\n", wt_[5] - wt_[4]);
+    // (printed after the last stamp: a device printf is a host round trip)
+    if (t == 0)
+        printf("WINPROF_REC coarse+state %llu records %llu rest %llu | fit %llu step %llu store %llu\n", wt_[6] - wt_[0],
+               wt_[7] - wt_[6], wt_[1] - wt_[7], wt_[8] - wt_[4], wt_[9] - wt_[8], wt_[5] - wt_[9]);
+    if (t == 0)
+        printf("WINPROF W=%lld K0=%lld fail=0 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu fit+publish %llu (10 ns)\n",
+               Wt, K0, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
+               g_winp[5] - g_winp[4], g_winp[2] - g_winp[5], g_winp[6] - g_winp[2], wt_[0] - g_winp[6],
+               wt_[1] - wt_[0], wt_[2] - wt_[1], wt_[3] - wt_[2], wt_[4] - wt_[3], wt_[5] - wt_[4]);
 #endif
 }
 

@@ -424,11 +424,12 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
     ps0 = ctx.path_stats()
     barrier()
     t0 = time.perf_counter()
-    fits = calls = timed_calls = 0
+    fits = calls = timed_calls = reused = 0
     for s_i in range(steps):
         st = step()
         fits += st["n_fits"]
         calls += st["n_nn_calls"]
+        reused += st.get("n_nn_reused", 0)
         if args.nn_timing == "all" or (args.nn_timing == "first" and s_i == 0):
             # NN launches that searched: a later stage's head reuses the previous call's
             # outputs (its launch is a no-op, kept in nn["ms"]: conservative)
@@ -440,10 +441,10 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
     ps1 = ctx.path_stats()
     ctx.profile_enable(0)
     prof = json.loads(ctx.profile_report())
-    dt_max, fits_all, calls_all = dt, fits, calls
+    dt_max, fits_all, calls_all, reused_all = dt, fits, calls, reused
     if D is not None:
         dt_max = D.max([dt])[0]
-        fits_all, calls_all = D.sum([fits, calls])
+        fits_all, calls_all, reused_all = D.sum([fits, calls, reused])
     out = None
     if rank == 0:
         nn = prof.get("nn_grid") or prof.get("nn_brute") or {"count": 0, "ms": 0.0}
@@ -466,7 +467,12 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
                        "nn": args.nn_mode},
             "iterations_per_step": fits_all / steps / world,
             "nn_calls_per_step": calls_all / steps / world,
-            "correspondences_per_s": calls_all * n / dt_max,
+            # correspondences searched per second: a later stage's head answers its NN call
+            # from the previous call's outputs (the source has not moved, ficp.py:151-153),
+            # so that call is not counted; the count of every call, reused included, beside it
+            "correspondences_per_s": (calls_all - reused_all) * n / dt_max,
+            "correspondences_per_s_incl_reused": calls_all * n / dt_max,
+            "nn_calls_reused_per_step": reused_all / steps / world,
             # fraction calls per run decided by the one-launch window path
             # and those that fell back to the full selection
             "selection_paths": {"fraction_calls_per_run": calls / steps,

@@ -221,10 +221,8 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             bool want_keys, int warm = 0, const int *skip = nullptr,
             const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true,
             const int *reuse = nullptr, bool store_key = true, bool multi = false,
-            const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr,
-            const NNWin *win = nullptr) {
+            const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr) {
     NNArgs a{};
-    a.win = win;  // k_nn_grid_q: the window selection's fused pass (device-side inputs)
     a.fin_orig = fin_orig;
     a.fin_x = fin_x;
     a.fin_y = fin_y;
@@ -539,25 +537,8 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     const char *wv = getenv("FICP_SEL_WIN");
     const bool use_win = fused && fuse_fit && keys_from_r && use_grid(c, n) && select_win_fits(n) &&
                          !(wv && atoi(wv) == 0);
-    // ... and its pass fused into the certified NN kernel of the same call (k_nn_grid_q):
-    // the NN workgroups classify their rows as they write them and one workgroup decides
-    // (k_sel_win_tail).  FICP_WIN_NN=0: k_sel_win's own pass.
-    const char *wn = getenv("FICP_WIN_NN");
-    const bool win_nn = FICP_WIN_NN_BUILD && use_win && select_win_nn_blocks(n) > 0 && !(wn && atoi(wn) == 0);
-    NNWin nnw{};
-    NNWin *nnw_dev = nullptr;
-    if (win_nn) {
-        CHK(ensure_bbox(c));  // (the descriptor carries the pivot)
-        CHK(c->worig.ensure((n + 1) * 4));  // (build_work_order's buffer, allocated here first)
-        nnw.st = dst;
-        nnw.orig = c->worig.as<uint32_t>();
-        nnw.o = select_win_out(c->sel_tmp.p, n);
-        nnw.px = c->pivot_x;
-        nnw.py = c->pivot_y;
-        nnw_dev = select_win_desc(c->sel_tmp.p);
-    }
     HIPCHK(launch_run_start(tflag, &c->h_rep->t[0], c->stream, sel_err_word(c->sel_tmp.p, n), dst,
-                            &lc, nnw_dev, win_nn ? &nnw : nullptr));
+                            &lc));
     // the CHM layer's bbox (grid plan, pivot) after k_run_start: that launch is queued
     // before the host waits for the bbox instead of after it
     CHK(ensure_bbox(c));
@@ -597,7 +578,6 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
     // part A of iteration i: the fit and the NN call; part B: the selection (and, not
     // fused, the loop step and the flag copy)
     int64_t last_a = -1;  // the last iteration whose fit + NN were enqueued
-    const int64_t win_nn_from = std::max<int64_t>(nn_multi_from, 1);
     auto enq_a = [&](int64_t i) -> int {
         if (!(fused && fuse_fit)) {
             ProfScope ps(c, P_FIT, "fit");
@@ -607,19 +587,13 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         // (a launch queued behind the loop's end writes the caller-order XY: fin_*)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
                     false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from,
-                    worig, sx, sy, (win_nn && i >= win_nn_from) ? nnw_dev : nullptr));
+                    worig, sx, sy));
         last_a = i;
         return FICP_OK;
     };
     auto enq_b = [&](int64_t i, bool win) -> int {
         const int slot = (int)(i % kLoopRing);
         if (fused) __atomic_store_n(&c->h_flags[slot], -1, __ATOMIC_RELAXED);
-        if (win && win_nn && i >= win_nn_from) {  // call i's NN ran the pass
-            ProfScope ps(c, P_SORT, "select");
-            HIPCHK(launch_select_win_tail(n, c->sel_tmp.p, dst, lc, &c->h_flags[slot], c->stream, fsrc,
-                                          c->fault));
-            return FICP_OK;
-        }
         if (win) {
             ProfScope ps(c, P_SORT, "select");
             HIPCHK(launch_select_win(c->r.as<double>(), worig, n, range_ptr(c),
@@ -1203,10 +1177,25 @@ int ficp_run_into(ficp_ctx *c, const double *src, double *out, int64_t n, int64_
                  c->md == 3 ? c->sz.as<double>() : nullptr, n, nstages, lambdas, threshold,
                  max_iterations, allow_reflection, stats));
     const auto t2 = clk::now();
+    const bool pinned = host_pinned(out);
+    if (out == src && !pinned) {
+        // in place into pageable rows (ficp_run): only the moved XY come back (16 B per
+        // row through the pinned staging), the caller's other columns are already right
+        HIPCHK(launch_interleave_xy(c->sx.as<double>(), c->sy.as<double>(), n, c->stage.as<double>(),
+                                    c->stream));
+        CHK(d2h_xy_columns(c, c->stage.as<double>(), n, out, ld));
+        if (stats) {
+            stats->host_ms[0] = ms(t0, t1);
+            stats->host_ms[1] = ms(t1, t2);
+            stats->host_ms[2] = ms(t2, clk::now());
+            stats->host_ms[3] = 0.0;
+        }
+        return FICP_OK;
+    }
     HIPCHK(launch_put_xy_rows(c->sx.as<double>(), c->sy.as<double>(), n, ld, c->stage.as<double>(),
                               c->stream));
     const size_t bytes = (size_t)n * (size_t)ld * 8;
-    if (host_pinned(out)) {
+    if (pinned) {
         HIPCHK(hipMemcpyAsync(out, c->stage.p, bytes, hipMemcpyDeviceToHost, c->stream));
         CHK(sync(c));
     } else {

@@ -265,6 +265,15 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // resets its own); zeroed here, before the fork, so an earlier failed run leaves none
         CHK(b.arrive.ensure(kMaxSub * 8));
         HIPCHK(hipMemsetAsync(b.arrive.p, 0, kMaxSub * 8, c->stream));
+        // the per-call k trace is cleared here too, before the fork: the sub-streams write
+        // their plots' rows as soon as the fork event lets them run
+        long long *trace = nullptr;  // per-call k of every plot (ficp_set_batch_trace), -1 = none
+        if (c->btrace_host && c->btrace_max > 0) {
+            const size_t tb = (size_t)nplots * (size_t)c->btrace_max * 8;
+            CHK(c->btrace.ensure(tb));
+            HIPCHK(hipMemsetAsync(c->btrace.p, 0xff, tb, c->stream));
+            trace = c->btrace.as<long long>();
+        }
         // Joins the sub-batch streams back into the context's stream on EVERY exit of this
         // scope, error returns included: kernels still queued on a sub-stream must finish
         // before the next run's uploads and memsets on c->stream reuse their buffers.
@@ -317,14 +326,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         const bool bfuse = !(bf && atoi(bf) == 0);
         BatchStepArgs step{sx, sy, b.ccx.as<double>(), b.ccy.as<double>(), b.grids.as<PlotGrid>(),
                            allow_refl, nstages, max_iter, threshold};
-        long long *trace = nullptr;  // per-call k of every plot (ficp_set_batch_trace), -1 = none
-        if (c->btrace_host && c->btrace_max > 0) {
-            const size_t tb = (size_t)nplots * (size_t)c->btrace_max * 8;
-            CHK(c->btrace.ensure(tb));
-            HIPCHK(hipMemsetAsync(c->btrace.p, 0xff, tb, c->stream));
-            trace = c->btrace.as<long long>();
-            step.max_trace = c->btrace_max;
-        }
+        if (trace) step.max_trace = c->btrace_max;
         auto enqueue = [&](Sub &u, int64_t bit) -> int {
             int *flag = &u.ring[bit % kBatchRing];
             __atomic_store_n(flag, -1, __ATOMIC_RELEASE);

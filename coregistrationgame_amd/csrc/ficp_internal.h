@@ -285,33 +285,7 @@ constexpr int kWinSlot = 64, kWinRec = 16;
 #define FICP_WIN_COPIES 8
 #endif
 constexpr int kWinCopies = FICP_WIN_COPIES;
-struct WinPassOut {
-    unsigned long long *wrec;
-    unsigned long long *wsk;
-    double *wsr;
-    uint32_t *wso, *wsp;
-    unsigned *gcc;
-    unsigned long long *gcf;
-};
 struct IterState;
-// The window pass fused into the certified NN kernel (k_grid_nn.hip nn_win_pass): when the
-// loop state allows the window path (win_ok), each k_nn_grid_q workgroup classifies its own
-// kWinNNRows rows right after writing them, and k_sel_win_tail (one workgroup) decides.
-constexpr int kWinNNRows = 1024;
-// Measured slower than k_sel_win's own pass (C3, 40-step A/B: 9,017-9,114 it/s against
-// 9,196-9,296): the pass adds ~6 us to each certified NN launch (its loads after the
-// workgroup's slowest scan, 96 VGPRs with spills against 87), and the separate tail reads
-// ~1,000 records cold (records phase 12.7 vs 7.1 us).  Built only with
-// -DFICP_WIN_NN_BUILD=1 (then FICP_WIN_NN=0 turns it off at run time).
-#ifndef FICP_WIN_NN_BUILD
-#define FICP_WIN_NN_BUILD 0
-#endif
-struct NNWin {
-    const IterState *st;        // nullable: no fused pass
-    const uint32_t *orig;       // caller index per work row (the selection's tie-break)
-    WinPassOut o;
-    double px, py;              // fit pivot
-};
 
 struct NNArgs {
     double *sx;                 // source x (updated in place when T != nullptr)
@@ -351,8 +325,6 @@ struct NNArgs {
     // fin_x[fin_orig[p]] = sx[p] (k_scatter_xy's work, no launch or host round trip of its own)
     const uint32_t *fin_orig;
     double *fin_x, *fin_y;
-    const NNWin *win;           // k_nn_grid_q: the fused window pass's inputs (device memory,
-                                // written by k_run_start; nullable: no pass)
 };
 
 // k_scatter_xy's work for rows [p0, p0 + cnt) of the work order
@@ -687,8 +659,7 @@ hipError_t launch_report(const ReportSeg &a, const ReportSeg &b, const ReportSeg
 // also initialise the loop state *st (the work of launch_loop_init, one launch less)
 hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s,
                             unsigned *selerr = nullptr, IterState *st = nullptr,
-                            const LoopCtl *lc = nullptr, NNWin *win_dst = nullptr,
-                            const NNWin *win_val = nullptr);
+                            const LoopCtl *lc = nullptr);
 
 // grid build (k_grid_nn.hip)
 // bbox of (x, y) -> out4 {xmin, xmax, ymin, ymax}; with ox, also copies x, y (z) there
@@ -845,14 +816,6 @@ hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
 // whether one k_sel_win launch can decide n rows (its records hold <= W_MAXWG workgroups;
 // larger layers would fail every window call and pay a retry round trip)
 bool select_win_fits(int64_t n);
-// the fused form (k_grid_nn.hip nn_win_pass + k_sel_win_tail): NN workgroups of n rows
-// (0: too many for one tail), the pass's output arrays inside the selection workspace, and
-// the tail's launch (the same outputs, flags and fallback as launch_select_win)
-int select_win_nn_blocks(int64_t n);
-WinPassOut select_win_out(void *tmp, int64_t n);
-NNWin *select_win_desc(void *tmp);  // the NNWin slot of the workspace (n-independent offset)
-hipError_t launch_select_win_tail(int64_t n, void *tmp, IterState *st, const LoopCtl &loop,
-                                  int *host_flag, hipStream_t s, const FitSrc &fit, int fault = 0);
 // test-only fault injection (ficp_set_fault): block 0 of k_sel_bounds_gather publishes a
 // wrong token, so every gather block times out (ERR_SPIN)
 constexpr int FICP_FAULT_SPIN = 1;

@@ -134,9 +134,6 @@ __global__ void k_batch_init(const int64_t *so, const int64_t *to, int nplots, i
 #ifndef FICP_BSEL_ST
 #define FICP_BSEL_ST 512
 #endif
-#ifndef FICP_BSEL_WIN
-#define FICP_BSEL_WIN 0  // the per-plot window path (measured slower, see k_batch_select)
-#endif
 #ifndef FICP_BSEL_RCACHE
 #define FICP_BSEL_RCACHE 1  // r kept in registers too (0: re-read from L2 in its two passes)
 #endif
@@ -404,7 +401,6 @@ struct BatchStep {
     unsigned long long *arrive;  // (arrivals << 32) + live plots of this launch (nullable)
     int *flag;                   // the last arrival stores the live count (pinned host word)
     int nplots;
-    int win;                     // the window path (FICP_BSEL_WIN=0: off)
     long long *trace;            // per-call k trace, max_trace per plot of this launch (nullable)
     int max_trace;
 };
@@ -583,147 +579,14 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
         }
     }
     BSEL_T(0);
-    // 0. The window path (a loop body after a loop body of this stage, as the single-plot
-    //    k_sel_win): rows below a key window around the previous threshold are counted and
-    //    summed, the window's rows ranked exactly, every other row counted into coarse
-    //    buckets whose widths grow with their distance from the window; the first minimum
-    //    inside the window stands if every coarse bucket's lower bound of h exceeds it
-    //    (frmsd_bounds.h), else the full selection below runs.  It skips the key range,
-    //    the 2048-bucket histogram and its bounds (~13 of the ~24 us per plot at C4), but
-    //    measured slower (128 plots: 793-797k vs 866-867k plot-it/s; 1024 plots equal): the
-    //    cached kernel went 205 -> 255 VGPRs with spills, and a plot's window holds few rows
-    //    (10k rows per plot), so the path often fell back.  Compile-time option
-    //    (-DFICP_BSEL_WIN=1, then FICP_BSEL_WIN=0 at run time turns it off).
-#if FICP_BSEL_WIN
-    if (CACHED && bs.fuse && bs.win && ph == PH_LOOP && s_it >= 1 && s_kprev > 0 && pe >= 1.0) {
-        const fb::WMap m0 = fb::win_map(s_tkey, s_tmove, s_wfl, N);
-        if (m0.ok) {  // (uniform per workgroup)
-            constexpr int NCW = 2 * fb::kWinNCS;
-            static_assert(NCW <= ST, "one coarse bucket per thread");
-            __shared__ unsigned w_cc[NCW];
-            __shared__ u64 w_cf[NCW];
-            __shared__ int w_ce[NCW];
-            __shared__ unsigned w_n;
-            __shared__ u64 w_aux[3];
-            if (t < NCW) {
-                w_cc[t] = 0u;
-                w_cf[t] = 0ULL;
-                w_ce[t] = fb::win_bucket_exp(m0, t);
-            }
-            if (t == 0) w_n = 0u;
-            __syncthreads();
-            unsigned cnt = 0;  // rows below (low 16 bits) + non-finite rows (high 16)
-            double sb = 0.0;
-            u64 kmn = ~0ULL;
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) {
-                const int64_t i = b + t + (int64_t)q * ST;
-                const u64 kk = kc[q];
-                const double rv = BSEL_RCACHE ? rc[q] : (i < e ? r[i] : INFINITY);
-                if (i < e) {
-                    if (!(rv < INFINITY)) {
-                        cnt += 1u << 16;
-                        continue;
-                    }
-                    kmn = min(kmn, kk);
-                    int bw = -1;
-                    if (kk < m0.wlo) {
-                        cnt += 1u;
-                        sb = sb + rv;
-                        bw = fb::kWinNCS - 1 - fb::win_cq((m0.wlo - 1ULL - kk) >> m0.su);
-                    } else if (kk < m0.whi) {
-                        const unsigned sl = atomicAdd(&w_n, 1u);
-                        if (sl < (unsigned)WCAP) {
-                            l_wk[sl] = kk;
-                            l_wr[sl] = rv;
-                            l_wrow[sl] = (uint32_t)i;
-                        }
-                    } else {
-                        bw = fb::kWinNCS + fb::win_cq((kk - m0.whi) >> m0.su);
-                    }
-                    if (bw >= 0) {
-                        const int eb = w_ce[bw];
-                        atomicAdd(&w_cc[bw], 1u);
-                        atomicAdd(&w_cf[bw], eb < 1024 ? (u64)ldexp(rv, m0.fxb - eb) : 0ULL);
-                    }
-                }
-            }
-            u64 ka = ~kmn, kz = 0ULL;
-            blk_max2_sum(ka, kz, cnt, red);  // (its barriers publish w_n and the buckets)
-            const long long K0w = (long long)(cnt & 0xffffu);
-            const unsigned Wn = w_n;
-            const double S_b = blk_sum_d(sb, red);
-            bool fail = (cnt >> 16) != 0 || Wn == 0u || Wn > (unsigned)ST;
-            double bfw = INFINITY;
-            long long bkw = 0x7fffffffffffffffLL;
-            double U = INFINITY, Swin = 0.0;
-            if (!fail) {
-                // exact (key, row) order of the window: one row per thread, ranked against all
-                if ((unsigned)t < Wn) {
-                    const u64 kq = l_wk[t];
-                    const uint32_t rq = l_wrow[t];
-                    unsigned rank = 0;
-                    for (unsigned j = 0; j < Wn; ++j)
-                        rank += (l_wk[j] < kq || (l_wk[j] == kq && l_wrow[j] < rq)) ? 1u : 0u;
-                    l_sk[rank] = kq;
-                    l_sr[rank] = l_wr[t];
-                    l_srow[rank] = rq;
-                }
-                __syncthreads();
-                const double v = (unsigned)t < Wn ? l_sr[t] : 0.0;
-                const double S = S_b + (blk_excl_scan_d(v, Swin, red) + v);
-                if ((unsigned)t < Wn) {
-                    const long long k = K0w + t + 1;
-                    bfw = (1.0 / pow((double)k / (double)N, lam)) * sqrt(S / (double)k);
-                    bkw = bfw == bfw ? k : 0x7fffffffffffffffLL;  // (NaN: never a minimum)
-                    if (bkw == 0x7fffffffffffffffLL) bfw = INFINITY;
-                }
-                blk_argmin(bfw, bkw, red);
-                fail = bkw == 0x7fffffffffffffffLL;
-                if (!fail && K0w + t + 1 == bkw) w_aux[0] = (u64)__double_as_longlong(S);
-                __syncthreads();
-                if (!fail) U = fb::h_of(bkw, __longlong_as_double((long long)w_aux[0]), pe) + fb::kMarg;
-            }
-            // every coarse bucket's lower bound of h (rows before it: the buckets before it,
-            // + K0 + W above the window; lower sums: the fixed-point brackets, the window's
-            // exact S_base + window sum above it)
-            fb::WMap mk = m0;
-            mk.kmin = ~ka;
-            const unsigned cc = t < NCW ? w_cc[t] : 0u;
-            const int eb = t < NCW ? w_ce[t] : 0;
-            const double los = (t < NCW && eb < 1024) ? ldexp((double)w_cf[t], eb - m0.fxb) : 0.0;
-            unsigned C0 = cc;
-            double Pb = t < fb::kWinNCS ? los : 0.0;
-            blk_excl_scan2(C0, Pb, red);
-            double Atot;
-            const double Pa = blk_excl_scan_d(t >= fb::kWinNCS && t < NCW ? los : 0.0, Atot, red);
-            long long okv = 1;
-            if (!fail && t < NCW) {
-                if (t == fb::kWinNCS - 1 && (long long)(C0 + cc) != K0w) okv = 0;  // (never)
-                if (cc) {
-                    const long long c0 = t < fb::kWinNCS ? (long long)C0 : (long long)C0 + Wn;
-                    const double P0 = t < fb::kWinNCS ? Pb : (S_b + Swin) + Pa;
-                    okv = fb::block_lb(c0, (long long)cc, P0, fb::lo_r(fb::win_bucket_lo(mk, t)), pe) > U;
-                }
-            }
-            long long okmin = okv, okmax = okv;
-            blk_minmax_ll(okmin, okmax, red);
-            if (!fail && okmin == 1) {
-                plot_step_fit<ST / 64>(st, p, bkw, (double)bkw / (double)N, bfw,
-                                       l_sk[bkw - K0w - 1], (long long)l_srow[bkw - K0w - 1], b, e,
-                                       key, bs, s_fit8, s_fitflag, (int)Wn);
-                return;
-            }
-            __syncthreads();  // (the full selection reuses the window's LDS)
-        }
-    }
-#else
+    // (A per-plot window path as k_sel_win measured slower here: 128 plots 793-797k vs
+    // 866-867k plot-it/s, 1024 plots equal -- 255 VGPRs with spills, and a 10k-row plot's
+    // window holds few rows; removed in round 5.)
     (void)s_it;
     (void)s_kprev;
     (void)s_tkey;
     (void)s_tmove;
     (void)s_wfl;
-#endif
     // 1. key range of the finite rows
     u64 amin = 0, kmax = 0;
     unsigned nfin = 0;
@@ -1259,8 +1122,6 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
         bs.nplots = nplots;
         bs.trace = step->trace;
         bs.max_trace = step->max_trace;
-        const char *wv = getenv("FICP_BSEL_WIN");
-        bs.win = !(wv && atoi(wv) == 0);
     }
     // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
     // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers)

@@ -19,7 +19,6 @@
 // Both fuse the pending rigid transform of the previous fit (ficp.py:135) into the
 // source load, and write idx, dist, d2, the sort key, and the matched stem's XY.
 #include "ficp_internal.h"
-#include "win_pass.h"
 
 #include <hip/hip_ext.h>
 
@@ -941,9 +940,6 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
     return pend;
 }
 
-static_assert(!FICP_WIN_NN_BUILD || kWinNNRows == 256 * QPT,
-              "the fused window pass classifies one k_nn_grid_q workgroup");
-
 
 template <int MD, bool APPLY, int Q, bool SKIP = false>
 __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g, int64_t i0) {
@@ -996,10 +992,6 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g,
             for (int e = t; e < tot; e += 256)
                 cert_scan<MD, SKIP>(a, g, S, i0 + s_list[e], true, cert_pad(g, s_mv[e]), kmin_c, kmax);
         }
-        // the window selection's pass on this workgroup's rows (uniform: the loop state)
-#if FICP_WIN_NN_BUILD
-        if (Q == QPT && a.win && win_ok(*a.win->st)) nn_win_pass<Q>(a, i0, i0 / (256 * Q));
-#endif
     } else {
         const Stems S = stems_of(g.pts, g.m);
         for (int q = 0; q < Q; ++q) {

@@ -67,9 +67,8 @@ __global__ __launch_bounds__(256) void k_trace_idx(const IterState *st, const in
 // event records, each of which left ~5 us of idle queue); with st, the loop state's
 // initialisation too (one launch less per run)
 __global__ void k_run_start(uint32_t *tflag, unsigned long long *t0, unsigned *selerr,
-                            IterState *st, LoopCtl lc, NNWin *win_dst, NNWin win_val) {
+                            IterState *st, LoopCtl lc) {
     if (threadIdx.x == 0) {
-        if (win_dst) *win_dst = win_val;  // the NN kernels' fused window pass inputs
         if (st) loop_init(st, lc);
         __hip_atomic_exchange(tflag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the selection's sticky error bits are per run (a failed run leaves no poison)
@@ -80,12 +79,10 @@ __global__ void k_run_start(uint32_t *tflag, unsigned long long *t0, unsigned *s
 }
 
 hipError_t launch_run_start(uint32_t *tflag, unsigned long long *t0, hipStream_t s,
-                            unsigned *selerr, IterState *st, const LoopCtl *lc, NNWin *win_dst,
-                            const NNWin *win_val) {
+                            unsigned *selerr, IterState *st, const LoopCtl *lc) {
     const LoopCtl c = lc ? *lc : LoopCtl{};
-    const NNWin w = win_val ? *win_val : NNWin{};
     hipLaunchKernelGGL(k_run_start, dim3(1), dim3(64), 0, s, tflag, t0, selerr, lc ? st : nullptr,
-                       c, win_val ? win_dst : nullptr, w);
+                       c);
     return hipGetLastError();
 }
 

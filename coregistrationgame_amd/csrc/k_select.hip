@@ -162,15 +162,8 @@ struct SelWS {
     uint32_t *oa, *ob;
     double *ra, *rb;
     uint32_t *pa, *pb;  // candidate row (work position): the fused fit reads its pair
-    // k_sel_reduce_bounds (the bounds spread over the reduce workgroups):
-    u64 *rbp;        // [RBLK * 5] each workgroup's bucket totals (count, lo, hi), tokened
-    double *ublk;    // [RBLK] upper bound of min h from each workgroup's bucket ends
-    double *sblb;    // [NB / 4] smallest lower bound of h in each run of 4 buckets (+inf:
-                     // empty)
-    long long *sbcb; // [NB / 4] rows in the buckets before each run
     double *fpre;    // [CAP][4] fused fit: the pair of pack slots < CAP (gather)
     // the window path (k_sel_win):
-    NNWin *nnwin;    // the fused pass's inputs (k_run_start writes them per run)
     u64 *wrec;       // [gather blocks][WREC] each workgroup's record (sc1 stores)
     u64 *wsk;        // [gather blocks][WSLOT] its window rows: key, r, caller index, work row
     double *wsr;
@@ -237,7 +230,6 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.gcc = (unsigned *)take(kWinCopies * NCB * 4);
     x.gcf = (u64 *)take(kWinCopies * NCB * 8);
     x.wctr = (unsigned *)take(9 * WCTR * 4);
-    x.nnwin = (NNWin *)take(sizeof(NNWin));
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
     x.fparts = (double *)take((int64_t)gather_blocks(n) * 64);
     x.ka = (u64 *)take(nn * 8);
@@ -248,13 +240,8 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.ob = (uint32_t *)take(nn * 4);
     x.pa = (uint32_t *)take(nn * 4);
     x.pb = (uint32_t *)take(nn * 4);
-    x.rbp = (u64 *)take((NB / 64) * 5 * 8);
-    x.ublk = (double *)take((NB / 64) * 8);
-    x.sblb = (double *)take(NB / 4 * 8);
-    x.sbcb = (long long *)take(NB / 4 * 8);
     x.fpre = (double *)take(CAP * 32);
-    // (k_sel_win's workgroups or the fused pass's NN workgroups, whichever are more)
-    const int64_t gbw = std::max<int64_t>(gather_blocks(n), (nn + kWinNNRows - 1) / kWinNNRows);
+    const int64_t gbw = gather_blocks(n);  // k_sel_win's workgroups
     x.wrec = (u64 *)take(gbw * WREC * 8);
     x.wsk = (u64 *)take(gbw * WSLOT * 8);
     x.wsr = (double *)take(gbw * WSLOT * 8);
@@ -829,220 +816,6 @@ __device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsig
     }
 }
 
-// k_sel_reduce + the bounds in one launch, spread over its NB / 64 workgroups (round 3:
-// the one-workgroup bounds took ~12 us at C3, and every gather block waited for them).
-// Workgroup j reduces buckets [64 j, 64 j + 64) (as k_sel_reduce), then its first wave:
-//  (1) scans its 64 buckets (count, lower and upper sum) and publishes the totals as five
-//      tokened 8-B granules (token in the high half: each granule is stored and seen whole,
-//      no fence; MI355X_MICROARCH.md hand-off table);
-//  (2) waits for the totals of workgroups 0..j-1 (dispatched before it: bounded spin, then
-//      ERR_SPIN), sums them in a fixed order: the rows and sums before its buckets;
-//  (3) evaluates every bucket: h at its end (an upper bound of the minimum) and the lower
-//      bound of h inside it, both exactly as the one-workgroup bounds did for the buckets
-//      it evaluated; stores the smallest upper bound of the workgroup and, per run of 4
-//      buckets, the smallest lower bound and the rows before the run.
-// The gather then takes U = min over workgroups and [b0, b1] = the first to the last run
-// whose lower bound is <= U (pre_bounds): the buckets bounds_body selects, and at most 3
-// more on either side.
-constexpr int RBLK = NB / RBPB;  // workgroups of the reduce
-__device__ __forceinline__ u64 tok_pack(unsigned gen, uint32_t v) { return ((u64)gen << 32) | v; }
-
-__global__ __launch_bounds__(1024) void k_sel_reduce_bounds(SelWS w, int nhb, const int *skip,
-                                                            HistPack hp, double lam,
-                                                            const double *lam_dev, unsigned gen,
-                                                            unsigned pub_gen) {
-    BPROF(64, 34);
-    const int sk = skip ? *skip : 0;
-    const double lamv = lam_dev ? *lam_dev : lam;
-    __shared__ unsigned s_c[RG][RBPB];
-    __shared__ u64 s_f[RG][RBPB];
-    const int bl = threadIdx.x % RBPB, g = threadIdx.x / RBPB;
-    const int bid = blockIdx.x;
-    const int b = bid * RBPB + bl;
-    const u64 mask = (1ULL << hp.shift) - 1ULL;
-    const int per = (nhb + RG - 1) / RG, q0 = g * per, q1 = min(nhb, q0 + per);
-    unsigned c = 0;
-    u64 f = 0;
-    int q = q0;
-    for (; q + 8 <= q1; q += 8) {
-        u64 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = w.ppk[(int64_t)(q + u) * NB + b];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            c += (unsigned)(v[u] >> hp.shift);
-            f += v[u] & mask;
-        }
-    }
-    for (; q < q1; ++q) {
-        const u64 v = w.ppk[(int64_t)q * NB + b];
-        c += (unsigned)(v >> hp.shift);
-        f += v & mask;
-    }
-    if (sk) return;
-    s_c[g][bl] = c;
-    s_f[g][bl] = f;
-    __syncthreads();
-    if (g != 0) return;
-#pragma unroll
-    for (int h = 1; h < RG; ++h) {
-        c += s_c[h][bl];
-        f += s_f[h][bl];
-    }
-    BPROF(64, 35);
-    const BMap bm = w.ctl->map;
-    const int e = bucket_exp(bm, b);
-    double lo, hi;
-    if (e >= 1024) {
-        lo = hi = c ? INFINITY : 0.0;
-    } else {
-        lo = ldexp((double)f, e - hp.fixb);
-        hi = ldexp((double)(f + c), e - hp.fixb);
-    }
-    // (1) inclusive scans over the 64 buckets in bucket order (a fixed pattern)
-    u64 ic = c;
-    double il = lo, ih = hi;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const u64 xc = __shfl_up(ic, o, 64);
-        const double xl = __shfl_up(il, o, 64), xh = __shfl_up(ih, o, 64);
-        if (bl >= o) {
-            ic += xc;
-            il = xl + il;
-            ih = xh + ih;
-        }
-    }
-    const u64 tc = __shfl(ic, 63, 64);
-    const double tl = __shfl(il, 63, 64), th = __shfl(ih, 63, 64);
-    if (bl == 0) {
-        const u64 ul = (u64)__double_as_longlong(tl), uh = (u64)__double_as_longlong(th);
-        u64 *pb = w.rbp + (int64_t)bid * 5;
-        __hip_atomic_store(pb + 0, tok_pack(pub_gen, (uint32_t)tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(pb + 1, tok_pack(pub_gen, (uint32_t)(ul >> 32)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(pb + 2, tok_pack(pub_gen, (uint32_t)ul), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(pb + 3, tok_pack(pub_gen, (uint32_t)(uh >> 32)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(pb + 4, tok_pack(pub_gen, (uint32_t)uh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (bid == 0) __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // (2) the totals of workgroups 0..bid-1: lane l takes workgroups l and l + 64
-    u64 pc = 0;
-    double pl = 0.0, ph = 0.0;
-    bool late = false;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int j = bl + 64 * h;
-        if (j >= bid) continue;
-        const u64 *pb = w.rbp + (int64_t)j * 5;
-        u64 v[5];
-        unsigned it = 0;
-        for (;;) {
-            bool ok = true;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                v[k] = __hip_atomic_load(pb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = ok && (unsigned)(v[k] >> 32) == gen;
-            }
-            if (ok) break;
-            if (++it == (1u << 20)) {  // >= ~30 ms: the run fails with ERR_SPIN, no hang
-                __hip_atomic_fetch_or(&w.ctl->err, ERR_SPIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                late = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (late) break;
-        pc += (uint32_t)v[0];
-        pl = pl + __longlong_as_double((long long)((v[1] << 32) | (v[2] & 0xffffffffULL)));
-        ph = ph + __longlong_as_double((long long)((v[3] << 32) | (v[4] & 0xffffffffULL)));
-    }
-    BPROF(64, 36);
-    pc = bcast63_u64(wave_sum63_u64(pc));
-    pl = bcast63(wave_sum63(pl));
-    ph = bcast63(wave_sum63(ph));
-    // (3) this bucket: rows and lower sum before it, upper sum through it
-    const u64 xc = __shfl_up(ic, 1, 64);
-    const double xl = __shfl_up(il, 1, 64);
-    const long long cb = (long long)(pc + (bl ? xc : 0ULL));
-    const double plo = pl + (bl ? xl : 0.0);
-    const double phi = ph + ih;
-    const double p = 2.0 * lamv + 1.0;
-    double hend = INFINITY, lb = INFINITY;
-    if (c) {
-        hend = h_of(cb + (long long)c, phi, p) + kMarg;
-        lb = (p >= 1.0) ? block_lb(cb, c, plo, lo_r(bucket_lo(bm, b)), p) : -INFINITY;
-    }
-    {  // runs of SBW = 4 buckets: their smallest lower bound and the rows before them
-        static_assert(NB / 4 == 2048, "sub-block layout");
-        double m = fmin(lb, dpp::mov_d<dpp::QP_XOR1>(INFINITY, lb));
-        m = fmin(m, dpp::mov_d<dpp::QP_XOR2>(INFINITY, m));
-        if ((bl & 3) == 0) {
-            w.sblb[b >> 2] = m;
-            w.sbcb[b >> 2] = cb;
-        }
-    }
-    const double um = wave_min63(hend);
-    if (bl == 63) w.ublk[bid] = um;
-    BPROF(64, 37);
-}
-
-// [b0, b1] and U from k_sel_reduce_bounds' per-bucket bounds (every gather block, GT
-// threads; a launch boundary after the reduce): U = min of the workgroups' upper bounds,
-// b0 / b1 = the first / last bucket whose lower bound is <= U (buckets of other
-// workgroups are skipped through their smallest lower bound).  Block 0 also stores b0,
-// b1, U and the rows below b0 for the final kernel.
-__device__ __forceinline__ void pre_bounds(const SelWS &w, int blk, int &b0, int &b1) {
-    // one round of loads: the workgroups' upper bounds and the 2048 runs of 4 buckets'
-    // smallest lower bounds.  [b0, b1] spans the first to the last run that may hold a
-    // candidate: the exact buckets plus at most 3 on either side (their rows are scanned
-    // exactly by the final, the answer is the same), without the dependent per-bucket load
-    // of the exact form (which took ~6 us at C3 against ~2 for the rest of the gather)
-    static_assert(RBLK == 128 && GT == 512, "two waves hold the reduce workgroups, 4 runs per thread");
-    __shared__ double s_u[GT / 64];
-    __shared__ int s_j[2 * (GT / 64)];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const double ub = t < RBLK ? w.ublk[t] : INFINITY;
-    const double4 sv = *reinterpret_cast<const double4 *>(w.sblb + 4 * t);
-    const double um = wave_min63(ub);
-    if (lane == 63) s_u[wv] = um;
-    __syncthreads();
-    const double U = fmin(s_u[0], s_u[1]);
-    int f = 0x7fffffff, l = -1;
-    if (!(sv.w > U)) { f = 4 * t + 3; l = 4 * t + 3; }
-    if (!(sv.z > U)) { f = 4 * t + 2; l = l < 0 ? 4 * t + 2 : l; }
-    if (!(sv.y > U)) { f = 4 * t + 1; l = l < 0 ? 4 * t + 1 : l; }
-    if (!(sv.x > U)) { f = 4 * t; l = l < 0 ? 4 * t : l; }
-    // block min of f, max of l (integers: any order)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        f = min(f, __shfl_xor(f, o, 64));
-        l = max(l, __shfl_xor(l, o, 64));
-    }
-    if (lane == 0) {
-        s_j[wv] = f;
-        s_j[GT / 64 + wv] = l;
-    }
-    __syncthreads();
-    int jf = s_j[0], jl = s_j[GT / 64];
-#pragma unroll
-    for (int q = 1; q < GT / 64; ++q) {
-        jf = min(jf, s_j[q]);
-        jl = max(jl, s_j[GT / 64 + q]);
-    }
-    if (jl < 0) {  // no bucket qualifies (non-finite r): every row is a candidate
-        b0 = 0;
-        b1 = NB - 1;
-    } else {
-        b0 = 4 * jf;
-        b1 = 4 * jl + 3;
-    }
-    if (blk == 0 && t == 0) {
-        w.ctl->b0 = b0;
-        w.ctl->b1 = b1;
-        w.ctl->U = U;
-        w.ctl->kbase = jl < 0 ? 0 : w.sbcb[jf];
-    }
-}
-
 // Bounds of the FRMSD curve over the level-0 buckets (one workgroup).  Per-thread
 // chunks of PER consecutive buckets; the per-bucket work (two or four log2 each) runs
 // only for the chunks that can hold the minimum, one bucket per lane (a chunk walked by
@@ -1241,7 +1014,7 @@ __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double la
 // published in ctl->bpub with the token gen; the rows' loads are issued before the wait
 __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig, const double *r,
                                             int64_t n, SelWS w, FitSrc fs, int blk,
-                                            unsigned gen, const int *skip, bool pre = false) {
+                                            unsigned gen, const int *skip) {
     GPROF(26);
     const int sk = skip ? *skip : 0;  // checked after the rows' loads have issued
     __shared__ double s_w[GT / 64];
@@ -1303,8 +1076,6 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
         __syncthreads();
         b0 = s_b[0];
         b1 = s_b[1];
-    } else if (pre) {
-        pre_bounds(w, blk, b0, b1);
     } else {
         b0 = w.ctl->b0;
         b1 = w.ctl->b1;
@@ -1407,8 +1178,8 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
 
 __global__ __launch_bounds__(GT) void k_sel_gather(const u64 *key, const uint32_t *orig,
                                                    const double *r, int64_t n, SelWS w,
-                                                   const int *skip, FitSrc fs, int pre) {
-    gather_body(key, orig, r, n, w, fs, blockIdx.x, 0u, skip, pre != 0);
+                                                   const int *skip, FitSrc fs) {
+    gather_body(key, orig, r, n, w, fs, blockIdx.x, 0u, skip);
 }
 
 // k_sel_bounds and k_sel_gather as one launch: block 0 computes the candidate buckets
@@ -2553,9 +2324,8 @@ __device__ unsigned long long g_winp[8];
     } while (0)
 #endif
 
-// The window path's decision (k_sel_win's last workgroup, or k_sel_win_tail after the NN's
-// fused pass, k_grid_nn.hip nn_win_pass): the coarse buckets (read and zeroed), the records
-// of the nwb pass workgroups
+// The window path's decision (k_sel_win's last workgroup): the coarse buckets (read and
+// zeroed), the records of the nwb pass workgroups
 __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap &m0, double lamv,
                                          IterState *st, const LoopCtl &lc, int *host_flag,
                                          const FitSrc &fs, int force_retry, Scr &scr) {
@@ -2620,7 +2390,7 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
             for (int u = 0; u < UR; ++u) {
                 const int r = rb + u * RP;
                 if (r < nwb) {
-                    if (e == 1) s_off[r] = (unsigned)v[u];  // window rows of record r
+                    if (e == 1 && r <= W_MAXWG) s_off[r] = (unsigned)v[u];  // window rows of record r
                     if (e < 3) iacc += v[u];
                     else if (e < 13) dacc = dacc + __longlong_as_double((long long)v[u]);
                     else if (e < 15) iacc = max(iacc, v[u]);
@@ -3078,33 +2848,6 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     win_tail(w, (int)gridDim.x, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
 }
 
-// The decision after the NN's fused window pass (k_grid_nn.hip nn_win_pass): one workgroup
-// reads the nwb NN workgroups' records, slots and coarse buckets and runs win_tail.  Its
-// state test is k_sel_win's, the one the NN kernel took (win_ok) on the same state.
-__global__ __launch_bounds__(HT) void k_sel_win_tail(int nwb, int64_t n, SelWS w, IterState *st,
-                                                    LoopCtl lc, int *host_flag, FitSrc fs,
-                                                    int force_retry) {
-    __shared__ Scr scr;
-    WINP_B(6);
-    const int sk = st->done;
-    const int ph = st->phase, itv = st->it, stg = st->stage, wfl = st->wfloor;
-    const long long kprev = st->k;
-    const u64 tkey = st->tkey, tmove = st->tmove;
-    const double lamv = st->lam_cur;
-    if (sk) {  // the run is over: the flag as k_sel_final's no-op
-        if (threadIdx.x == 0 && host_flag)
-            __hip_atomic_store(host_flag, kFlagDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-    }
-    const WMap m0 = win_map(tkey, tmove, wfl, n);
-    if (!(ph == PH_LOOP && (itv >= 1 || win_first_body(itv, stg, tmove)) && kprev > 0 &&
-          2.0 * lamv + 1.0 >= 1.0 && m0.ok)) {  // (never: the NN pass took the same test)
-        if (threadIdx.x == 0) win_retry(st, host_flag);
-        return;
-    }
-    win_tail(w, nwb, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
-}
-
 __global__ void k_sel_init(SelWS w) {
     if (threadIdx.x == 0) {
         __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3220,7 +2963,7 @@ hipError_t launch_select_dist_gather(const unsigned long long *key, const uint32
     const int gb = gather_blocks(n);
     if (n > 0)
         hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip,
-                           FitSrc{}, 0);
+                           FitSrc{});
     hipLaunchKernelGGL(k_sel_pack, dim3(1), dim3(HT), 0, s, w, n > 0 ? gb : 0, skip, pack, capd);
     return hipGetLastError();
 }
@@ -3240,32 +2983,13 @@ hipError_t launch_select_dist_final(const long long *packs, int world, int capd,
 
 bool select_win_fits(int64_t n) { return n > 0 && gather_blocks(n) <= W_MAXWG; }
 
-int select_win_nn_blocks(int64_t n) {
-    const int64_t b = (n + kWinNNRows - 1) / kWinNNRows;
-    return (n > 0 && b <= W_MAXWG) ? (int)b : 0;
-}
-
-NNWin *select_win_desc(void *tmp) { return carve(tmp, 0).nnwin; }
-
-WinPassOut select_win_out(void *tmp, int64_t n) {
-    const SelWS w = carve(tmp, n);
-    return WinPassOut{w.wrec, w.wsk, w.wsr, w.wso, w.wsp, w.gcc, w.gcf};
-}
-
-hipError_t launch_select_win_tail(int64_t n, void *tmp, IterState *st, const LoopCtl &loop,
-                                  int *host_flag, hipStream_t s, const FitSrc &fit, int fault) {
-    const int nwb = select_win_nn_blocks(n);
-    if (nwb <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_sel_win_tail, dim3(1), dim3(HT), 0, s, nwb, n, carve(tmp, n), st, loop,
-                       host_flag, fit, (fault & FICP_FAULT_WIN) ? 1 : 0);
-    return hipGetLastError();
-}
-
 hipError_t launch_select_win(const double *r, const uint32_t *orig, int64_t n,
                              const unsigned long long *range, int64_t range_parts, void *tmp,
                              IterState *st, const LoopCtl &loop, int *host_flag, hipStream_t s,
                              const FitSrc &fit, int fault) {
-    if (n <= 0 || !orig) return hipErrorInvalidValue;  // (the work order's caller indices)
+    // (the work order's caller indices; the tail's LDS holds the offsets of at most
+    // W_MAXWG workgroups, select_win_fits)
+    if (n <= 0 || !orig || !select_win_fits(n)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_sel_win, dim3(gather_blocks(n)), dim3(HT), 0, s, r, orig, n, range,
                        range_parts, carve(tmp, n), st, loop, host_flag, fit,
                        (fault & FICP_FAULT_WIN) ? 1 : 0);
@@ -3296,38 +3020,24 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     unsigned gen = ++s_gen & 0x3fffffffu;
     if (gen == 0) gen = ++s_gen & 0x3fffffffu;  // 0 means "no flag"
     const unsigned pub = (fault & FICP_FAULT_SPIN) ? (gen ^ 0x40000000u) : gen;
-    // Three forms of the bounds:
+    // Two forms of the bounds:
     //  * default: k_sel_bounds_gather -- block 0 of the gather computes the bounds and
-    //    publishes them in-launch (relies on block 0 being dispatched first) while the
-    //    other blocks' row loads are in flight;
-    //  * FICP_SEL_RB=1: k_sel_reduce_bounds -- the bounds spread over the reduce's
-    //    workgroups (each waits only for the totals of the workgroups dispatched before
-    //    it), the gather reads [b0, b1] (runs of 4 buckets) at its start.  Measured 2 %
-    //    slower at C3 (8,296-8,319 vs 8,456-8,476 it/s, tools/ab_bench.sh FICP_SEL_RB=1): the gather's
-    //    row loads take as long as the one-workgroup bounds, which they hid, and the
-    //    reduce grew by its exchange;
-    //  * FICP_SEL_SPLIT=1: k_sel_bounds + k_sel_gather, no in-launch hand-off at all.
-    // The first two raise ERR_SPIN instead of hanging should the dispatch order not hold.
+    //    publishes them in-launch (relies on block 0 being dispatched first, raising
+    //    ERR_SPIN instead of hanging should that order not hold) while the other blocks'
+    //    row loads are in flight;
+    //  * FICP_SEL_SPLIT=1: k_sel_bounds + k_sel_gather, no in-launch hand-off at all (the
+    //    fallback should a dispatcher not keep blockIdx order; ~1.4 % slower at C3).
     const char *sp = getenv("FICP_SEL_SPLIT");
     const bool split = sp && atoi(sp) != 0;
-    const char *rbe = getenv("FICP_SEL_RB");
-    const bool rb = !split && rbe && atoi(rbe) != 0;
-    if (rb) {
-        hipLaunchKernelGGL(k_sel_reduce_bounds, dim3(RBLK), dim3(1024), 0, s, w, hist_blocks(n), skip,
-                           hp, lam, lam_dev, gen, pub);
-        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs, 1);
+    hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip,
+                       hp, (long long *)nullptr);
+    if (split) {
+        hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip,
+                           hp.fixb);
+        hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs);
     } else {
-        hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip,
-                           hp, (long long *)nullptr);
-        if (split) {
-            hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip,
-                               hp.fixb);
-            hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, s, key, orig, r, n, w, skip, fs,
-                               0);
-        } else {
-            hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n,
-                               w, lam, lam_dev, skip, hp.fixb, fs, gen, pub);
-        }
+        hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n,
+                           w, lam, lam_dev, skip, hp.fixb, fs, gen, pub);
     }
     LoopCtl lc{};
     if (loop) lc = *loop;

@@ -20,6 +20,7 @@ There is no CPU fallback: without the library or a GPU the methods raise.
 from __future__ import annotations
 
 import os
+import threading
 import time
 
 import numpy as np
@@ -27,6 +28,11 @@ import numpy as np
 from . import _lib
 
 _PREFETCH = None  # worker threads of the constructor's target prefetch (see __init__)
+# Instances holding a prefetched (pooled) context that run() has not taken yet: each holds
+# one device context, so constructing many instances before running them would otherwise
+# create that many contexts.  Past the limit the constructor skips the prefetch.
+_PREFETCH_MAX = int(os.environ.get("FICP_PREFETCH_MAX", "4"))
+_PREFETCH_SLOTS = threading.BoundedSemaphore(max(_PREFETCH_MAX, 1))
 
 
 def _prefetch_pool():
@@ -59,6 +65,13 @@ def _release_done(fut):
         _lib.release_context(fut.result())
 
 
+def _writable_again(arr):
+    try:
+        arr.flags.writeable = True
+    except ValueError:  # a view of a read-only base: leave it
+        pass
+
+
 class FractionalICP:
     def __init__(
         self,
@@ -88,14 +101,24 @@ class FractionalICP:
         # upload to a pooled context (+ the grid's inputs) starts on a worker thread while
         # the source is copied: run() then finds the CHM layer on the device.
         # FICP_PREFETCH=0: no prefetch.
+        # While the prefetch is pending (until run() takes it, or close()), self.target is
+        # read-only: the device copy must stay the layer run() would read (ficp.py:123), so
+        # an in-place edit raises instead of running on a stale layer.  Assigning a new
+        # array to icp.target (or changing device / nn_mode / match dims) discards the
+        # prefetch, and run() uploads what it finds then.
         self._prefetch = None
         if (_plain_rows(source) and _plain_rows(target) and len(source) and len(target)
-                and os.environ.get("FICP_PREFETCH", "1") != "0"):
-            self.target = _lib.copy_array(target)
-            md = 3 if (source.shape[1] >= 3 and target.shape[1] >= 3) else 2
-            mode = {"auto": _lib.NN_AUTO, "brute": _lib.NN_BRUTE, "grid": _lib.NN_GRID}[nn_mode]
-            self._prefetch = (_prefetch_pool().submit(_prefetch_target, self.target, md, device, mode),
-                              self.target, md)
+                and os.environ.get("FICP_PREFETCH", "1") != "0" and _PREFETCH_SLOTS.acquire(blocking=False)):
+            try:
+                self.target = _lib.copy_array(target)
+                self.target.flags.writeable = False
+                md = 3 if (source.shape[1] >= 3 and target.shape[1] >= 3) else 2
+                mode = {"auto": _lib.NN_AUTO, "brute": _lib.NN_BRUTE, "grid": _lib.NN_GRID}[nn_mode]
+                self._prefetch = (_prefetch_pool().submit(_prefetch_target, self.target, md, device, mode),
+                                  self.target, md, device, mode)
+            except BaseException:
+                _PREFETCH_SLOTS.release()
+                raise
             self.source = _lib.copy_array(source)
         else:
             self.source = _lib.copy_array(source)
@@ -123,21 +146,31 @@ class FractionalICP:
 
     def _take_prefetch(self):
         """The pooled context the constructor uploaded self.target to (None: none, or the
-        attribute has been replaced since, or the match dims changed)."""
+        attribute has been replaced since, or the match dims, device or NN mode changed)."""
         pf, self._prefetch = getattr(self, "_prefetch", None), None
         if pf is None:
             return None
-        fut, tgt, md = pf
-        if tgt is not self.target or md != self.match_dims:
-            fut.add_done_callback(_release_done)
+        _PREFETCH_SLOTS.release()
+        fut, tgt, md, device, mode = pf
+        if tgt is not self.target or md != self.match_dims or device != self.device or mode != self.nn_mode:
+            self._discard(fut, tgt)
             return None
-        return fut.result()  # (raises what the upload raised: no GPU, bad layer)
+        try:
+            return fut.result()  # (raises what the upload raised: no GPU, bad layer)
+        finally:
+            _writable_again(tgt)  # the upload has read it
+
+    @staticmethod
+    def _discard(fut, tgt):
+        fut.add_done_callback(_release_done)
+        fut.add_done_callback(lambda _f: _writable_again(tgt))
 
     def close(self):
         """Releases the constructor's prefetched context, if run() has not used it."""
         pf, self._prefetch = getattr(self, "_prefetch", None), None
         if pf is not None:
-            pf[0].add_done_callback(_release_done)
+            _PREFETCH_SLOTS.release()
+            self._discard(pf[0], pf[1])
 
     def __del__(self):
         try:

@@ -39,9 +39,8 @@ def load_run(name):
 
 
 def allow_refl(run):
-    """The run fixture's allow_reflection kwarg (ficp.py:13); fixtures from before round 4
-    have none and ran with the default False."""
-    return bool(int(run.get("kwargs_allow_reflection", 0)))
+    """The run fixture's allow_reflection kwarg (ficp.py:13); every run fixture records it."""
+    return bool(int(run["kwargs_allow_reflection"]))
 
 
 RUN_FIXTURES = sorted(p.stem[4:] for p in GOLDEN.glob("run_*.npz") if p.stem != "run_real_stand10")

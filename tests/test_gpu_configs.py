@@ -144,4 +144,11 @@ def test_c5_8M_partitioned_vs_oracle_and_single(oracle):
     pinned = otr["gap"] > K_GAP_PIN_LARGE
     assert pinned.sum() >= 3  # measured: calls 0, 1, 3 (gaps 1e-11, 4e-12, 1e-12)
     np.testing.assert_array_equal(icp.last_stats["k"][pinned], otr["k"][pinned])
-    assert np.all(np.abs(icp.last_stats["k"] - otr["k"]) <= 2), (icp.last_stats["k"], otr["k"])
+    # every call whose k differs is a rounding-level tie of the oracle's own curve, and the
+    # trajectory rejoins the oracle's at the very next call (and ends on its k)
+    k_gpu = np.asarray(icp.last_stats["k"])
+    off = np.flatnonzero(k_gpu != otr["k"])
+    assert np.all(otr["gap"][off] < K_GAP_PIN_LARGE), (off, otr["gap"][off])
+    assert np.all(off + 1 < len(k_gpu)), off
+    np.testing.assert_array_equal(k_gpu[off + 1], otr["k"][off + 1])
+    assert k_gpu[-1] == otr["k"][-1]

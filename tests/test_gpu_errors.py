@@ -1,9 +1,8 @@
 """Sticky device error paths and the pooled host path.
 
 * ERR_SPIN: the test-only fault injection (ficp_set_fault) makes the in-launch hand-off
-  publish a wrong token (block 0 of k_sel_bounds_gather, or every workgroup of
-  k_sel_reduce_bounds with FICP_SEL_RB=1), so every waiting workgroup's bounded wait runs
-  out.  The run must end (no hang), append nothing out of bounds, and raise FicpError
+  publish a wrong token (block 0 of k_sel_bounds_gather), so every waiting workgroup's
+  bounded wait runs out.  The run must end (no hang), append nothing out of bounds, and raise FicpError
   naming the flag; the same context must run clean afterwards (the flag is per run).
 * The facade borrows pooled contexts: a second FractionalICP reuses the first one's
   context, and results do not depend on which pooled context ran them.
@@ -19,10 +18,8 @@ from coregistrationgame_amd.ficp import FractionalICP
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("rb", ["0", "1"])  # hand-off in k_sel_bounds_gather / k_sel_reduce_bounds
 @pytest.mark.parametrize("n", [3000, 120_000])  # below / above the half-step lookahead (64k rows)
-def test_err_spin_reaches_python(n, rb, oracle, monkeypatch):
-    monkeypatch.setenv("FICP_SEL_RB", rb)
+def test_err_spin_reaches_python(n, oracle):
     p = synth.make_plot(n, n, 0.8, seed=77, md=3)
     ctx = _lib.Context(0, _lib.NN_GRID)
     try:

@@ -90,3 +90,36 @@ def test_memcpy_d2d_copy_kernel_and_fallback():
     finally:
         for p in bufs:
             L.ficp_dev_free(ctx.h, C.c_void_p(p))
+
+
+def test_prefetched_target_guarded_until_run():
+    """while the prefetch is pending the constructor's target is read-only (an
+    in-place edit raises instead of running on a stale device copy); run() makes it writable
+    again; a changed nn_mode or device discards the prefetch."""
+    from coregistrationgame_amd import FractionalICP
+    p = _plot(n=120_000, seed=6)
+    icp = FractionalICP(p.source, p.target)
+    assert icp._prefetch is not None
+    with pytest.raises(ValueError):
+        icp.target[0, 0] += 1.0
+    out = icp.run()
+    assert icp.target.flags.writeable
+    icp2 = FractionalICP(p.source, p.target)
+    from coregistrationgame_amd import _lib
+    icp2.nn_mode = _lib.NN_BRUTE                            # a different NN path: re-upload
+    assert icp2._take_prefetch() is None
+    assert icp2.target.flags.writeable or icp2._prefetch is None
+    np.testing.assert_array_equal(out, FractionalICP(p.source, p.target).run())
+
+
+def test_outstanding_prefetches_are_bounded():
+    from coregistrationgame_amd import FractionalICP, ficp as F
+    p = _plot(n=120_000, seed=7)
+    held = [FractionalICP(p.source, p.target) for _ in range(F._PREFETCH_MAX + 3)]
+    assert sum(h._prefetch is not None for h in held) == F._PREFETCH_MAX
+    outs = [h.run() for h in held]                          # prefetched and plain runs agree
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
+    again = FractionalICP(p.source, p.target)               # every slot came back
+    assert again._prefetch is not None
+    again.close()

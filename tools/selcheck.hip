@@ -165,7 +165,7 @@ int main(int argc, char **argv) {
                                (const double *)nullptr, (const int *)nullptr, hist_pack(n).fixb);
             CK(hipEventRecord(ev[2], 0));
             hipLaunchKernelGGL(k_sel_gather, dim3(gb), dim3(GT), 0, 0, dkey, dorig, dr, n, w,
-                               (const int *)nullptr, FitSrc{}, 0);
+                               (const int *)nullptr, FitSrc{});
         }
         CK(hipEventRecord(ev[3], 0));
         LoopCtl lc{};

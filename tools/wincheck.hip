@@ -17,11 +17,8 @@
 //     full path's, the fused fit's T equal to the CPU fit of the selected rows; or
 //   * fall back (kFlagRetry): the state unchanged but win_fail / nn_reuse, and the full
 //     selection run after it bit-identical (whole IterState) to the full path run alone.
-// Every case runs twice: k_sel_win (its own pass, one launch) and the fused form (the NN
-// kernel's pass, k_pass_only here, then k_sel_win_tail), each against the same bars.
 // Prints one line per case; exit status 1 on any mismatch.
 #include "../coregistrationgame_amd/csrc/k_select.hip"
-#include "../coregistrationgame_amd/csrc/win_pass.h"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -42,12 +39,6 @@ using namespace ficp;
             exit(2);                                                                       \
         }                                                                                  \
     } while (0)
-
-// the fused pass alone (k_grid_nn.hip runs it inside k_nn_grid_q on the rows it wrote)
-__global__ __launch_bounds__(256) void k_pass_only(NNArgs a) {
-    const int64_t tile = blockIdx.x;
-    nn_win_pass<kWinNNRows / 256>(a, tile * kWinNNRows, tile);
-}
 
 __global__ void k_keys_of_r(const double *r, int64_t n, unsigned long long *key) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -225,13 +216,6 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e1));
 
     const int wstart = win_start_log(n), whmax = win_hmax_log(n);
-    const bool nn_form = select_win_nn_blocks(n) > 0;  // (layers the fused pass can take)
-    // win_ok (ficp_internal.h) on the host: the state test the NN kernel makes
-    auto win_ok_host = [&](const IterState &s, int64_t nn) {
-        const int f = s.wfloor > 0 ? s.wfloor : win_start_log(nn);
-        return s.phase == PH_LOOP && !s.done && s.it >= 1 && s.k > 0 && win_lh(s.tmove, f) <= win_hmax_log(nn) &&
-               2.0 * s.lam_cur + 1.0 >= 1.0;
-    };
     // floors: lh = floor + 1 (tmove 0); the last one is past the limit (lh > hmax: the
     // launch must refuse at once)
     const int floors[5] = {std::max(kWinHMinLog, wstart - 3), wstart, wstart + 2, whmax - 1, whmax};
@@ -282,32 +266,14 @@ int main(int argc, char **argv) {
             CK(launch_select(nullptr, dorig, dr, n, 0.0, &st->lam_cur, drange, 0, tmp, st, &st->done, &lc,
                              dflag, 0, &fs, 0));
             CK(hipMemcpy(&full, st, sizeof full, hipMemcpyDeviceToHost));
-          for (int form = 0; form < (nn_form ? 2 : 1); ++form) {
-            // (2) the window path from s0: k_sel_win, or the fused pass + k_sel_win_tail
+          {
+            // (2) the window path from s0 (k_sel_win)
             IterState win{};
             int flag = -1;
             CK(hipMemcpy(st, &s0, sizeof s0, hipMemcpyHostToDevice));
             CK(hipMemcpy(dflag, &flag, 4, hipMemcpyHostToDevice));
             CK(hipEventRecord(e0, 0));
-            if (form == 0) {
-                CK(launch_select_win(dr, dorig, n, drange, 0, tmp, st, lc, dflag, 0, fs, 0));
-            } else {
-                // the NN kernel runs the pass only when the state allows the window path
-                if (win_ok_host(s0, n)) {
-                    NNArgs na{};
-                    na.n = n;
-                    na.r = dr;
-                    na.sx = dxs;
-                    na.sy = dys;
-                    na.cx = dxt;
-                    na.cy = dyt;
-                    const NNWin nw{st, dorig, select_win_out(tmp, n), 0.0, 0.0};
-                    CK(hipMemcpy(select_win_desc(tmp), &nw, sizeof nw, hipMemcpyHostToDevice));
-                    na.win = select_win_desc(tmp);
-                    hipLaunchKernelGGL(k_pass_only, dim3((unsigned)select_win_nn_blocks(n)), dim3(256), 0, 0, na);
-                }
-                CK(launch_select_win_tail(n, tmp, st, lc, dflag, 0, fs, 0));
-            }
+            CK(launch_select_win(dr, dorig, n, drange, 0, tmp, st, lc, dflag, 0, fs, 0));
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             CK(hipMemcpy(&win, st, sizeof win, hipMemcpyDeviceToHost));
@@ -357,7 +323,7 @@ int main(int argc, char **argv) {
             if (!ok) ++bad;
             printf("n=%lld mode=%d lam=%g floor=2^%d window=2^%d place=%-11s rows_in_window=%-7lld "
                    "form=%s path=%-8s k=%lld %s%s\n",
-                   (long long)n, mode, lam, fl, lh, pl.name, wrows, form ? "nn+tail " : "sel_win ", path,
+                   (long long)n, mode, lam, fl, lh, pl.name, wrows, "sel_win ", path,
                    (long long)(flag == kFlagRetry ? full.k : win.k), ok ? "ok" : "MISMATCH: ", ok ? "" : why);
           }
         }

@@ -897,15 +897,42 @@ int ficp_path_stats(ficp_ctx *c, int64_t out[4]) {
     return FICP_OK;
 }
 
+// wall-clock length of the union of intervals (ms): records on concurrent streams (the batch
+// sub-batches) overlap, so their summed durations overstate the time the kernels held the GPU
+static double union_ms(std::vector<std::pair<double, double>> iv) {
+    std::sort(iv.begin(), iv.end());
+    double tot = 0.0, a = 0.0, b = 0.0;
+    bool open = false;
+    for (const auto &x : iv) {
+        if (!open || x.first > b) {
+            if (open) tot += b - a;
+            a = x.first;
+            b = x.second;
+            open = true;
+        } else {
+            b = std::max(b, x.second);
+        }
+    }
+    return open ? tot + (b - a) : 0.0;
+}
+
 int ficp_profile_report(ficp_ctx *c, char *buf, int64_t buflen) {
     CHK(check_ctx(c));
     CHK(sync(c));
+    // every record's interval as offsets from the first record's start event (signed)
+    std::map<std::string, std::vector<std::pair<double, double>>> ivs;
+    std::vector<std::pair<double, double>> all;
+    const hipEvent_t ref = c->recs.empty() ? nullptr : c->recs.front().a;
     for (auto &r : c->recs) {
-        float ms = 0.f;
+        float ms = 0.f, oa = 0.f, ob = 0.f;
         (void)hipEventElapsedTime(&ms, r.a, r.b);
+        (void)hipEventElapsedTime(&oa, ref, r.a);
+        (void)hipEventElapsedTime(&ob, ref, r.b);
         auto &acc = c->prof_acc[r.name];
         acc.first += 1;
         acc.second += ms;
+        ivs[r.name].push_back({(double)oa, (double)ob});
+        all.push_back({(double)oa, (double)ob});
         c->ev_pool.push_back(r.a);
         c->ev_pool.push_back(r.b);
     }
@@ -913,11 +940,19 @@ int ficp_profile_report(ficp_ctx *c, char *buf, int64_t buflen) {
     std::string s = "{";
     bool first = true;
     for (auto &kv : c->prof_acc) {
-        char item[256];
-        snprintf(item, sizeof item, "%s\"%s\": {\"count\": %lld, \"ms\": %.6f}", first ? "" : ", ",
-                 kv.first.c_str(), (long long)kv.second.first, kv.second.second);
+        char item[320];
+        const auto it = ivs.find(kv.first);
+        const double wall = it == ivs.end() ? 0.0 : union_ms(it->second);
+        snprintf(item, sizeof item, "%s\"%s\": {\"count\": %lld, \"ms\": %.6f, \"wall_ms\": %.6f}",
+                 first ? "" : ", ", kv.first.c_str(), (long long)kv.second.first, kv.second.second, wall);
         s += item;
         first = false;
+    }
+    if (!all.empty()) {  // every recorded interval together
+        char item[160];
+        snprintf(item, sizeof item, "%s\"_all\": {\"count\": %lld, \"wall_ms\": %.6f}", first ? "" : ", ",
+                 (long long)all.size(), union_ms(all));
+        s += item;
     }
     s += "}";
     c->prof_acc.clear();

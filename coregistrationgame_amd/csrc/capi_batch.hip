@@ -29,6 +29,7 @@ struct BatchBufs {
     DevBuf cell_of, counts, fill, cell_start, pts, scan_tmp, bs_tmp;
     DevBuf key, gap, r, ccx, ccy, bp, dz2, wkey, skey, wrow, srow, wr, sr;
     DevBuf sx, sy, sz, tx, ty, tz, stage;  // staging of the host entry point
+    DevBuf wx, wy, wz, worig;              // the trees in the batch work order (k_bsort mode 3)
     DevBuf fpart, fctr;                    // batch fit: per-chunk sums, per-plot arrivals
     DevBuf arrive;                         // fused step: per sub-batch arrival/live counter
     unsigned fctr_init_gen = 0;            // fctr allocation whose counters are zeroed
@@ -50,7 +51,8 @@ void batch_release(BatchBufs *b) {
                       &b->r,        &b->ccx,     &b->ccy,      &b->wkey,  &b->skey,  &b->wrow,
                       &b->srow,     &b->wr,      &b->sr,       &b->sx,    &b->sy,    &b->sz,
                       &b->tx,       &b->ty,      &b->tz,       &b->stage, &b->bp,
-                      &b->dz2,      &b->bs_tmp,  &b->fpart,   &b->fctr, &b->arrive};
+                      &b->dz2,      &b->bs_tmp,  &b->fpart,   &b->fctr, &b->arrive,
+                      &b->wx,       &b->wy,      &b->wz,      &b->worig};
     for (DevBuf *d : bufs) d->release();
     b->up.release();
     b->rep.release();
@@ -79,10 +81,21 @@ BatchBufs *batch_of(ficp_ctx *c) {
     return c->batch;
 }
 
-// per-plot CHM grids in one set of arrays (cells of plot p: cell_base_p .. +gx*gy-1)
+// The trees of a batch job: their columns, count and (device) plot of every tree.
+struct BatchTrees {
+    const double *x, *y, *z;
+    int64_t n;
+    const int32_t *plot;
+};
+
+// per-plot CHM grids in one set of arrays (cells of plot p: cell_base_p .. +gx*gy-1) and,
+// with trees.n > 0, the batch work order of the trees in the same four bucket-sort launches
+// (k_bsort.hip modes 2 and 3: plot, then 8x8-cell supertile of the plot's grid, then cell,
+// then caller row) into b.wx / wy / wz / worig.  Returns in *work whether it was built.
 int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *to_h,
                       const double *tx, const double *ty, const double *tz, int64_t m, int md,
-                      std::vector<PlotGrid> &grids) {
+                      std::vector<PlotGrid> &grids, const BatchTrees &trees, bool *work) {
+    *work = false;
     CHK(b.bb.ensure((size_t)nplots * 4 * 8));
     HIPCHK(launch_batch_bbox(tx, ty, b.to.as<int64_t>(), nplots, b.bb.as<double>(), c->stream));
     // the bboxes through the report kernel into coherent pinned memory and a polled flag
@@ -99,17 +112,19 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
     }
     const double *bb = b.rep.as<const double>();
     grids.assign(nplots, PlotGrid{});
-    int64_t ncells = 0;
+    int64_t ncells = 0, nwkeys = 0;
     for (int32_t p = 0; p < nplots; ++p) {
         PlotGrid &g = grids[p];
         const int64_t mp = to_h[p + 1] - to_h[p];
         g.m = (int)mp;
         g.cell_base = ncells;
+        g.wbase = nwkeys;
         if (mp == 0) {  // no CHM stems: the plot never runs (ficp.py:66-68, 125-126)
             g.x0 = g.y0 = g.px = g.py = 0.0;
             g.h = g.inv_h = 1.0;
             g.gx = g.gy = 1;
             ncells += 1;
+            nwkeys += 64;
             continue;
         }
         const double x0 = bb[4 * p], x1 = bb[4 * p + 1], y0 = bb[4 * p + 2], y1 = bb[4 * p + 3];
@@ -128,6 +143,7 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
         g.px = x0 + 0.5 * (x1 - x0);  // fit pivot: the plot's CHM bbox centre
         g.py = y0 + 0.5 * (y1 - y0);
         ncells += gx * gy;
+        nwkeys += ((gx + 7) / 8) * ((gy + 7) / 8) * 64;  // (k_bsort.hip st_key's range)
     }
     if (ncells > 0x7ffffffe) return fail(FICP_EINVAL, "batch grid too large");
     CHK(b.grids.ensure((size_t)nplots * sizeof(PlotGrid)));
@@ -137,10 +153,30 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
     CHK(b.cell_start.ensure((ncells + 1) * 4));
     CHK(b.pts.ensure(m * sizeof(TPt)));
     HIPCHK(launch_fill_plot_ids(b.to.as<int64_t>(), nplots, b.tplot.as<int32_t>(), c->stream));
+    // the work order's job (mode 3), when the bucket sort can plan it
+    const bool want_work = trees.n > 0 && bsort_supported(trees.n, nwkeys);
+    BSortGeom wg{};
+    BSortOut wo{};
+    if (want_work) {
+        CHK(b.wx.ensure(trees.n * 8));
+        CHK(b.wy.ensure(trees.n * 8));
+        if (md == 3) CHK(b.wz.ensure(trees.n * 8));
+        CHK(b.worig.ensure(trees.n * 4));
+        wg.mode = 3;
+        wg.plot = trees.plot;
+        wg.grids = b.grids.as<PlotGrid>();
+        wo.wx = b.wx.as<double>();
+        wo.wy = b.wy.as<double>();
+        wo.wz = md == 3 ? b.wz.as<double>() : nullptr;
+        wo.worig = b.worig.as<uint32_t>();
+    }
+    const int64_t wtmp = want_work ? bsort_tmp_bytes(trees.n, nwkeys) : 0;
     if (bsort_supported(m, ncells) && !getenv("FICP_GRID_ATOMIC")) {
         // the two-level bucket sort of the single-plot grid (k_bsort.hip) keyed by the
-        // global cell id of each stem's plot grid: 1.3 -> ~0.25 ms per 1024-plot batch
-        CHK(b.bs_tmp.ensure(bsort_tmp_bytes(m, ncells)));
+        // global cell id of each stem's plot grid: 1.3 -> ~0.25 ms per 1024-plot batch;
+        // the trees' work order rides in the same four launches (as the single plot's)
+        const int64_t gtmp = bsort_tmp_bytes(m, ncells);
+        CHK(b.bs_tmp.ensure(gtmp + wtmp));
         BSortGeom bg{};
         bg.mode = 2;
         bg.plot = b.tplot.as<int32_t>();
@@ -148,8 +184,19 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
         BSortOut bo{};
         bo.pts = b.pts.as<TPt>();
         bo.cell_start = b.cell_start.as<int32_t>();
-        HIPCHK(launch_bsort(tx, ty, md == 3 ? tz : nullptr, m, bg, ncells, bo, b.bs_tmp.p, c->stream));
+        const BSJob gj = bsort_job(tx, ty, md == 3 ? tz : nullptr, m, bg, ncells, bo, b.bs_tmp.p);
+        const BSJob wj = want_work ? bsort_job(trees.x, trees.y, md == 3 ? trees.z : nullptr, trees.n, wg,
+                                               nwkeys, wo, b.bs_tmp.as<char>() + gtmp)
+                                   : BSJob{};
+        HIPCHK(launch_bsort2(gj, wj, c->stream));
+        *work = want_work;
         return FICP_OK;
+    }
+    if (want_work) {
+        CHK(b.bs_tmp.ensure(wtmp));
+        HIPCHK(launch_bsort(trees.x, trees.y, md == 3 ? trees.z : nullptr, trees.n, wg, nwkeys, wo,
+                            b.bs_tmp.p, c->stream));
+        *work = true;
     }
     // counting sort with global atomics (grids the bucket sort cannot plan)
     CHK(b.cell_of.ensure(m * 4));
@@ -198,13 +245,25 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
     }
     HIPCHK(launch_batch_init(b.so.as<int64_t>(), b.to.as<int64_t>(), nplots, nstages,
                              b.st.as<PlotState>(), c->stream));
+    bool work = false;  // the trees run in the batch work order (b.wx, wy, wz, worig)
     if (n > 0 && m > 0 && nstages > 0) {
         std::vector<PlotGrid> grids;
-        {
-            ProfScope ps(c, P_GRID, "batch_grid_build");
-            CHK(build_batch_grids(c, b, nplots, to_h, tx, ty, tz, m, md, grids));
-        }
         CHK(b.plot_of.ensure(n * 4));
+        HIPCHK(launch_fill_plot_ids(b.so.as<int64_t>(), nplots, b.plot_of.as<int32_t>(),
+                                    c->stream));
+        {
+            // FICP_BATCH_WORK=0: the trees stay in caller order
+            const char *we = getenv("FICP_BATCH_WORK");
+            const bool want = !(we && atoi(we) == 0);
+            const BatchTrees trees{sx, sy, md == 3 ? sz : nullptr, want ? n : 0, b.plot_of.as<int32_t>()};
+            ProfScope ps(c, P_GRID, "batch_grid_build");
+            CHK(build_batch_grids(c, b, nplots, to_h, tx, ty, tz, m, md, grids, trees, &work));
+        }
+        // the columns the batch iterations read and move: the work order's, or the caller's
+        double *qx = work ? b.wx.as<double>() : sx;
+        double *qy = work ? b.wy.as<double>() : sy;
+        const double *qz = (md == 3) ? (work ? b.wz.as<double>() : sz) : nullptr;
+        const uint32_t *worig = work ? b.worig.as<uint32_t>() : nullptr;
         CHK(b.key.ensure(n * 8));
         CHK(b.gap.ensure(n * sizeof(gap_t)));
         CHK(b.dz2.ensure(n * 8));
@@ -220,15 +279,13 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         CHK(b.sr.ensure(n * 8));
         const BatchSelScratch ws{b.wkey.as<unsigned long long>(), b.skey.as<unsigned long long>(),
                                  b.wrow.as<uint32_t>(), b.srow.as<uint32_t>(), b.wr.as<double>(),
-                                 b.sr.as<double>()};
+                                 b.sr.as<double>(), worig};
         int64_t max_rows = 0;
         for (int32_t p = 0; p < nplots; ++p) max_rows = std::max(max_rows, so_h[p + 1] - so_h[p]);
-        HIPCHK(launch_fill_plot_ids(b.so.as<int64_t>(), nplots, b.plot_of.as<int32_t>(),
-                                    c->stream));
         NNArgs a{};
-        a.sx = sx;
-        a.sy = sy;
-        a.sz = md == 3 ? sz : nullptr;
+        a.sx = qx;
+        a.sy = qy;
+        a.sz = qz;
         a.n = n;
         a.idx = nullptr;  // the batch returns XY and per-plot records, not the NN index
         a.r = b.r.as<double>();
@@ -324,9 +381,10 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // the separate k_batch_fit and k_batch_update launches.
         const char *bf = getenv("FICP_BATCH_FUSE");
         const bool bfuse = !(bf && atoi(bf) == 0);
-        BatchStepArgs step{sx, sy, b.ccx.as<double>(), b.ccy.as<double>(), b.grids.as<PlotGrid>(),
+        BatchStepArgs step{qx, qy, b.ccx.as<double>(), b.ccy.as<double>(), b.grids.as<PlotGrid>(),
                            allow_refl, nstages, max_iter, threshold};
         if (trace) step.max_trace = c->btrace_max;
+        step.worig = worig;
         auto enqueue = [&](Sub &u, int64_t bit) -> int {
             int *flag = &u.ring[bit % kBatchRing];
             __atomic_store_n(flag, -1, __ATOMIC_RELEASE);
@@ -338,15 +396,15 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             const PlotGrid *gu = b.grids.as<PlotGrid>() + u.p0;
             if (!bfuse) {
                 ProfScope ps(c, prof ? P_FIT : 0, "batch_fit", u.s);
-                HIPCHK(launch_batch_fit(sx, sy, b.ccx.as<double>(), b.ccy.as<double>(),
+                HIPCHK(launch_batch_fit(qx, qy, b.ccx.as<double>(), b.ccy.as<double>(),
                                         b.key.as<unsigned long long>(), sou, gu, u.np, max_rows,
                                         allow_refl, su, b.fpart.as<double>() + (size_t)u.p0 * fch,
-                                        b.fctr.as<unsigned>() + u.p0, u.s));
+                                        b.fctr.as<unsigned>() + u.p0, u.s, worig));
             }
             NNArgs au = a;  // this sub-batch's trees: the per-tree arrays from its first row
             au.warm_c = bit > 0 ? 1 : 0;
-            au.sx = sx + u.r0;
-            au.sy = sy + u.r0;
+            au.sx = qx + u.r0;
+            au.sy = qy + u.r0;
             au.sz = a.sz ? a.sz + u.r0 : nullptr;
             au.n = u.nr;
             au.r = a.r + u.r0;
@@ -399,6 +457,10 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         for (int q = 0; q < nsub; ++q)
             if (!subs[q].finished) return fail(FICP_EHIP, "batch did not converge within its bound");
     }  // JoinGuard: the sub-streams join c->stream here
+    // the moved XY back into the caller's rows (k_scatter_xy: sx[worig[w]] = wx[w])
+    if (work)
+        HIPCHK(launch_scatter_xy(b.worig.as<uint32_t>(), b.wx.as<double>(), b.wy.as<double>(), n, sx, sy,
+                                 c->stream));
     // one report kernel copies the plot states into coherent pinned memory and raises a
     // flag the host polls (a pageable D2H copy + stream sync left ~40 us of idle device)
     const size_t sbytes = (size_t)nplots * sizeof(PlotState);

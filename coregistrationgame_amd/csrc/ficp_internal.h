@@ -274,19 +274,17 @@ struct GridView {
 // query instead of 8 + 8; C3 it/s unchanged against fp64 within noise, all -m gpu green).
 typedef float gap_t;
 
-// Per-launch NN arguments.
-// The window selection's per-workgroup outputs (k_select.hip SelWS's window part): each
-// pass workgroup's record (kWinRec words), its window rows (at most kWinSlot: key, r, caller
-// index, work row) and the coarse buckets (agent-scope atomics, read and zeroed by the tail).
-constexpr int kWinSlot = 64, kWinRec = 16;
-// copies of the coarse buckets, one per XCD (blockIdx % 8): memory-side atomics on one word
-// serialise (~88 per us), and 977 NN workgroups on 256 words took ~11 us
+// The window selection's cross-workgroup words (k_select.hip SelWS's window part: coarse
+// buckets, accumulators, append counters) come in copies, one per XCD (blockIdx % 8):
+// memory-side atomics on one word serialise (~88 per us), and 977 NN workgroups on 256
+// words took ~11 us
 #ifndef FICP_WIN_COPIES
 #define FICP_WIN_COPIES 8
 #endif
 constexpr int kWinCopies = FICP_WIN_COPIES;
 struct IterState;
 
+// Per-launch NN arguments.
 struct NNArgs {
     double *sx;                 // source x (updated in place when T != nullptr)
     double *sy;
@@ -703,8 +701,10 @@ struct BSortGeom {
     double x0, y0, inv_h;
     int gx, gy;
     int mode;                // 2: many plots (C4): key = cell_base + cell of the point's plot
-    const int32_t *plot;     // mode 2: plot of each point
-    const PlotGrid *grids;   // mode 2: per-plot geometry
+                             // 3: many plots' trees: key = wbase + the supertile-order key of
+                             //    the point in its plot's grid (the batch work order)
+    const int32_t *plot;     // modes 2, 3: plot of each point
+    const PlotGrid *grids;   // modes 2, 3: per-plot geometry
 };
 struct BSortPlan {
     int fs;         // fine bits (key & ((1 << fs) - 1))
@@ -909,6 +909,8 @@ struct PlotGrid {
     int gx, gy;
     int m;                                   // CHM stems of the plot (0: plot is skipped)
     int pad;
+    long long wbase;                         // first work-order key of the plot's trees
+                                             // (k_bsort.hip mode 3: 8x8-supertile order)
 };
 
 
@@ -953,7 +955,8 @@ int batch_fit_chunks(int64_t max_rows);
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
                             const double *cy, const unsigned long long *key, const int64_t *so,
                             const PlotGrid *grids, int nplots, int64_t max_rows, int allow_refl,
-                            PlotState *st, double *part, unsigned *ctr, hipStream_t s);
+                            PlotState *st, double *part, unsigned *ctr, hipStream_t s,
+                            const uint32_t *worig = nullptr);
 hipError_t launch_batch_fit_ctr_zero(unsigned *ctr, int n, hipStream_t s);
 // Per-plot FRMSD-optimal fraction (ficp.py:73-86), one workgroup per live plot: bucket
 // histogram of the plot's keys, bounds, exact sort of the candidate window only; sets
@@ -963,6 +966,9 @@ struct BatchSelScratch {
     unsigned long long *wkey, *skey;
     uint32_t *wrow, *srow;
     double *wr, *sr;
+    // the caller's row of each work row (the batch work order, k_bsort.hip mode 3; nullable:
+    // the rows are in caller order): the selection's tie-break at equal keys
+    const uint32_t *worig;
 };
 // the loop step and the next body's rigid fit inside the selection (nullable: the separate
 // k_batch_fit and k_batch_update launches)
@@ -978,6 +984,7 @@ struct BatchStepArgs {
     int *flag = nullptr;
     long long *trace = nullptr;  // per-call k trace rows of this launch's plots (nullable)
     int max_trace = 0;
+    const uint32_t *worig = nullptr;  // the fit's tie-break at the threshold key (as above)
 };
 hipError_t launch_batch_live(int nplots, const PlotState *st, int *flag, hipStream_t s);
 hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,

@@ -403,6 +403,7 @@ struct BatchStep {
     int nplots;
     long long *trace;            // per-call k trace, max_trace per plot of this launch (nullable)
     int max_trace;
+    const uint32_t *worig;       // caller row of each work row (nullable: caller order)
 };
 
 // thread 0 of plot p's workgroup, its state final for this call: one agent-scope atomic
@@ -474,7 +475,9 @@ __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, do
 #pragma unroll
         for (int u = 0; u < FU; ++u) {
             const int64_t i = i0 + (int64_t)u * NT;
-            if (i < e && (kv[u] < tkey || (kv[u] == tkey && i <= trow))) fit_add(c, xs[u], ys[u], xt[u], yt[u], g.px, g.py);
+            // (the tie at the threshold key: the caller's row, loaded only then)
+            if (i < e && (kv[u] < tkey || (kv[u] == tkey && (bs.worig ? (long long)bs.worig[i] : i) <= trow)))
+                fit_add(c, xs[u], ys[u], xt[u], yt[u], g.px, g.py);
         }
     }
 #pragma unroll
@@ -777,7 +780,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
         } else if (bk <= bmax) {
             const int64_t slot = (int64_t)s_cnt[bk] - K0 + atomicAdd(&fill[bk], 1u);
             wk[slot] = kk;
-            wrw[slot] = (uint32_t)i;
+            wrw[slot] = ws.worig ? ws.worig[i] : (uint32_t)i;  // (ties: the caller's row)
             wr[slot] = rv;
         }
     })
@@ -878,7 +881,7 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
                                                   const unsigned long long *key,
                                                   const int64_t *so, const PlotGrid *grids,
                                                   int allow_refl, PlotState *st, double *part,
-                                                  unsigned *ctr, int gmax) {
+                                                  unsigned *ctr, int gmax, const uint32_t *worig) {
     __shared__ double s[8 * (BB / 64)];
     __shared__ int s_last;
     const int p = blockIdx.x / gmax, g = blockIdx.x % gmax;
@@ -915,7 +918,7 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
 #pragma unroll
         for (int u = 0; u < FU; ++u) {
             const int64_t i = i0 + (int64_t)u * BB;
-            if (i < e && (kv[u] < tk || (kv[u] == tk && i <= t))) {
+            if (i < e && (kv[u] < tk || (kv[u] == tk && (worig ? (int64_t)worig[i] : i) <= t))) {
                 const double a0 = xs[u] - px, a1 = ys[u] - py;
                 const double b0 = xt[u] - px, b1 = yt[u] - py;
                 c[0] = c[0] + a0;
@@ -1075,11 +1078,12 @@ int batch_fit_chunks(int64_t max_rows) {
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
                             const double *cy, const unsigned long long *key, const int64_t *so,
                             const PlotGrid *grids, int nplots, int64_t max_rows, int allow_refl,
-                            PlotState *st, double *part, unsigned *ctr, hipStream_t s) {
+                            PlotState *st, double *part, unsigned *ctr, hipStream_t s,
+                            const uint32_t *worig) {
     if (nplots <= 0) return hipSuccess;
     const int gmax = batch_fit_chunks(max_rows);
     hipLaunchKernelGGL(k_batch_fit, dim3((unsigned)nplots * (unsigned)gmax), dim3(BB), 0, s, sx, sy,
-                       cx, cy, key, so, grids, allow_refl, st, part, ctr, gmax);
+                       cx, cy, key, so, grids, allow_refl, st, part, ctr, gmax, worig);
     return hipGetLastError();
 }
 
@@ -1122,6 +1126,7 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
         bs.nplots = nplots;
         bs.trace = step->trace;
         bs.max_trace = step->max_trace;
+        bs.worig = step->worig;
     }
     // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
     // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers)

@@ -44,20 +44,25 @@ __device__ __forceinline__ int bs_coord(double v, double v0, double inv_h, int g
 // key of a point: mode 0 = cell id cy * gx + cx (the grid layout); mode 1 = 8x8-supertile
 // order (supertile row-major, then the cell inside it row-major); mode 2 = the global cell
 // id of the batch grids (the point's plot's cell_base + its cell in that plot's grid, as
-// k_batch_grid_count)
+// k_batch_grid_count); mode 3 = the batch work order (the point's plot's wbase + its mode-1
+// key in that plot's grid: plot-major, so every plot keeps its contiguous row range)
+__device__ __forceinline__ uint32_t st_key(int cx, int cy, int gx) {
+    const uint32_t nstx = (uint32_t)(gx + 7) >> 3;
+    const uint32_t st = ((uint32_t)cy >> 3) * nstx + ((uint32_t)cx >> 3);
+    return (st << 6) | ((uint32_t)(cy & 7) << 3) | (uint32_t)(cx & 7);
+}
 __device__ __forceinline__ uint32_t bs_key(double x, double y, const BSortGeom &g, int64_t i) {
-    if (g.mode == 2) {
+    if (g.mode >= 2) {
         const PlotGrid &pg = g.grids[g.plot[i]];
         const int cx = bs_coord(x, pg.x0, pg.inv_h, pg.gx);
         const int cy = bs_coord(y, pg.y0, pg.inv_h, pg.gy);
-        return (uint32_t)(pg.cell_base + (long long)cy * pg.gx + cx);
+        if (g.mode == 2) return (uint32_t)(pg.cell_base + (long long)cy * pg.gx + cx);
+        return (uint32_t)(pg.wbase + (long long)st_key(cx, cy, pg.gx));
     }
     const int cx = bs_coord(x, g.x0, g.inv_h, g.gx);
     const int cy = bs_coord(y, g.y0, g.inv_h, g.gy);
     if (g.mode == 0) return (uint32_t)cy * (uint32_t)g.gx + (uint32_t)cx;
-    const uint32_t nstx = (uint32_t)(g.gx + 7) >> 3;
-    const uint32_t st = ((uint32_t)cy >> 3) * nstx + ((uint32_t)cx >> 3);
-    return (st << 6) | ((uint32_t)(cy & 7) << 3) | (uint32_t)(cx & 7);
+    return st_key(cx, cy, g.gx);
 }
 
 // Every kernel runs one or two sort jobs side by side (the grid build and the work

@@ -100,10 +100,8 @@ constexpr int NS_LOG = 12;
 constexpr int MAXLEV = 4;
 // window path (k_sel_win): rows a workgroup may hand over, coarse buckets per side of the
 // window (4 per octave of distance), record words per workgroup, arrival counter stride
-constexpr int WSLOT = kWinSlot;
 constexpr int NCS = fb::kWinNCS;
 constexpr int NCB = 2 * NCS;
-constexpr int WREC = kWinRec;
 constexpr int WCTR = 64;
 constexpr int SMALL_C = 160;  // final_small: above it the binned sort ranks faster (390: 5.8 vs 3.4 us)
 #ifndef FICP_GT
@@ -164,13 +162,15 @@ struct SelWS {
     uint32_t *pa, *pb;  // candidate row (work position): the fused fit reads its pair
     double *fpre;    // [CAP][4] fused fit: the pair of pack slots < CAP (gather)
     // the window path (k_sel_win):
-    u64 *wrec;       // [gather blocks][WREC] each workgroup's record (sc1 stores)
-    u64 *wsk;        // [gather blocks][WSLOT] its window rows: key, r, caller index, work row
-    double *wsr;
-    uint32_t *wso, *wsp;
-    unsigned *gcc;   // [NCB] coarse bucket counts (agent-scope atomics; the last workgroup
-    u64 *gcf;        //   reads and zeroes them with exchanges) and fixed-point sums of r
+    unsigned *gcc;   // [copies][NCB] coarse bucket counts (agent-scope atomics; the last
+    u64 *gcf;        //   workgroup reads and zeroes them with exchanges) and fixed-point sums
     unsigned *wctr;  // arrival counters: top + 8 groups, WCTR words apart (atomics only)
+    u64 *wacc;       // [copies][WACC] the workgroups' totals (atomics; the tail zeroes them)
+    unsigned *wcnt;  // [copies][WCNT_S] window-row append counters (atomics, zeroed likewise)
+    u64 *wk;         // [copies][CAP] the window rows appended: key, r, caller index and
+    double *wr;      //   the fit pair (xs, ys, cx, cy)
+    uint32_t *wo;
+    double *wp;
 };
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
@@ -230,6 +230,12 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.gcc = (unsigned *)take(kWinCopies * NCB * 4);
     x.gcf = (u64 *)take(kWinCopies * NCB * 8);
     x.wctr = (unsigned *)take(9 * WCTR * 4);
+    x.wacc = (u64 *)take(kWinCopies * 32 * 8);
+    x.wcnt = (unsigned *)take(kWinCopies * 16 * 4);
+    x.wk = (u64 *)take(kWinCopies * CAP * 8);
+    x.wr = (double *)take(kWinCopies * CAP * 8);
+    x.wo = (uint32_t *)take(kWinCopies * CAP * 4);
+    x.wp = (double *)take(kWinCopies * CAP * 32);
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
     x.fparts = (double *)take((int64_t)gather_blocks(n) * 64);
     x.ka = (u64 *)take(nn * 8);
@@ -241,12 +247,6 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.pa = (uint32_t *)take(nn * 4);
     x.pb = (uint32_t *)take(nn * 4);
     x.fpre = (double *)take(CAP * 32);
-    const int64_t gbw = gather_blocks(n);  // k_sel_win's workgroups
-    x.wrec = (u64 *)take(gbw * WREC * 8);
-    x.wsk = (u64 *)take(gbw * WSLOT * 8);
-    x.wsr = (double *)take(gbw * WSLOT * 8);
-    x.wso = (uint32_t *)take(gbw * WSLOT * 4);
-    x.wsp = (uint32_t *)take(gbw * WSLOT * 4);
     if (w) *w = x;
     return (int64_t)(p - p0) + 256;
 }
@@ -2217,12 +2217,18 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 // gather / final (~47 us of four launches at C3):
 //  * every workgroup (HT threads x GI rows, the gather's shape) classifies its rows against
 //    the key window [wlo, whi) of half-width H = 2^win_lh(tmove, wfloor) around the previous
-//    threshold key: a row below it is selected whatever k is, so it adds to the count,
-//    the fp64 sum of r (fixed tree) and the 8 fit sums; a row inside is handed over (key,
-//    r, caller index, work row; at most WSLOT per workgroup, in row order); every row
-//    outside adds to one of NCS coarse buckets per side, whose widths grow with the
-//    distance from the window (H/4 units: 1, 1, 1, 1, then 4 per octave), counted with
-//    exact fixed-point sums of r (LDS atomics, then agent-scope atomics into NCB words);
+//    threshold key: a row below it is selected whatever k is, so it adds to the count, the
+//    sum of r and the 8 fit sums; a row inside is appended to the window rows (key, r,
+//    caller index and its fit pair; one append counter per XCD); every row outside adds to
+//    one of NCS coarse buckets per side, whose widths grow with the distance from the
+//    window (H/4 units: 1, 1, 1, 1, then 4 per octave), counted with exact fixed-point sums
+//    of r (LDS atomics, then agent-scope atomics into NCB words);
+//  * the workgroup's totals go to the launch's accumulators with agent-scope atomics, in an
+//    order-free exact form (round 5): counts as integers, the workgroup's fp64 sums of r
+//    and of the fit terms (fixed trees inside the workgroup) as fixed-point integers on a
+//    grid that holds them exactly (wfx_grid), split into 48-bit digits.  Any arrival order
+//    gives the same total bits, so the last workgroup reads ~300 words instead of ~250
+//    per-workgroup records (round 4: records + their fixed-order sums, ~5 us of its tail);
 //  * the last workgroup to arrive (k_fit_sums' two-level hand-off) sorts the window rows
 //    in LDS, scans them from (K0, S0) and takes the first FRMSD minimum inside the window,
 //    then proves it global as k_sel_bounds does: every non-empty coarse bucket's lower
@@ -2231,10 +2237,10 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
 //    so its lower bound stays above the curve's rise there (fixed-width coarse buckets
 //    next to the window were ~1e-3 loose in h at the window edge, where the curve rises
 //    ~1e-7 above its minimum).  Then publish, the loop step, the fit of the next body
-//    (the rows below the window + the selected window rows, in a fixed order) and the
-//    host flag, as k_sel_final.
-//  * Anything unproven (a workgroup with > WSLOT window rows, > CAP in all, none, a
-//    non-finite r, a bound <= U): the launch leaves the state alone except win_fail and
+//    (the rows below the window + the selected window rows in sorted order) and the host
+//    flag, as k_sel_final.
+//  * Anything unproven (> CAP window rows, none, a non-finite r, a workgroup sum of r off
+//    the grid, a bound <= U): the launch leaves the state alone except win_fail and
 //    nn_reuse (the queued NN launch becomes a no-op) and stores kFlagRetry; the host
 //    then enqueues launch_select for the same call.  The result never depends on which
 //    path decided: both give the first minimum of the same exact curve (S sums differ in
@@ -2298,7 +2304,65 @@ __device__ ScanOut win_scan_small(unsigned c, const FinalIn &in, const u64 *lk, 
     return r;
 }
 
-// candidates staged in LDS for lds_sort_scan<CAP, true, true> + their work rows
+// --- order-free exact accumulation across workgroups
+// v * 2^g truncated toward zero, two's complement in 128 bits (|v| 2^g < 2^126); *exact:
+// whether no bit of v lies below the grid
+__device__ __forceinline__ u128 wfx_grid(double v, int g, bool *exact) {
+    const u64 b = (u64)__double_as_longlong(v);
+    const int ex = (int)((b >> 52) & 0x7ff);
+    if (ex == 0) {  // zero or subnormal
+        *exact = (b << 1) == 0ULL;
+        return (u128)0;
+    }
+    const u64 m = (b & 0xfffffffffffffULL) | (1ULL << 52);
+    const int sft = ex - 1075 + g;
+    u128 a;
+    if (sft >= 0) {
+        a = (u128)m << sft;
+        *exact = true;
+    } else if (sft > -64) {
+        a = (u128)(m >> (-sft));
+        *exact = (m & ((1ULL << (-sft)) - 1ULL)) == 0ULL;
+    } else {
+        a = (u128)0;
+        *exact = false;
+    }
+    return (b >> 63) ? (u128)0 - a : a;
+}
+// the three 48-bit digits of a (the top one signed), each added with one atomic: the
+// digit sums of up to 2^12 workgroups per word stay below 2^60
+constexpr u64 kD48 = (1ULL << 48) - 1ULL;
+__device__ __forceinline__ void wfx_add3(u64 *w3, u128 a) {
+    __hip_atomic_fetch_add(&w3[0], (u64)a & kD48, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&w3[1], (u64)(a >> 48) & kD48, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&w3[2], (u64)((__int128)a >> 96), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the accumulated value (digit sums s0, s1 >= 0, s2 signed) / 2^g, rounded (a fixed
+// formula: the same bits for the same digit sums)
+__device__ __forceinline__ double wfx_total(u64 s0, u64 s1, u64 s2, int g) {
+    const u128 lo = (u128)s0 + ((u128)s1 << 48);  // < 2^61 + 2^109
+    const double dlo = ldexp((double)(u64)(lo >> 64), 64 - g) + ldexp((double)(u64)lo, -g);
+    return dlo + ldexp((double)(long long)s2, 96 - g);
+}
+// the accumulator words of one copy (kWinCopies copies, blockIdx % kWinCopies)
+constexpr int WA_BEL = 0;   // rows below the window
+constexpr int WA_BAD = 1;   // non-finite rows + workgroup sums of r off the grid
+constexpr int WA_S0 = 2;    // 3 digits: sum of r below the window, grid 2^(100 - e_below)
+constexpr int WA_FIT = 5;   // 8 x 3 digits: the fit sums of the rows below it, grid 2^56
+constexpr int WA_KMN = 29;  // max of ~key (the call's smallest finite key)
+constexpr int WA_KMX = 30;  // max of key
+constexpr int WACC = 32;
+constexpr int WFIT_G = 56;
+constexpr int WCNT_S = 16;  // append counters 64 B apart (one per XCD copy)
+static_assert(WACC == 32 && WCNT_S == 16, "carve_bytes' window words");
+__device__ __forceinline__ int win_s0_grid(const WMap &m) {
+    // r < 2^e for every row below the window (the nearest coarse bucket's exponent); a
+    // workgroup's sum < 2^(e + 12) lands below 2^112 on this grid
+    const int e = win_bucket_exp(m, NCS - 1);
+    return 100 - min(e, 900);
+}
+
+// window rows in LDS for lds_sort_scan<CAP, true, true> + where each one's pair lies
 constexpr int W_ROW = LdsLay<CAP, true>::END;
 constexpr int W_MAXWG = 2 * NSB - 1;  // workgroups of one launch (8M rows: 1954)
 constexpr int W_SMEM = W_ROW + CAP * 4;
@@ -2324,9 +2388,9 @@ __device__ unsigned long long g_winp[8];
     } while (0)
 #endif
 
-// The window path's decision (k_sel_win's last workgroup): the coarse buckets (read and
-// zeroed), the records of the nwb pass workgroups
-__device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap &m0, double lamv,
+// The window path's decision (k_sel_win's last workgroup): the accumulators, the coarse
+// buckets and the append counters (each read and zeroed), the window rows, the bounds.
+__device__ __forceinline__ void win_tail(SelWS w, int64_t n, const WMap &m0, double lamv,
                                          IterState *st, const LoopCtl &lc, int *host_flag,
                                          const FitSrc &fs, int force_retry, Scr &scr) {
     const int t = threadIdx.x;
@@ -2338,6 +2402,9 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     __shared__ IterState s_st;
     __shared__ double s_fit[8];
     __shared__ u64 s_tko[2];
+    __shared__ u64 s_acc[kWinCopies * WACC];
+    __shared__ unsigned s_wc[kWinCopies + 1];
+    // one round of exchanges: the coarse buckets, the accumulators, the append counters
     unsigned cc = 0;
     u64 cf = 0;
     if (t < NCB) {
@@ -2354,180 +2421,113 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
             cf += fq[q];
         }
     }
+    static_assert(kWinCopies * WACC <= HT, "one accumulator word per thread");
+    const u64 av = t < kWinCopies * WACC
+                       ? __hip_atomic_exchange(&w.wacc[t], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : 0ULL;
+    const unsigned wcv = (t >= HT - kWinCopies)
+                             ? __hip_atomic_exchange(&w.wcnt[(t - (HT - kWinCopies)) * WCNT_S], 0u,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0u;
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
+    if (t < kWinCopies * WACC) s_acc[t] = av;
+    if (t >= HT - kWinCopies) s_wc[t - (HT - kWinCopies)] = wcv;
+    __syncthreads();
     WINP_T(6);
-    // The records, read coalesced: 16 lanes per record (lane e reads word e), 32 records per
-    // pass of the workgroup (a record per thread read 15 scattered words: ~9 us for the
-    // fused pass's ~1,000 records).  Thread (e, r0) accumulates word e of records r0, r0 +
-    // 32, ... in that order; the 32 partials of a word are then added in r0 order (a fixed
-    // tree: deterministic), the window-row counts kept per record for their offsets.
-    using LY = LdsLay<CAP, true>;
-    unsigned *s_off = (unsigned *)(sm + LY::BC);  // [nwb + 1] (the sort's bin area, free until it)
-    static_assert(2 * NSB >= W_MAXWG + 1, "workgroup offsets in the bin area");
-    // the 32 partials of each word: in the window rows' key area (free until they load)
-    u64 (*s_part)[HT / 16 + 1] = reinterpret_cast<u64 (*)[HT / 16 + 1]>(sm + LY::K);
-    static_assert(16 * (HT / 16 + 1) * 8 <= CAP * 8, "record partials in the key area");
-    __shared__ u64 s_tot[16];
-    {
-        const int e = t & 15, r0 = t >> 4;
-        constexpr int RP = HT / 16;
-        u64 iacc = 0ULL;  // e 0-2: integer sums; 13, 14: max
-        double dacc = 0.0;  // e 3-12: fp64 sums in record order
-        // UR records' loads in flight per thread before their first use (a plain loop
-        // waited for each load in turn: ~31 dependent latencies at ~1,000 records)
-        constexpr int UR = 16;
-        for (int rb = r0; rb < nwb; rb += UR * RP) {  // (rb: uniform per 16-lane group)
-            u64 v[UR];
-#pragma unroll
-            for (int u = 0; u < UR; ++u) {
-                const int r = rb + u * RP;
-                v[u] = r < nwb ? __hip_atomic_load(&w.wrec[(int64_t)r * WREC + e], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : 0ULL;
-            }
-#pragma unroll
-            for (int u = 0; u < UR; ++u) {
-                const int r = rb + u * RP;
-                if (r < nwb) {
-                    if (e == 1 && r <= W_MAXWG) s_off[r] = (unsigned)v[u];  // window rows of record r
-                    if (e < 3) iacc += v[u];
-                    else if (e < 13) dacc = dacc + __longlong_as_double((long long)v[u]);
-                    else if (e < 15) iacc = max(iacc, v[u]);
-                }
-            }
+    // the copies combined (integers: any order), field by field
+    __shared__ u64 s_tot[WACC];
+    if (t < WACC) {
+        u64 v = 0ULL;
+        for (int q = 0; q < kWinCopies; ++q) {
+            const u64 x = s_acc[q * WACC + t];
+            v = (t == WA_KMN || t == WA_KMX) ? max(v, x) : v + x;
         }
-        s_part[e][r0] = (e >= 3 && e < 13) ? (u64)__double_as_longlong(dacc) : iacc;
-        __syncthreads();
-        WINP_T(7);
-        if (t < 15) {
-            // the 32 partials loaded together, then added in q order (one LDS round trip
-            // instead of 32 dependent ones)
-            u64 pv[RP];
-#pragma unroll
-            for (int q = 0; q < RP; ++q) pv[q] = s_part[t][q];
-            u64 ia = 0ULL;
-            double da = 0.0;
-            if (t < 3) {
-#pragma unroll
-                for (int q = 0; q < RP; ++q) ia += pv[q];
-            } else if (t < 13) {
-#pragma unroll
-                for (int q = 0; q < RP; ++q) da = da + __longlong_as_double((long long)pv[q]);
-            } else {
-#pragma unroll
-                for (int q = 0; q < RP; ++q) ia = max(ia, pv[q]);
-            }
-            s_tot[t] = (t >= 3 && t < 13) ? (u64)__double_as_longlong(da) : ia;
-        }
-        __syncthreads();
+        s_tot[t] = v;
     }
-    const long long K0 = (long long)s_tot[0], Wt = (long long)s_tot[1];
-    const long long bad = (long long)s_tot[2] + (nwb > W_MAXWG ? 1 : 0);
-    const double S0 = __longlong_as_double((long long)s_tot[3]);
-    const double Swin = __longlong_as_double((long long)s_tot[12]);
-    const u64 kra = s_tot[13], krb = s_tot[14];
+    if (t == WACC) {  // the append counters' prefix (region q: rows [s_wc[q], s_wc[q + 1]))
+        unsigned run = 0;
+        bool over = false;
+        for (int q = 0; q < kWinCopies; ++q) {
+            const unsigned c = s_wc[q];
+            over = over || c > (unsigned)CAP;
+            s_wc[q] = run;
+            run += c;
+        }
+        s_wc[kWinCopies] = over ? (unsigned)(CAP + 1) : run;
+    }
+    __syncthreads();
+    const long long K0 = (long long)s_tot[WA_BEL];
+    const long long Wt = (long long)s_wc[kWinCopies];
+    const long long bad = (long long)s_tot[WA_BAD];
+    const int g0 = win_s0_grid(m0);
+    const double S0 = wfx_total(s_tot[WA_S0], s_tot[WA_S0 + 1], s_tot[WA_S0 + 2], g0);
     WMap m = m0;  // with the call's key range (the lowest coarse bucket's lowest r)
-    m.kmin = ~kra;
-    m.kmax = krb;
-    if (t < 8) s_fit[t] = __longlong_as_double((long long)s_tot[4 + t]);  // (+ the window rows' part after the sort)
+    m.kmin = ~s_tot[WA_KMN];
+    m.kmax = s_tot[WA_KMX];
+    if (t < 8)
+        s_fit[t] = wfx_total(s_tot[WA_FIT + 3 * t], s_tot[WA_FIT + 3 * t + 1], s_tot[WA_FIT + 3 * t + 2], WFIT_G);
     bool fail = bad != 0 || Wt <= 0 || Wt > CAP;
     const double p = 2.0 * lamv + 1.0;
-    // each coarse bucket's lower bound of h (k_sel_bounds' block_lb), before the sort: only
-    // its comparison with U waits for the minimum.  Rows before a bucket: the buckets before
-    // it, + K0 + Wt above the window; lower sum: the fixed-point brackets (the window's
-    // exact S0 + Swin above it)
-    double lbv = INFINITY;
-    bool lbok = true;
-    {
-        const int eb = t < NCB ? win_bucket_exp(m, t) : 0;
-        const double lo_sum = eb < 1024 ? ldexp((double)cf, eb - m.fxb) : 0.0;  // (exact)
-        long long C0 = t < NCB ? (long long)cc : 0;
-        double Pb = (t < NCS) ? lo_sum : 0.0;
-        double Pa = (t >= NCS && t < NCB) ? lo_sum : 0.0;
-        blk_excl_scan3(C0, Pb, Pa, scr);
-        if (t < NCB) {
-            if (t == NCS - 1 && C0 + (long long)cc != K0) lbok = false;  // (a row lost: never)
-            if (cc) {
-                const long long c0 = t < NCS ? C0 : C0 + Wt;  // (C0 counts every row below the window)
-                const double P0 = t < NCS ? Pb : (S0 + Swin) + Pa;
-                lbv = block_lb(c0, (long long)cc, P0, lo_r(win_bucket_lo(m, t)), p);
-            }
-        }
-    }
-    WINP_T(1);
-    // the window rows into LDS, in workgroup order (lds_sort_scan's layout + work rows)
+    // the window rows into LDS (lds_sort_scan's layout; lrow: where the row's pair lies):
+    // their loads first, then the coarse buckets' bounds while they are in flight
+    using LY = LdsLay<CAP, true>;
     u64 *lk = (u64 *)(sm + LY::K);
     double *lr = (double *)(sm + LY::R);
     uint32_t *lo = (uint32_t *)(sm + LY::O);
     uint32_t *lrow = (uint32_t *)(sm + W_ROW);
-    // each workgroup's first candidate index (in the sort's bin area, free until the sort):
-    // an exclusive scan of the records' window-row counts, a contiguous run per thread; then
-    // every candidate loads its slot: one round of loads (a per-workgroup loop of dependent
-    // loads serialised them)
-    {
-        const int G = (nwb + HT - 1) / HT;
-        const int g0 = min(nwb, t * G), g1 = min(nwb, g0 + G);
-        long long loc = 0;
-        for (int g = g0; g < g1; ++g) loc += s_off[g];
-        long long tot_unused;
-        long long off = blk_excl_scan_ll(loc, scr, tot_unused);  // (its barriers: s_off read)
-        if (!fail) {
-            for (int g = g0; g < g1; ++g) {
-                const unsigned c = s_off[g];
-                s_off[g] = (unsigned)off;
-                off += c;
-            }
-            if (t == 0) s_off[nwb] = (unsigned)Wt;
-        }
-    }
-    __syncthreads();
+    constexpr int EU = CAP / HT;
+    uint32_t sl[EU];
+    u64 vk[EU];
+    double vr[EU];
+    uint32_t vo[EU];
     if (!fail) {
-        constexpr int EU = CAP / HT;
-        int64_t sl[EU];
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const int e = t + u * HT;
-            sl[u] = -1;
+            int q = 0;
+#pragma unroll
+            for (int j = 1; j < kWinCopies; ++j) q += (e >= (int)s_wc[j]) ? 1 : 0;
+            sl[u] = (uint32_t)(q * CAP + (e - (int)s_wc[q]));
             if (e < Wt) {
-                int lo_g = 0, hi_g = nwb;  // the last workgroup whose first index is <= e
-                while (hi_g - lo_g > 1) {
-                    const int mid = (lo_g + hi_g) >> 1;
-                    if ((int)s_off[mid] <= e) lo_g = mid;
-                    else hi_g = mid;
-                }
-                sl[u] = (int64_t)lo_g * WSLOT + (e - (int)s_off[lo_g]);
+                vk[u] = __hip_atomic_load(&w.wk[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vr[u] = __hip_atomic_load(&w.wr[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vo[u] = __hip_atomic_load(&w.wo[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        u64 vk[EU];
-        double vr[EU];
-        uint32_t vo[EU], vp[EU];
+    }
+    // each coarse bucket below the window: its lower bound of h (k_sel_bounds' block_lb):
+    // rows before it = the buckets before it; lower sum = their fixed-point brackets.  The
+    // buckets above the window need the window's sum: after the scan.
+    double lbv = INFINITY;
+    bool lbok = true;
+    const int eb = t < NCB ? win_bucket_exp(m, t) : 0;
+    const double lo_sum = (t < NCB && eb < 1024) ? ldexp((double)cf, eb - m.fxb) : 0.0;  // (exact)
+    long long C0 = t < NCB ? (long long)cc : 0;
+    double Pb = (t < NCS) ? lo_sum : 0.0;
+    double Pa = (t >= NCS && t < NCB) ? lo_sum : 0.0;
+    blk_excl_scan3(C0, Pb, Pa, scr);
+    if (t < NCS) {
+        if (t == NCS - 1 && C0 + (long long)cc != K0) lbok = false;  // (a row lost: never)
+        if (cc) lbv = block_lb(C0, (long long)cc, Pb, lo_r(win_bucket_lo(m, t)), p);
+    }
+    if (!fail) {
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
-            if (sl[u] >= 0) {
-                vk[u] = __hip_atomic_load(&w.wsk[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                vr[u] = __hip_atomic_load(&w.wsr[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                vo[u] = __hip_atomic_load(&w.wso[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                vp[u] = __hip_atomic_load(&w.wsp[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < EU; ++u) {
-            if (sl[u] >= 0) {
-                const int e = t + u * HT;
+            const int e = t + u * HT;
+            if (e < Wt) {
                 lk[e] = vk[u];
                 lr[e] = vr[u];
                 lo[e] = vo[u];
-                lrow[e] = vp[u];
+                lrow[e] = sl[u];
             }
         }
     }
     __syncthreads();
     WINP_T(2);
-    const double lam = lamv;
     FinalIn in;
     in.N = n;
-    in.lam = lam;
+    in.lam = lamv;
     in.S0 = S0;
     in.K0 = K0;
     in.U = 0.0;
@@ -2556,34 +2556,43 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
             s_tko[0] = rs.tk;
             s_tko[1] = (u64)rs.to;
         }
+        // the buckets above the window: every row below them is counted (K0 + Wt + the
+        // buckets before), their lower sum is S0 + the window's sum (its sorted scan) + the
+        // brackets before
+        if (t >= NCS && t < NCB && cc)
+            lbv = block_lb(C0 + K0 + Wt, (long long)cc, (S0 + rs.total) + Pa, lo_r(win_bucket_lo(m, t)), p);
     }
     const bool ok = lbok && (lbv > U);  // (empty buckets: lbv = inf)
     fail = fail || blk_max_ll(ok ? 0 : 1, scr) != 0 || force_retry;  // (its barriers publish s_tko)
     WINP_T(4);
 #ifdef FICP_WIN_PROF
     if (fail && t == 0)
-        printf("WINPROF_REC coarse+state %llu records %llu rest %llu\n", wt_[6] - wt_[0], wt_[7] - wt_[6], wt_[1] - wt_[7]);
-    if (fail && t == 0)
-        printf("WINPROF W=%lld K0=%lld fail=%d | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu (10 ns)\n",
-               Wt, K0, (int)fail, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
+        printf("WINPROF W=%lld K0=%lld fail=1 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | acc %llu rows %llu sort %llu bounds %llu (10 ns)\n",
+               Wt, K0, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
                g_winp[5] - g_winp[4], g_winp[2] - g_winp[5], g_winp[6] - g_winp[2], wt_[0] - g_winp[6],
-               wt_[1] - wt_[0], wt_[2] - wt_[1], wt_[3] - wt_[2], wt_[4] - wt_[3]);
+               wt_[6] - wt_[0], wt_[2] - wt_[6], wt_[3] - wt_[2], wt_[4] - wt_[3]);
 #endif
     if (fail) {
         if (t == 0) win_retry(st, host_flag);
         return;
     }
-    // the fit of the selected window rows, candidate order (deterministic)
-    const u64 tk = s_tko[0];
-    const uint32_t to = (uint32_t)s_tko[1];
-    double cf8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (fs.on)
-        for (int e = t; e < (int)Wt; e += HT)
-            if (!less_ko(tk, to, lk[e], lo[e])) fit_row(cf8, fs, lrow[e]);
-    if (fs.on) blk_sum8_add(cf8, s_fit, scr);
+    // the fit of the selected window rows, in sorted order (positions t, t + HT, ...; a
+    // fixed tree: deterministic), their pairs from the window rows' pair array
+    const uint32_t nsel = (uint32_t)(rs.bk - K0);
+    if (fs.on) {
+        const uint16_t *pos = (const uint16_t *)(sm + LY::POS);
+        double cf8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t q = t; q < nsel; q += HT) {
+            const uint32_t s = lrow[pos[q]];
+            const double2 a = *reinterpret_cast<const double2 *>(w.wp + 4 * (int64_t)s);
+            const double2 b = *reinterpret_cast<const double2 *>(w.wp + 4 * (int64_t)s + 2);
+            fit_add(cf8, a.x, a.y, b.x, b.y, fs.px, fs.py);
+        }
+        blk_sum8_add(cf8, s_fit, scr);
+    }
     WINP_T(8);
     if (t == 0) {
-        publish(&s_st, in, rs.bf, rs.bk, tk, to);
+        publish(&s_st, in, rs.bf, rs.bk, s_tko[0], (uint32_t)s_tko[1]);
         // the next window's smallest half-width from this one's row count (2^lh keys)
         {
             const int f = win_floor(s_st.wfloor, n);
@@ -2604,13 +2613,11 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     WINP_T(5);
     // (printed after the last stamp: a device printf is a host round trip)
     if (t == 0)
-        printf("WINPROF_REC coarse+state %llu records %llu rest %llu | fit %llu step %llu store %llu\n", wt_[6] - wt_[0],
-               wt_[7] - wt_[6], wt_[1] - wt_[7], wt_[8] - wt_[4], wt_[9] - wt_[8], wt_[5] - wt_[9]);
-    if (t == 0)
-        printf("WINPROF W=%lld K0=%lld fail=0 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | rec %llu fill %llu sort %llu bounds %llu fit+publish %llu (10 ns)\n",
+        printf("WINPROF W=%lld K0=%lld fail=0 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | acc %llu rows %llu sort %llu bounds %llu fit %llu step %llu store %llu (10 ns)\n",
                Wt, K0, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
                g_winp[5] - g_winp[4], g_winp[2] - g_winp[5], g_winp[6] - g_winp[2], wt_[0] - g_winp[6],
-               wt_[1] - wt_[0], wt_[2] - wt_[1], wt_[3] - wt_[2], wt_[4] - wt_[3], wt_[5] - wt_[4]);
+               wt_[6] - wt_[0], wt_[2] - wt_[6], wt_[3] - wt_[2], wt_[4] - wt_[3], wt_[8] - wt_[4],
+               wt_[9] - wt_[8], wt_[5] - wt_[9]);
 #endif
 }
 
@@ -2628,8 +2635,8 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     constexpr int WREP = 8, WRS = NCB + 1;
     __shared__ unsigned s_cc[WREP * WRS];
     __shared__ u64 s_cf[WREP * WRS];
-    __shared__ double s_red[NWAVE][11];
-    __shared__ unsigned s_wc[NWAVE];
+    __shared__ double s_red[NWAVE][9];
+    __shared__ u64 s_cnt[NWAVE];
     __shared__ int s_last;
     WINP_B(0);
     // every independent load first: the state's window inputs, the rows, the range parts
@@ -2687,7 +2694,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     // classify the rows
     unsigned nbel = 0, nbad = 0;
     u64 kmn = ~0ULL, kmx = 0ULL;  // the finite rows' key range (the last workgroup's kmin)
-    double sb = 0.0, swn = 0.0;
+    double sb = 0.0;
     double c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     u64 kk[WI];
     unsigned inw = 0;
@@ -2717,7 +2724,6 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
                 atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
             } else if (k < m0.whi) {
                 inw |= 1u << q;
-                swn = swn + v;
             } else {
                 const int b = NCS + win_cq((k - m0.whi) >> m0.su);
                 const int e = s_ce[b];
@@ -2727,18 +2733,44 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
         }
     }
     WINP_B(3);
-    // window rows handed over in row order (wave, then row slot, then lane): deterministic
-    u64 masks[WI];
-    unsigned wtot = 0;
+    // the window rows appended to this XCD copy's region (one atomic per wave that has
+    // any; the tail orders them by (key, caller index), so the append order is free)
+    const int cp = (int)(blockIdx.x % kWinCopies);
+    {
+        u64 masks[WI];
+        unsigned wtot = 0;
 #pragma unroll
-    for (int q = 0; q < WI; ++q) {
-        masks[q] = __ballot((inw >> q) & 1u);
-        wtot += (unsigned)__popcll(masks[q]);
+        for (int q = 0; q < WI; ++q) {
+            masks[q] = __ballot((inw >> q) & 1u);
+            wtot += (unsigned)__popcll(masks[q]);
+        }
+        if (wtot) {  // (uniform per wave)
+            unsigned wb = 0;
+            if (lane == 0)
+                wb = __hip_atomic_fetch_add(&w.wcnt[cp * WCNT_S], wtot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wb = __shfl(wb, 0);
+            const u64 lt = (1ULL << lane) - 1ULL;
+#pragma unroll
+            for (int q = 0; q < WI; ++q) {
+                if ((inw >> q) & 1u) {
+                    const unsigned sidx = wb + (unsigned)__popcll(masks[q] & lt);
+                    if (sidx < (unsigned)CAP) {  // (past CAP the tail fails the launch)
+                        const int64_t s = (int64_t)cp * CAP + sidx;
+                        __hip_atomic_store(&w.wk[s], kk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&w.wr[s], rr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&w.wo[s], oo[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&w.wp[4 * s], xs[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&w.wp[4 * s + 1], ys[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&w.wp[4 * s + 2], xt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&w.wp[4 * s + 3], yt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                wb += (unsigned)__popcll(masks[q]);
+            }
+        }
     }
-    if (lane == 0) s_wc[wave] = wtot;
     // the workgroup's sums (fixed trees: DPP wave sums, then the waves in order)
     sb = wave_sum63(sb);
-    swn = wave_sum63(swn);
 #pragma unroll
     for (int e = 0; e < 8; ++e) c8[e] = wave_sum63(c8[e]);
     const u64 cnt = wave_sum63_u64((u64)nbel | ((u64)nbad << 32));
@@ -2748,17 +2780,14 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     if (lane == 63) {
         s_kr[wave][0] = pka;
         s_kr[wave][1] = pkb;
-    }
-    if (lane == 63) {
         s_red[wave][0] = sb;
 #pragma unroll
         for (int e = 0; e < 8; ++e) s_red[wave][1 + e] = c8[e];
-        s_red[wave][9] = __longlong_as_double((long long)cnt);
-        s_red[wave][10] = swn;
+        s_cnt[wave] = cnt;
     }
     __syncthreads();  // (the LDS atomics, the wave counts and sums are complete)
     WINP_B(4);
-    // the coarse buckets first: their atomics complete while the rest is stored
+    // the coarse buckets first: their atomics complete while the rest is added
     if (t < NCB) {
         unsigned c = 0;
         u64 f = 0;
@@ -2768,60 +2797,40 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
             f += s_cf[q * WRS + t];
         }
         if (c) {
-            const int cp = (int)(blockIdx.x % kWinCopies) * NCB + t;  // (the XCD's copy)
-            __hip_atomic_fetch_add(&w.gcc[cp], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&w.gcf[cp], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int cb = cp * NCB + t;  // (the XCD's copy)
+            __hip_atomic_fetch_add(&w.gcc[cb], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&w.gcf[cb], f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    unsigned wpos = 0, wall = 0;
-#pragma unroll
-    for (int q = 0; q < NWAVE; ++q) {
-        wpos += q < wave ? s_wc[q] : 0u;
-        wall += s_wc[q];
-    }
-    const int blk = blockIdx.x;
-    if (wtot && wall <= (unsigned)WSLOT) {
-        const u64 lt = (1ULL << lane) - 1ULL;
-#pragma unroll
-        for (int q = 0; q < WI; ++q) {
-            if ((inw >> q) & 1u) {
-                const int64_t slot = (int64_t)blk * WSLOT + wpos + (unsigned)__popcll(masks[q] & lt);
-                __hip_atomic_store(&w.wsk[slot], kk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&w.wsr[slot], rr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&w.wso[slot], oo[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&w.wsp[slot], (uint32_t)row_of(q), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-            wpos += (unsigned)__popcll(masks[q]);
-        }
-    }
-    if (t == HT - 12) {  // the record's key range words: max(~key), max(key)
-        u64 a = s_kr[0][0], b = s_kr[0][1];
-        for (int q = 1; q < NWAVE; ++q) {
-            a = max(a, s_kr[q][0]);
-            b = max(b, s_kr[q][1]);
-        }
-        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 13], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&w.wrec[(int64_t)blockIdx.x * WREC + 14], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (t >= HT - 11) {  // the record (the last wave: wave 0 flushed the buckets): count
-                         // below, window rows, bad rows, sum of r below, fit sums, window r
-        const int f = t - (HT - 11);
-        double v = s_red[0][f];
-        u64 cv = (u64)__double_as_longlong(s_red[0][9]);
-        for (int q = 1; q < NWAVE; ++q) {
-            v = v + s_red[q][f];
-            cv += (u64)__double_as_longlong(s_red[q][9]);
-        }
-        u64 *rec = w.wrec + (int64_t)blk * WREC;
-        if (f == 9) {
-            const u64 bad = (cv >> 32) + (wall > (unsigned)WSLOT ? 1ULL : 0ULL);
-            __hip_atomic_store(&rec[0], cv & 0xffffffffULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&rec[1], (u64)wall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&rec[2], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the workgroup's totals into the accumulators (the last wave: wave 0 flushed the
+    // buckets): lane 0 the sum of r below (grid 2^g0), lanes 1-8 the fit sums (2^56),
+    // lane 9 the counts, lane 10 the key range
+    if (wave == NWAVE - 1 && lane < 11) {
+        u64 *acc = w.wacc + cp * WACC;
+        if (lane < 9) {
+            double v = s_red[0][lane];
+            for (int q = 1; q < NWAVE; ++q) v = v + s_red[q][lane];
+            bool exact = true;
+            const u128 a = wfx_grid(v, lane == 0 ? win_s0_grid(m0) : WFIT_G, &exact);
+            wfx_add3(acc + (lane == 0 ? WA_S0 : WA_FIT + 3 * (lane - 1)), a);
+            // a sum of r off its grid cannot be carried exactly: the tail falls back
+            if (lane == 0 && !exact)
+                __hip_atomic_fetch_add(&acc[WA_BAD], 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (lane == 9) {
+            u64 cv = 0;
+            for (int q = 0; q < NWAVE; ++q) cv += s_cnt[q];
+            if (cv & 0xffffffffULL)
+                __hip_atomic_fetch_add(&acc[WA_BEL], cv & 0xffffffffULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cv >> 32)
+                __hip_atomic_fetch_add(&acc[WA_BAD], cv >> 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(&rec[f < 9 ? 3 + f : 12], (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            u64 a = s_kr[0][0], b = s_kr[0][1];
+            for (int q = 1; q < NWAVE; ++q) {
+                a = max(a, s_kr[q][0]);
+                b = max(b, s_kr[q][1]);
+            }
+            __hip_atomic_fetch_max(&acc[WA_KMN], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_max(&acc[WA_KMX], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     WINP_B(5);
@@ -2845,7 +2854,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     }
     __syncthreads();
     if (!s_last) return;
-    win_tail(w, (int)gridDim.x, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
+    win_tail(w, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
 }
 
 __global__ void k_sel_init(SelWS w) {
@@ -2863,6 +2872,10 @@ __global__ void k_sel_init(SelWS w) {
     }
     for (int b = threadIdx.x; b < 9 * WCTR; b += blockDim.x)
         __hip_atomic_exchange(&w.wctr[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int b = threadIdx.x; b < kWinCopies * WACC; b += blockDim.x)
+        __hip_atomic_exchange(&w.wacc[b], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int b = threadIdx.x; b < kWinCopies * WCNT_S; b += blockDim.x)
+        __hip_atomic_exchange(&w.wcnt[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- distributed selection (source rows split over ranks) -------

@@ -163,6 +163,39 @@ def test_batch_matches_single_runs():
         assert b.stats[j]["k_last"] == icp.last_stats["k_last"]
 
 
+def test_batch_c4_size_plots_vs_oracle(oracle, monkeypatch):
+    """plots of C4's own size (10k trees x 10k stems) inside a batch, against the
+    oracle run of each plot alone: NN-call count, k of every call the oracle's curve pins,
+    XY within 1e-6, Z bit-identical -- in the batch work order (default) and in caller
+    order (FICP_BATCH_WORK=0), which must take the same calls and k.  Plot 5 has duplicated
+    trees (exact equal distances: ties at k are broken by the caller's row in both orders)."""
+    from coregistrationgame_amd import FractionalICPBatch, synth
+    plots = synth.make_batch(64, 10_000, 10_000, 0.8, 10_000_000, md=3)
+    srcs = [p.source for p in plots]
+    tgts = [p.target for p in plots]
+    dup = srcs[5].copy()
+    dup[1::2] = dup[0::2][: len(dup[1::2])]  # every odd tree repeats its even neighbour
+    srcs[5] = dup
+    runs = {}
+    for name, env in (("work", "1"), ("caller", "0")):
+        monkeypatch.setenv("FICP_BATCH_WORK", env)
+        b = FractionalICPBatch(srcs, tgts)
+        runs[name] = (b.run(trace=True), b.stats, b.k_trace)
+    (fw, sw, kw), (fc, sc, kc) = runs["work"], runs["caller"]
+    for j in range(64):
+        np.testing.assert_array_equal(kw[j], kc[j], err_msg=str(j))
+        np.testing.assert_allclose(fw[j][:, :2], fc[j][:, :2], atol=1e-6, rtol=0, err_msg=str(j))
+    for j in (0, 5, 31, 40, 63):  # both sub-batches
+        ofinal, otr = oracle.run(srcs[j], tgts[j], nthreads=8)
+        assert sw[j]["n_nn_calls"] == len(otr["k"]), j
+        first = pinned_prefix(otr["gap"], otr["frmsd"], 1.0 + np.abs(srcs[j][:, :2]).max())
+        assert first >= 3, (j, first)
+        np.testing.assert_array_equal(kw[j][:first], otr["k"][:first], err_msg=str(j))
+        assert sw[j]["k_last"] == otr["k"][-1], j
+        np.testing.assert_allclose(fw[j][:, :2], ofinal[:, :2], atol=1e-6, rtol=0, err_msg=str(j))
+        np.testing.assert_array_equal(bits(fw[j][:, 2]), bits(srcs[j][:, 2]))
+
+
 def test_batch_c4_properties():
     """C4 at full size (1024 plots x 10k/10k): every plot undoes its misregistration, the
     per-plot transforms reproduce the moved XY, and stage counters are consistent."""

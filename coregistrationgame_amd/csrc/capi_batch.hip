@@ -86,6 +86,7 @@ struct BatchTrees {
     const double *x, *y, *z;
     int64_t n;
     const int32_t *plot;
+    const int64_t *off_h, *off_d;  // per-plot row offsets (host, device)
 };
 
 // per-plot CHM grids in one set of arrays (cells of plot p: cell_base_p .. +gx*gy-1) and,
@@ -113,12 +114,15 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
     const double *bb = b.rep.as<const double>();
     grids.assign(nplots, PlotGrid{});
     int64_t ncells = 0, nwkeys = 0;
+    int64_t ps_pts = 0, ps_keys = 0;  // the per-plot sort's largest plot (points, keys)
     for (int32_t p = 0; p < nplots; ++p) {
         PlotGrid &g = grids[p];
         const int64_t mp = to_h[p + 1] - to_h[p];
         g.m = (int)mp;
         g.cell_base = ncells;
         g.wbase = nwkeys;
+        // (every plot's trees, those of plots without stems included, fit the plot sort or not)
+        if (trees.n > 0) ps_pts = std::max<int64_t>(ps_pts, trees.off_h[p + 1] - trees.off_h[p]);
         if (mp == 0) {  // no CHM stems: the plot never runs (ficp.py:66-68, 125-126)
             g.x0 = g.y0 = g.px = g.py = 0.0;
             g.h = g.inv_h = 1.0;
@@ -144,14 +148,50 @@ int build_batch_grids(ficp_ctx *c, BatchBufs &b, int32_t nplots, const int64_t *
         g.py = y0 + 0.5 * (y1 - y0);
         ncells += gx * gy;
         nwkeys += ((gx + 7) / 8) * ((gy + 7) / 8) * 64;  // (k_bsort.hip st_key's range)
+        ps_keys = std::max<int64_t>(ps_keys, ((gx + 7) / 8) * ((gy + 7) / 8) * 64);  // (>= gx * gy)
+        ps_pts = std::max<int64_t>(ps_pts, mp);
     }
     if (ncells > 0x7ffffffe) return fail(FICP_EINVAL, "batch grid too large");
     CHK(b.grids.ensure((size_t)nplots * sizeof(PlotGrid)));
     HIPCHK(hipMemcpyAsync(b.grids.p, grids.data(), (size_t)nplots * sizeof(PlotGrid),
                           hipMemcpyHostToDevice, c->stream));
-    CHK(b.tplot.ensure(m * 4));
     CHK(b.cell_start.ensure((ncells + 1) * 4));
     CHK(b.pts.ensure(m * sizeof(TPt)));
+    // Plots that fit one workgroup (C4: 10k stems and trees): the per-plot LDS sort of both
+    // jobs in one launch (k_batch.hip k_plot_sort, the same order as the bucket sort below).
+    // FICP_PLOT_SORT=0: the bucket sort.
+    const char *pse = getenv("FICP_PLOT_SORT");
+    if (plot_sort_fits(ps_pts, ps_keys) && !(pse && atoi(pse) == 0) && !getenv("FICP_GRID_ATOMIC")) {
+        PlotSortJob gjob{};
+        gjob.x = tx;
+        gjob.y = ty;
+        gjob.z = md == 3 ? tz : nullptr;
+        gjob.off = b.to.as<int64_t>();
+        gjob.mode = 0;
+        gjob.pts = b.pts.as<TPt>();
+        gjob.cell_start = b.cell_start.as<int32_t>();
+        PlotSortJob wjob{};
+        if (trees.n > 0) {
+            CHK(b.wx.ensure(trees.n * 8));
+            CHK(b.wy.ensure(trees.n * 8));
+            if (md == 3) CHK(b.wz.ensure(trees.n * 8));
+            CHK(b.worig.ensure(trees.n * 4));
+            wjob.x = trees.x;
+            wjob.y = trees.y;
+            wjob.z = md == 3 ? trees.z : nullptr;
+            wjob.off = trees.off_d;
+            wjob.mode = 1;
+            wjob.wx = b.wx.as<double>();
+            wjob.wy = b.wy.as<double>();
+            wjob.wz = md == 3 ? b.wz.as<double>() : nullptr;
+            wjob.worig = b.worig.as<uint32_t>();
+        }
+        HIPCHK(launch_plot_sort(gjob, trees.n > 0 ? &wjob : nullptr, b.grids.as<PlotGrid>(), nplots, c->stream));
+        *work = trees.n > 0;
+        return FICP_OK;
+    }
+    // the bucket sort and the atomic grid build key the stems by their plot
+    CHK(b.tplot.ensure(m * 4));
     HIPCHK(launch_fill_plot_ids(b.to.as<int64_t>(), nplots, b.tplot.as<int32_t>(), c->stream));
     // the work order's job (mode 3), when the bucket sort can plan it
     const bool want_work = trees.n > 0 && bsort_supported(trees.n, nwkeys);
@@ -255,7 +295,8 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             // FICP_BATCH_WORK=0: the trees stay in caller order
             const char *we = getenv("FICP_BATCH_WORK");
             const bool want = !(we && atoi(we) == 0);
-            const BatchTrees trees{sx, sy, md == 3 ? sz : nullptr, want ? n : 0, b.plot_of.as<int32_t>()};
+            const BatchTrees trees{sx, sy, md == 3 ? sz : nullptr, want ? n : 0, b.plot_of.as<int32_t>(),
+                                   so_h, b.so.as<int64_t>()};
             ProfScope ps(c, P_GRID, "batch_grid_build");
             CHK(build_batch_grids(c, b, nplots, to_h, tx, ty, tz, m, md, grids, trees, &work));
         }

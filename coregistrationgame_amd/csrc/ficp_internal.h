@@ -401,7 +401,7 @@ __host__ __device__ __forceinline__ int win_start_log(long long n) {
     return v < kWinHMinLog ? kWinHMinLog : (v > 48 ? 48 : v);
 }
 #ifndef FICP_WIN_HMAX_EXTRA
-#define FICP_WIN_HMAX_EXTRA 4  // doublings of the window above its start (tools/build_variant.sh A/B)
+#define FICP_WIN_HMAX_EXTRA 7  // doublings of the window above its start (big windows from +3)
 #endif
 __host__ __device__ __forceinline__ int win_hmax_log(long long n) {
     return win_start_log(n) + FICP_WIN_HMAX_EXTRA;
@@ -948,6 +948,21 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
                                 const PlotState *st, int md, hipStream_t s);
 hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
                              PlotState *st, hipStream_t s);
+// Per-plot LDS counting sort (k_batch.hip k_plot_sort): mode 0 the batch grid (TPt records
+// + cell_start, as k_bsort.hip mode 2), mode 1 the batch work order (wx, wy, wz, worig, as
+// mode 3), the same (key, row) order; one workgroup per plot and job (b: a second job).
+struct PlotSortJob {
+    const double *x, *y, *z;  // the points' columns (z nullable), plots concatenated
+    const int64_t *off;       // [nplots + 1] (device)
+    int mode;
+    TPt *pts;
+    int32_t *cell_start;
+    double *wx, *wy, *wz;
+    uint32_t *worig;
+};
+bool plot_sort_fits(int64_t max_points, int64_t max_keys);
+hipError_t launch_plot_sort(const PlotSortJob &a, const PlotSortJob *b, const PlotGrid *grids,
+                            int nplots, hipStream_t s);
 // plot chunks of the batch fit (k_batch_fit) for plots of at most max_rows rows
 int batch_fit_chunks(int64_t max_rows);
 // part: nplots * batch_fit_chunks(max_rows) * 8 doubles; ctr: nplots arrival counters

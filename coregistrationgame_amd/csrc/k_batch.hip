@@ -1037,6 +1037,164 @@ __global__ __launch_bounds__(UT) void k_batch_live(int nplots, const PlotState *
     }
 }
 
+// ---------------------------------------------------------------- per-plot sorts
+// The batch grid (stems by the cell of their plot's grid, row-major) and the batch work
+// order (trees by 8x8-cell supertile, then cell) as one LDS counting sort per plot: one
+// workgroup holds a plot's points in registers (PS_R per thread), counts their keys in LDS,
+// scans the counts, drops each point into its key's bin and ranks it there by its row
+// (bins hold ~1 point), then writes it at its final position -- scattered stores inside the
+// plot's own ~80-320 KB region, which its CU's L2 merges into whole lines.  The order is the
+// two-level bucket sort's (key, row), so the outputs are bit-identical to it; that sort moved
+// every point's 32-B record through global memory twice (~0.45 ms per 10M points).
+constexpr int PS_T = 1024;
+constexpr int PS_R = 12;
+constexpr int PS_MAXN = PS_T * PS_R;  // points of one plot (16-bit indices)
+constexpr int PS_MAXK = PS_T * PS_R;  // keys of one plot
+constexpr int PS_KPT = PS_MAXK / PS_T;
+
+__device__ __forceinline__ uint32_t ps_st_key(int cx, int cy, int gx) {  // (k_bsort.hip st_key)
+    const uint32_t nstx = (uint32_t)(gx + 7) >> 3;
+    const uint32_t stl = ((uint32_t)cy >> 3) * nstx + ((uint32_t)cx >> 3);
+    return (stl << 6) | ((uint32_t)(cy & 7) << 3) | (uint32_t)(cx & 7);
+}
+
+__global__ __launch_bounds__(PS_T) void k_plot_sort(PlotSortJob A, PlotSortJob B, const PlotGrid *grids,
+                                                    int nplots) {
+    const bool jb = (int)blockIdx.x >= nplots;
+    const PlotSortJob J = jb ? B : A;
+    const int p = (int)blockIdx.x - (jb ? nplots : 0);
+    const PlotGrid g = grids[p];
+    const int64_t b = J.off[p], e = J.off[p + 1];
+    const int N = (int)(e - b);
+    const int nk = J.mode == 0 ? g.gx * g.gy : ((g.gx + 7) >> 3) * ((g.gy + 7) >> 3) * 64;
+    if (N > PS_MAXN || nk >= PS_MAXK) return;  // (the host checks every plot: never)
+    // the sort's arrays, and afterwards (aliased) one output column staged in final order
+    __shared__ __align__(16) unsigned char s_mem[PS_MAXN * 8];
+    static_assert(PS_MAXK / 2 * 4 + PS_MAXK * 4 + PS_MAXN * 2 <= PS_MAXN * 8, "sort arrays in the stage");
+    uint32_t *s_cnt2 = (uint32_t *)s_mem;                            // two 16-bit counts per word
+    uint32_t *s_start = s_cnt2 + PS_MAXK / 2;                        // bin starts, then fill
+    uint16_t *s_idx = (uint16_t *)(s_start + PS_MAXK);               // bin slot -> point
+    __shared__ uint32_t s_w[PS_T / 64];
+    const int t = threadIdx.x;
+    for (int k = t; k < PS_MAXK / 2; k += PS_T) s_cnt2[k] = 0u;
+    // the points' keys (their coordinates are reloaded, coalesced and L2-hot, when the
+    // outputs are written: holding x, y, z of PS_R points per thread spilled 98 VGPRs)
+    int key[PS_R];
+    {
+        double px[PS_R], py[PS_R];
+#pragma unroll
+        for (int u = 0; u < PS_R; ++u) {
+            const int i = t + u * PS_T;
+            const bool in = i < N;
+            px[u] = in ? J.x[b + i] : 0.0;
+            py[u] = in ? J.y[b + i] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PS_R; ++u) {
+            key[u] = -1;
+            if (t + u * PS_T < N) {
+                const int cx = cell_coord_b(px[u], g.x0, g.inv_h, g.gx);
+                const int cy = cell_coord_b(py[u], g.y0, g.inv_h, g.gy);
+                key[u] = J.mode == 0 ? cy * g.gx + cx : (int)ps_st_key(cx, cy, g.gx);
+                atomicAdd(&s_cnt2[key[u] >> 1], (key[u] & 1) ? 0x10000u : 1u);
+            }
+        }
+    }
+    __syncthreads();
+    auto cnt_of = [&](int k) -> uint32_t { return (s_cnt2[k >> 1] >> (16 * (k & 1))) & 0xffffu; };
+    {  // exclusive scan of the counts, PS_KPT keys per thread (a contiguous run)
+        uint32_t c[PS_KPT], tot = 0;
+#pragma unroll
+        for (int j = 0; j < PS_KPT; ++j) {
+            const int k = t * PS_KPT + j;
+            c[j] = k < nk ? cnt_of(k) : 0u;
+            tot += c[j];
+        }
+        const uint32_t xi = (uint32_t)wave_incl_scan_ll((long long)tot);
+        const int lane = t & 63, w = t >> 6;
+        if (lane == 63) s_w[w] = xi;
+        __syncthreads();
+        uint32_t run = xi - tot;
+        for (int q = 0; q < w; ++q) run += s_w[q];
+#pragma unroll
+        for (int j = 0; j < PS_KPT; ++j) {
+            const int k = t * PS_KPT + j;
+            s_start[k] = run;
+            // the grid's cell starts (global rows; the cell after the plot's last one is the
+            // next plot's first: the same value from both plots)
+            if (J.mode == 0 && k <= nk) J.cell_start[g.cell_base + k] = (int32_t)(b + run);
+            run += c[j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PS_R; ++u)
+        if (key[u] >= 0) s_idx[atomicAdd(&s_start[key[u]], 1u)] = (uint16_t)(t + u * PS_T);
+    __syncthreads();
+    // final position of each point (its rank inside its bin by row), in key[]'s registers
+#pragma unroll
+    for (int u = 0; u < PS_R; ++u) {
+        if (key[u] < 0) continue;
+        const int i = t + u * PS_T;
+        const uint32_t be = s_start[key[u]], bs = be - cnt_of(key[u]);
+        uint32_t rank = 0;
+        for (uint32_t q = bs; q < be; ++q) rank += s_idx[q] < (uint16_t)i ? 1u : 0u;
+        key[u] = (int)(bs + rank);
+    }
+    const int *pos = key;
+    // the outputs field by field through the stage: each point's value reloaded (coalesced,
+    // L2-hot) and stored into the stage at its final position, then coalesced global stores
+    // (scattered 8-B global stores: every lane of a store on its own cache line).  Grid
+    // records (32 B: x, y, z, row) in two halves of positions, 16 B per record per pass.
+    double *sd = (double *)s_mem;
+    uint32_t *su = (uint32_t *)s_mem;
+    const int half = PS_MAXN / 2;
+    const int npass = J.mode == 0 ? 4 : 4;  // mode 0: (xy | zr) x 2 halves; mode 1: x, y, z, row
+    for (int ps = 0; ps < npass; ++ps) {
+        if (J.mode == 1 && ps == 2 && !J.wz) continue;  // (uniform: 2-D plots have no z)
+        const int f = J.mode == 0 ? (ps >> 1) : ps;     // mode 0: 0 = (x, y), 1 = (z, row)
+        const int h = J.mode == 0 ? (ps & 1) : 0;
+        const int r0 = h * half, r1 = J.mode == 0 ? min(N, r0 + half) : N;
+        __syncthreads();  // (the sort's arrays / the previous pass are consumed)
+        for (int sub = 0; sub < (J.mode == 0 ? 2 : 1); ++sub) {  // mode 0: the two words
+            const double *col = J.mode == 0 ? (f == 0 ? (sub ? J.y : J.x) : (sub ? nullptr : J.z))
+                                            : (ps == 0 ? J.x : (ps == 1 ? J.y : (ps == 2 ? J.z : nullptr)));
+            double v[PS_R];
+#pragma unroll
+            for (int u = 0; u < PS_R; ++u) {
+                const int i = t + u * PS_T;
+                v[u] = (pos[u] >= 0 && col) ? col[b + i] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < PS_R; ++u) {
+                if (pos[u] < 0 || pos[u] < r0 || pos[u] >= r1) continue;
+                const uint32_t row = (uint32_t)(b + t + u * PS_T);
+                if (J.mode == 0) {
+                    // (f 1: z -- 0 for 2-D layers, v = 0 -- then the row as the index word)
+                    sd[2 * (pos[u] - r0) + sub] = (f == 1 && sub == 1) ? __longlong_as_double((long long)row) : v[u];
+                } else if (ps == 3) {
+                    su[pos[u]] = row;
+                } else {
+                    sd[pos[u]] = v[u];
+                }
+            }
+        }
+        __syncthreads();
+        if (J.mode == 0) {
+            for (int r = r0 + t; r < r1; r += PS_T)
+                *reinterpret_cast<double2 *>(reinterpret_cast<double *>(J.pts + b + r) + 2 * f) =
+                    make_double2(sd[2 * (r - r0)], sd[2 * (r - r0) + 1]);
+        } else {
+            double *dst = ps == 0 ? J.wx : (ps == 1 ? J.wy : J.wz);
+            for (int r = t; r < N; r += PS_T) {
+                if (ps == 3) J.worig[b + r] = su[r];
+                else dst[b + r] = sd[r];
+            }
+        }
+    }
+}
+
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
@@ -1096,6 +1254,19 @@ hipError_t launch_batch_fit_ctr_zero(unsigned *ctr, int n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_zero_u32_atomic, dim3((unsigned)std::min(1024, (n + 255) / 256)), dim3(256), 0,
                        s, ctr, n);
+    return hipGetLastError();
+}
+
+bool plot_sort_fits(int64_t max_points, int64_t max_keys) {
+    return max_points <= PS_MAXN && max_keys < PS_MAXK;  // (key nk: the plot's end)
+}
+
+hipError_t launch_plot_sort(const PlotSortJob &a, const PlotSortJob *b, const PlotGrid *grids,
+                            int nplots, hipStream_t s) {
+    if (nplots <= 0) return hipSuccess;
+    const PlotSortJob bb = b ? *b : a;
+    hipLaunchKernelGGL(k_plot_sort, dim3((unsigned)nplots * (b ? 2u : 1u)), dim3(PS_T), 0, s, a, bb,
+                       grids, nplots);
     return hipGetLastError();
 }
 

@@ -75,15 +75,21 @@ __device__ __forceinline__ uint32_t bs_key(double x, double y, const BSortGeom &
     const BSortGeom g = J.g;                                   \
     const BSortPlan p = J.p;
 
+// The slices of k_bs_count / k_bs_scatter are dealt XCD-aware (slice = xcd_block of the
+// workgroup within its job; each job's workgroups start at a multiple of 8): an XCD's
+// slices are one contiguous range of points, so when the keys follow the point order (the
+// batch: plot-major) its scattered records fill whole lines of its own L2.
 __global__ __launch_bounds__(BT) void k_bs_count(BSPair P) {
     BS_PICK(P.split[0])
+    if (bid >= p.nb1) return;  // (the padding of job a's workgroups to a multiple of 8)
+    const int sl = (int)xcd_block(bid, p.nb1);
     const double *x = J.x, *y = J.y;
     const int64_t n = J.n;
     uint32_t *counts = J.counts;
     __shared__ uint32_t h[BMAXB];
     for (int b = threadIdx.x; b < p.nbk; b += BT) h[b] = 0u;
     __syncthreads();
-    const int64_t i0 = (int64_t)bid * p.per, i1 = min(n, i0 + p.per);
+    const int64_t i0 = (int64_t)sl * p.per, i1 = min(n, i0 + p.per);
     constexpr int U = 8;  // points in flight per thread
     for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * BT) {
         double xv[U], yv[U];
@@ -99,7 +105,7 @@ __global__ __launch_bounds__(BT) void k_bs_count(BSPair P) {
                 atomicAdd(&h[bs_key(xv[u], yv[u], g, i + (int64_t)u * BT) >> p.fs], 1u);
     }
     __syncthreads();
-    uint32_t *c = counts + (int64_t)bid * p.nbk;
+    uint32_t *c = counts + (int64_t)sl * p.nbk;
     for (int b = threadIdx.x; b < p.nbk; b += BT) c[b] = h[b];
 }
 
@@ -138,6 +144,8 @@ __global__ __launch_bounds__(1024) void k_bs_colscan(BSPair P) {
 
 __global__ __launch_bounds__(BT) void k_bs_scatter(BSPair P) {
     BS_PICK(P.split[2])
+    if (bid >= p.nb1) return;  // (padding, as k_bs_count)
+    const int sl = (int)xcd_block(bid, p.nb1);
     const double *x = J.x, *y = J.y, *z = J.z;
     const int64_t n = J.n;
     const uint32_t *colpref = J.counts, *totals = J.totals;
@@ -170,14 +178,14 @@ __global__ __launch_bounds__(BT) void k_bs_scatter(BSPair P) {
     for (int j = 0; j < PB; ++j) {
         const int b = threadIdx.x * PB + j;
         if (b < p.nbk) {
-            fill[b] = run + colpref[(int64_t)bid * p.nbk + b];
-            if (bid == 0) base_out[b] = run;
+            fill[b] = run + colpref[(int64_t)sl * p.nbk + b];
+            if (sl == 0) base_out[b] = run;
         }
         run += v[j];
     }
-    if (bid == 0 && threadIdx.x == 0) base_out[p.nbk] = (uint32_t)n;
+    if (sl == 0 && threadIdx.x == 0) base_out[p.nbk] = (uint32_t)n;
     __syncthreads();
-    const int64_t i0 = (int64_t)bid * p.per, i1 = min(n, i0 + p.per);
+    const int64_t i0 = (int64_t)sl * p.per, i1 = min(n, i0 + p.per);
     constexpr int U = 8;  // points in flight per thread (the loop was load-latency bound)
     for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * BT) {
         double xv[U], yv[U], zv[U];
@@ -428,6 +436,8 @@ hipError_t launch_bsort2(const BSJob &a, const BSJob &b, hipStream_t s) {
     int tot[4];
     for (int k = 0; k < 4; ++k) {
         P.split[k] = blocks(a, k);
+        // the slice kernels: job b's workgroups start at a multiple of 8 (XCD-aware slices)
+        if (two && (k == 0 || k == 2)) P.split[k] = (P.split[k] + 7) & ~7;
         tot[k] = P.split[k] + (two ? blocks(b, k) : 0);
     }
     auto lds_of = [](const BSJob &j) {

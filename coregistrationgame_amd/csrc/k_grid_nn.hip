@@ -1511,7 +1511,10 @@ __global__ __launch_bounds__(256) void k_gather_work(const uint32_t *perm, const
 __global__ __launch_bounds__(256) void k_scatter_xy(const uint32_t *worig, const double *wx,
                                                     const double *wy, int64_t n, double *sx,
                                                     double *sy) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // XCD-aware: each XCD takes one contiguous eighth of the work rows, so the caller rows
+    // one region of work rows scatters to (a batch plot's) fill whole lines in one L2
+    // instead of partial lines from every XCD (C4, 10M rows: 250 us with the plain order)
+    const int64_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const uint32_t i = worig[p];
     sx[i] = wx[p];

@@ -196,6 +196,40 @@ def test_batch_c4_size_plots_vs_oracle(oracle, monkeypatch):
         np.testing.assert_array_equal(bits(fw[j][:, 2]), bits(srcs[j][:, 2]))
 
 
+@pytest.mark.parametrize("work", ["1", "0"])
+def test_plot_sort_equals_bucket_sort(work, monkeypatch):
+    """The per-plot LDS sort (k_plot_sort: the batch grid and the batch work order, one
+    workgroup per plot) orders by (key, row) as the two-level bucket sort does, so whole
+    batch runs are bit-identical with either (mixed plot sizes, an empty CHM layer, 2-D
+    plots, duplicated stems sharing cells)."""
+    from coregistrationgame_amd import FractionalICPBatch, synth
+    monkeypatch.setenv("FICP_BATCH_WORK", work)
+    rng = np.random.default_rng(17)
+    srcs, tgts = [], []
+    for p in range(70):
+        n = int(rng.choice([1, 40, 900, 6000, 12000]))
+        m = int(rng.choice([60, 700, 5000, 9000]))  # (grids within one plot-sort workgroup)
+        pl = synth.make_plot(n, m, 0.8, seed=60_000 + p, md=3)
+        s, t = pl.source, pl.target
+        if p % 9 == 4:
+            s, t = s[:, :2], t[:, :2]
+        if p % 11 == 6 and len(t) <= 5000:
+            t = np.concatenate([t, t[: len(t) // 3]])  # duplicated stems: equal keys, rows decide
+        srcs.append(s)
+        tgts.append(t)
+    tgts[3] = tgts[3][:0]
+    out = {}
+    for name, env in (("plot", "1"), ("bucket", "0")):
+        monkeypatch.setenv("FICP_PLOT_SORT", env)
+        b = FractionalICPBatch(srcs, tgts)
+        out[name] = (b.run(trace=True), b.stats, b.k_trace)
+    (fp, sp, kp), (fb, sb, kb) = out["plot"], out["bucket"]
+    for j in range(len(srcs)):
+        np.testing.assert_array_equal(bits(fp[j]), bits(fb[j]), err_msg=str(j))
+        np.testing.assert_array_equal(kp[j], kb[j], err_msg=str(j))
+        assert sp[j]["n_nn_calls"] == sb[j]["n_nn_calls"], j
+
+
 def test_batch_c4_properties():
     """C4 at full size (1024 plots x 10k/10k): every plot undoes its misregistration, the
     per-plot transforms reproduce the moved XY, and stage counters are consistent."""

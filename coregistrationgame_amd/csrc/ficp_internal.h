@@ -401,7 +401,7 @@ __host__ __device__ __forceinline__ int win_start_log(long long n) {
     return v < kWinHMinLog ? kWinHMinLog : (v > 48 ? 48 : v);
 }
 #ifndef FICP_WIN_HMAX_EXTRA
-#define FICP_WIN_HMAX_EXTRA 7  // doublings of the window above its start (big windows from +3)
+#define FICP_WIN_HMAX_EXTRA 4  // doublings of the window above its start (tools/build_variant.sh A/B)
 #endif
 __host__ __device__ __forceinline__ int win_hmax_log(long long n) {
     return win_start_log(n) + FICP_WIN_HMAX_EXTRA;

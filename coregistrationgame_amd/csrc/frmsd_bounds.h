@@ -34,10 +34,41 @@ __device__ __forceinline__ double lo_r(unsigned long long klo) {
 // minimum FRMSD a candidate: 700-2200 rows at C3 whatever the bucket width.)
 constexpr double kMarg = 1e-9;
 
+// log2 for the bounds (round 5): x = 2^e m, m in [sqrt(1/2), sqrt(2)), log2 m = 2 atanh(s) /
+// ln 2 with s = (m - 1) / (m + 1), |s| < 0.1716, the odd series to s^19 (the next term is
+// ~4e-18), s from one reciprocal + a Newton step.  Absolute error ~1e-15 + the rounding of
+// e + log2 m (~1e-13 at |e| ~ 1000), far inside kMarg.  ~25 dependent fp64 operations
+// against ~60 in ocml's double-double log2, whose chains were the longest part of every
+// bounds phase (the one-workgroup bounds of k_sel_bounds, the window tail, k_batch_select).
+__device__ __forceinline__ double fast_log2(double x) {
+    int e;
+    double m = frexp(x, &e);  // m in [0.5, 1)
+    if (m < 0.70710678118654752) {
+        m = m + m;
+        e -= 1;
+    }
+    const double a = m - 1.0, b = m + 1.0;  // (m - 1 exact)
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    const double s = a * r, z = s * s;
+    double P = 1.0 / 19.0;
+    P = fma(P, z, 1.0 / 17.0);
+    P = fma(P, z, 1.0 / 15.0);
+    P = fma(P, z, 1.0 / 13.0);
+    P = fma(P, z, 1.0 / 11.0);
+    P = fma(P, z, 1.0 / 9.0);
+    P = fma(P, z, 1.0 / 7.0);
+    P = fma(P, z, 1.0 / 5.0);
+    P = fma(P, z, 1.0 / 3.0);
+    P = fma(P, z, 1.0);
+    constexpr double k2_ln2 = 2.8853900817779268;  // 2 / ln 2
+    return (double)e + (s * P) * k2_ln2;
+}
+
 __device__ __forceinline__ double lg2(double x) {
     if (!(x > 0.0)) return x == 0.0 ? -INFINITY : NAN;
     if (!(x < INFINITY)) return INFINITY;
-    return log2(x);
+    return fast_log2(x);
 }
 
 __device__ __forceinline__ double h_of(long long k, double S, double p) {

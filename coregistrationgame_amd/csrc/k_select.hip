@@ -171,9 +171,6 @@ struct SelWS {
     double *wr;      //   the fit pair (xs, ys, cx, cy)
     uint32_t *wo;
     double *wp;
-    unsigned *gfc;   // [NFB] big windows: fine bucket counts and fixed-point floor sums of r
-    u64 *gff;        //   (agent-scope atomics; the tail reads and zeroes them)
-    unsigned *wgc;   // [gather blocks] big windows: each workgroup's window rows (its slots)
 };
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
@@ -235,15 +232,12 @@ int64_t carve_bytes(int64_t n, SelWS *w, char *p0) {
     x.wctr = (unsigned *)take(9 * WCTR * 4);
     x.wacc = (u64 *)take(kWinCopies * 32 * 8);
     x.wcnt = (unsigned *)take(kWinCopies * 16 * 4);
-    x.gfc = (unsigned *)take(1024 * 4);
-    x.gff = (u64 *)take(1024 * 8);
-    // the window rows: kWinCopies regions of CAP (appended), or WSB slots per workgroup (big)
-    const int64_t nwr = std::max<int64_t>((int64_t)kWinCopies * CAP, (int64_t)gather_blocks(n) * 256);
+    // the window rows: kWinCopies regions of CAP, appended
+    const int64_t nwr = (int64_t)kWinCopies * CAP;
     x.wk = (u64 *)take(nwr * 8);
     x.wr = (double *)take(nwr * 8);
     x.wo = (uint32_t *)take(nwr * 4);
     x.wp = (double *)take(nwr * 32);
-    x.wgc = (unsigned *)take((int64_t)gather_blocks(n) * 4);
     x.parts = (double *)take((int64_t)gather_blocks(n) * 8);
     x.fparts = (double *)take((int64_t)gather_blocks(n) * 64);
     x.ka = (u64 *)take(nn * 8);
@@ -2278,7 +2272,13 @@ __device__ ScanOut win_scan_small(unsigned c, const FinalIn &in, const u64 *lk, 
         const u64 k = lk[t];
         const uint32_t o = lo[t];
         unsigned rank = 0;
-        for (unsigned j = 0; j < c; ++j) rank += less_ko(lk[j], lo[j], k, o) ? 1u : 0u;
+        // 8 rows' LDS loads in flight at a time (a plain loop waited for each in turn)
+        const unsigned c8 = c & ~7u;
+        for (unsigned j = 0; j < c8; j += 8) {
+#pragma unroll
+            for (unsigned u = 0; u < 8; ++u) rank += less_ko(lk[j + u], lo[j + u], k, o) ? 1u : 0u;
+        }
+        for (unsigned j = c8; j < c; ++j) rank += less_ko(lk[j], lo[j], k, o) ? 1u : 0u;
         pos[rank] = (uint16_t)t;
     }
     __syncthreads();
@@ -2368,26 +2368,13 @@ constexpr int WA_S0 = 2;    // 3 digits: sum of r below the window, grid 2^(100 
 constexpr int WA_FIT = 5;   // 8 x 3 digits: the fit sums of the rows below it, grid 2^56
 constexpr int WA_KMN = 29;  // max of ~key (the call's smallest finite key)
 constexpr int WA_KMX = 30;  // max of key
+constexpr int WA_SWIN = 31; // the window rows' fixed-point floor sum of r (unit 2^(e_win - fxb))
 constexpr int WACC = 32;
 constexpr int WFIT_G = 56;
 constexpr int WCNT_S = 16;  // append counters 64 B apart (one per XCD copy)
-// Big windows (round 5: lh >= the start + 3, e.g. C3 stage 1's third to fifth calls, whose
-// thresholds move by hundreds to thousands of rows): the window rows also go to NFB fine
-// buckets (counts and fixed-point floor sums of r, agent-scope atomics, one copy), the tail
-// bounds the FRMSD curve over them as k_sel_bounds does over its buckets, and only the rows
-// of the fine buckets that can hold the minimum are sorted.  The rows themselves sit in
-// per-workgroup slots (WSB each, in row order: the rows below the candidates are summed in
-// a fixed order).
-constexpr int NFB_LOG = 10, NFB = 1 << NFB_LOG;
-constexpr int WSB = 256;
-constexpr int WBIG_EXTRA = 3;
-static_assert(WACC == 32 && WCNT_S == 16 && NFB == 1024 && WSB == 256, "carve_bytes' window words");
-__device__ __forceinline__ bool win_big(const WMap &m, int64_t n) { return m.su + 2 >= win_start_log(n) + WBIG_EXTRA; }
-__device__ __forceinline__ int win_fsh(const WMap &m) { return max(0, m.su + 3 - NFB_LOG); }
-// r < 2^e for every row of fine bucket f (keys [wlo + f 2^sh, wlo + (f + 1) 2^sh))
-__device__ __forceinline__ int win_fine_exp(const WMap &m, int sh, int f) {
-    const u64 d = ((u64)(f + 1) << sh) - 1ULL;
-    const u64 khi = d > m.whi - 1ULL - m.wlo ? m.whi - 1ULL : m.wlo + d;
+static_assert(WACC == 32 && WCNT_S == 16, "carve_bytes' window words");
+// r < 2^e for every row with a key <= khi (win_bucket_exp's rule)
+__device__ __forceinline__ int win_key_exp(u64 khi) {
     if (!(khi >> 63)) return 0;
     const int ex = (int)((khi >> 52) & 0x7ffULL);
     return min(2 * ex - 2044, 1024);
@@ -2427,8 +2414,7 @@ __device__ unsigned long long g_winp[8];
 
 // The window path's decision (k_sel_win's last workgroup): the accumulators, the coarse
 // buckets and the append counters (each read and zeroed), the window rows, the bounds.
-// Big windows: also the fine buckets and the per-workgroup slot counts (nwb workgroups).
-__device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap &m0, double lamv,
+__device__ __forceinline__ void win_tail(SelWS w, int64_t n, const WMap &m0, double lamv,
                                          IterState *st, const LoopCtl &lc, int *host_flag,
                                          const FitSrc &fs, int force_retry, Scr &scr) {
     const int t = threadIdx.x;
@@ -2436,7 +2422,6 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     unsigned long long wt_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // (phase stamps, FICP_WIN_PROF)
 #endif
     WINP_T(0);
-    const bool big = win_big(m0, n);
     __shared__ __align__(16) unsigned char sm[W_SMEM];
     __shared__ IterState s_st;
     __shared__ double s_fit[8];
@@ -2444,10 +2429,10 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     __shared__ u64 s_acc[kWinCopies * WACC];
     __shared__ unsigned s_wc[kWinCopies + 1];
     using LY = LdsLay<CAP, true>;
-    unsigned *s_off = (unsigned *)(sm + LY::BC);  // big: [nwb + 1] slot offsets (the sort's bin area)
-    static_assert(2 * NSB >= W_MAXWG + 1, "workgroup offsets in the bin area");
-    // one round of exchanges and loads: the coarse buckets, the accumulators, the append
-    // counters; big windows: the fine buckets and the per-workgroup slot counts
+    // small windows (<= SMALL_C rows): the rows' fit pairs, also in the bin area (no bins)
+    double4 *lpair = (double4 *)(sm + LY::BC);
+    static_assert(SMALL_C * 32 <= 2 * NSB * 4, "the window pairs in the bin area");
+    // one round of exchanges: the coarse buckets, the accumulators, the append counters
     unsigned cc = 0;
     u64 cf = 0;
     if (t < NCB) {
@@ -2472,24 +2457,6 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
                              ? __hip_atomic_exchange(&w.wcnt[(t - (HT - kWinCopies)) * WCNT_S], 0u,
                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                              : 0u;
-    static_assert(NFB == 2 * HT, "two fine buckets per thread");
-    unsigned fcn[2] = {0u, 0u};
-    u64 ffx[2] = {0ULL, 0ULL};
-    const int G = (nwb + HT - 1) / HT;  // big: slot counts per thread (a contiguous run)
-    const int g0 = min(nwb, t * G), g1 = min(nwb, g0 + G);
-    long long loc = 0;
-    if (big) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            fcn[j] = __hip_atomic_exchange(&w.gfc[2 * t + j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ffx[j] = __hip_atomic_exchange(&w.gff[2 * t + j], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        for (int g = g0; g < g1; ++g) {
-            const unsigned c = __hip_atomic_load(&w.wgc[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_off[g] = c;
-            loc += c;
-        }
-    }
     constexpr int SW = (int)(sizeof(IterState) / 4);
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
     if (t < kWinCopies * WACC) s_acc[t] = av;
@@ -2506,7 +2473,7 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
         }
         s_tot[t] = v;
     }
-    if (t == WACC && !big) {  // the append counters' prefix (region q: rows [s_wc[q], s_wc[q + 1]))
+    if (t == WACC) {  // the append counters' prefix (region q: rows [s_wc[q], s_wc[q + 1]))
         unsigned run = 0;
         bool over = false;
         for (int q = 0; q < kWinCopies; ++q) {
@@ -2517,43 +2484,36 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
         }
         s_wc[kWinCopies] = over ? (unsigned)(CAP + 1) : run;
     }
-    long long Wt = 0;
-    if (big) {  // the slot offsets (exclusive scan of the counts, workgroup order)
-        long long tot;
-        long long off = blk_excl_scan_ll(loc, scr, tot);  // (its barriers: s_off, s_tot read)
-        for (int g = g0; g < g1; ++g) {
-            const unsigned c = s_off[g];
-            s_off[g] = (unsigned)off;
-            off += c;
-        }
-        if (t == 0) s_off[nwb] = (unsigned)tot;
-        Wt = tot;
-    }
     __syncthreads();
-    if (!big) Wt = (long long)s_wc[kWinCopies];
+    const long long Wt = (long long)s_wc[kWinCopies];  // (a region past CAP: the launch fails)
     const long long K0 = (long long)s_tot[WA_BEL];
     const long long bad = (long long)s_tot[WA_BAD];
     const int gs0 = win_s0_grid(m0);
     const double S0 = wfx_total(s_tot[WA_S0], s_tot[WA_S0 + 1], s_tot[WA_S0 + 2], gs0);
+    // a lower bound of the window rows' sum (their floor sums: order-free, so the coarse
+    // bounds above the window need not wait for the sorted scan)
+    const double Swin_lo = ldexp((double)s_tot[WA_SWIN], win_key_exp(m0.whi - 1ULL) - m0.fxb);
     WMap m = m0;  // with the call's key range (the lowest coarse bucket's lowest r)
     m.kmin = ~s_tot[WA_KMN];
     m.kmax = s_tot[WA_KMX];
     if (t < 8)
         s_fit[t] = wfx_total(s_tot[WA_FIT + 3 * t], s_tot[WA_FIT + 3 * t + 1], s_tot[WA_FIT + 3 * t + 2], WFIT_G);
-    bool fail = bad != 0 || Wt <= 0 || (!big && Wt > CAP);
+    bool fail = bad != 0 || Wt <= 0 || Wt > CAP;
     const double p = 2.0 * lamv + 1.0;
     u64 *lk = (u64 *)(sm + LY::K);
     double *lr = (double *)(sm + LY::R);
     uint32_t *lo = (uint32_t *)(sm + LY::O);
     uint32_t *lrow = (uint32_t *)(sm + W_ROW);  // where each LDS row's pair lies (slot)
     constexpr int EU = CAP / HT;
-    // small windows: every window row is a candidate; their loads first, the coarse
-    // bounds while they are in flight
+    const bool pin = Wt <= SMALL_C;  // the small windows' pairs go to LDS
+    // every window row is a candidate; their loads first (the pairs of the first HT rows
+    // too), the coarse bounds while they are in flight
     uint32_t sl[EU];
     u64 vk[EU];
     double vr[EU];
     uint32_t vo[EU];
-    if (!fail && !big) {
+    double4 vp = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (!fail) {
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const int e = t + u * HT;
@@ -2565,31 +2525,33 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
                 vk[u] = __hip_atomic_load(&w.wk[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 vr[u] = __hip_atomic_load(&w.wr[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 vo[u] = __hip_atomic_load(&w.wo[sl[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (u == 0 && pin && fs.on) {
+                    const double *pp = w.wp + 4 * (int64_t)sl[0];
+                    vp = make_double4(win_ld(pp), win_ld(pp + 1), win_ld(pp + 2), win_ld(pp + 3));
+                }
             }
         }
     }
-    // each coarse bucket below the window: its lower bound of h (k_sel_bounds' block_lb):
-    // rows before it = the buckets before it; lower sum = their fixed-point brackets.  The
-    // buckets above the window need the window's sum: after the scan.
+    // every coarse bucket's lower bound of h (k_sel_bounds' block_lb): rows before it = the
+    // buckets before it (+ the window's rows above it); lower sum = the fixed-point brackets
+    // before it (+ S0 and the window's floor sum above it)
     double lbv = INFINITY;
     bool lbok = true;
-    const int eb = t < NCB ? win_bucket_exp(m, t) : 0;
-    const double lo_sum = (t < NCB && eb < 1024) ? ldexp((double)cf, eb - m.fxb) : 0.0;  // (exact)
-    long long C0 = t < NCB ? (long long)cc : 0;
-    double Pb = (t < NCS) ? lo_sum : 0.0;
-    double Pa = (t >= NCS && t < NCB) ? lo_sum : 0.0;
-    blk_excl_scan3(C0, Pb, Pa, scr);
-    if (t < NCS) {
+    {
+        const int eb = t < NCB ? win_bucket_exp(m, t) : 0;
+        const double lo_sum = (t < NCB && eb < 1024) ? ldexp((double)cf, eb - m.fxb) : 0.0;  // (exact)
+        long long C0 = t < NCB ? (long long)cc : 0;
+        double Pb = (t < NCS) ? lo_sum : 0.0;
+        double Pa = (t >= NCS && t < NCB) ? lo_sum : 0.0;
+        blk_excl_scan3(C0, Pb, Pa, scr);
         if (t == NCS - 1 && C0 + (long long)cc != K0) lbok = false;  // (a row lost: never)
-        if (cc) lbv = block_lb(C0, (long long)cc, Pb, lo_r(win_bucket_lo(m, t)), p);
+        if (t < NCB && cc) {
+            const bool below = t < NCS;
+            lbv = block_lb(below ? C0 : C0 + Wt, (long long)cc, below ? Pb : (S0 + Swin_lo) + Pa,
+                           lo_r(win_bucket_lo(m, t)), p);
+        }
     }
-    long long Kb = 0;   // window rows below the candidates (all selected)
-    double Sb = 0.0;    // their sum of r (a fixed order)
-    double Sa = 0.0;    // the window rows above the candidates: their sum of r
-    long long Wc = Wt;  // candidates (window rows sorted and scanned)
-    __shared__ int s_fb[2];
-    __shared__ unsigned s_nc;
-    if (!fail && !big) {
+    if (!fail) {
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const int e = t + u * HT;
@@ -2598,143 +2560,34 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
                 lr[e] = vr[u];
                 lo[e] = vo[u];
                 lrow[e] = sl[u];
+                if (u == 0 && pin) lpair[e] = vp;
             }
         }
-    }
-    if (!fail && big) {
-        // the fine buckets' bounds (k_sel_bounds' rule): U = the smallest upper bound of h at
-        // a fine bucket's end; the candidates = the fine buckets whose lower bound is <= U
-        const int fsh = win_fsh(m0);
-        long long fc = (long long)fcn[0] + (long long)fcn[1];
-        double flo[2], fun[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int ef = win_fine_exp(m0, fsh, 2 * t + j);
-            flo[j] = ef < 1024 ? ldexp((double)ffx[j], ef - m0.fxb) : INFINITY;
-            fun[j] = ef < 1024 ? ldexp(1.0, ef - m0.fxb) : INFINITY;  // one floor unit
-        }
-        double plo = flo[0] + flo[1];
-        double phi = (flo[0] + (double)fcn[0] * fun[0]) + (flo[1] + (double)fcn[1] * fun[1]);
-        blk_excl_scan3(fc, plo, phi, scr);
-        double ub = INFINITY, lbf[2];
-        long long C = K0 + fc;
-        double Pl = S0 + plo, Ph = S0 + phi;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            lbf[j] = INFINITY;
-            if (fcn[j]) {
-                const u64 klo = m0.wlo + ((u64)(2 * t + j) << fsh);
-                lbf[j] = block_lb(C, (long long)fcn[j], Pl, lo_r(klo), p);
-                C += fcn[j];
-                Pl = Pl + flo[j];
-                Ph = Ph + (flo[j] + (double)fcn[j] * fun[j]);
-                ub = fmin(ub, h_of(C, Ph, p) + kMarg);
-            }
-        }
-        const double Uf = blk_min_d(ub, scr);
-        int f0 = NFB, f1 = -1;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (fcn[j] && !(lbf[j] > Uf)) {
-                f0 = min(f0, 2 * t + j);
-                f1 = max(f1, 2 * t + j);
-            }
-        const long long fmn = blk_min_ll(f0, scr), fmx = blk_max_ll(f1, scr);
-        if (t == 0) {
-            s_fb[0] = (int)fmn;
-            s_fb[1] = (int)fmx;
-            s_nc = 0u;
-        }
-        __syncthreads();
-        const int fb0 = s_fb[0], fb1 = s_fb[1];
-        fail = fb1 < fb0;
-        // the window rows in slot order (thread t: rows t, t + HT, ...; the same order in
-        // both passes below): below the candidates -> counted and summed, inside -> LDS
-        // (any order: they are sorted), above -> summed (the coarse bounds above the window)
-        long long kb = 0;
-        double sb = 0.0, sa = 0.0;
-        double cf8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (!fail) {
-            for (long long e0 = t; e0 < Wt; e0 += 4 * HT) {
-                uint32_t s4[4];
-                u64 k4[4];
-                double r4[4];
-                uint32_t o4[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const long long e = e0 + (long long)u * HT;
-                    const int ee = (int)(e < Wt ? e : e0);
-                    int lo_g = 0, hi_g = nwb;  // the last workgroup whose first slot index is <= ee
-                    while (hi_g - lo_g > 1) {
-                        const int mid = (lo_g + hi_g) >> 1;
-                        if ((int)s_off[mid] <= ee) lo_g = mid;
-                        else hi_g = mid;
-                    }
-                    s4[u] = (uint32_t)(lo_g * WSB + (ee - (int)s_off[lo_g]));
-                    k4[u] = __hip_atomic_load(&w.wk[s4[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    r4[u] = __hip_atomic_load(&w.wr[s4[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    o4[u] = __hip_atomic_load(&w.wo[s4[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const long long e = e0 + (long long)u * HT;
-                    if (e >= Wt) continue;
-                    const int f = (int)((k4[u] - m0.wlo) >> fsh);
-                    if (f < fb0) {
-                        ++kb;
-                        sb = sb + r4[u];
-                        if (fs.on) {  // (agent-scope loads: stored by other workgroups of this launch)
-                            const double *pp = w.wp + 4 * (int64_t)s4[u];
-                            fit_add(cf8, win_ld(pp), win_ld(pp + 1), win_ld(pp + 2), win_ld(pp + 3), fs.px, fs.py);
-                        }
-                    } else if (f <= fb1) {
-                        const unsigned c = atomicAdd(&s_nc, 1u);
-                        if (c < (unsigned)CAP) {
-                            lk[c] = k4[u];
-                            lr[c] = r4[u];
-                            lo[c] = o4[u];
-                            lrow[c] = s4[u];
-                        }
-                    } else {
-                        sa = sa + r4[u];
-                    }
-                }
-            }
-        }
-        // fixed trees over the threads (every thread's rows in a fixed order): the same bits
-        // (the scan's barriers also complete s_nc)
-        (void)blk_excl_scan_ll(kb, scr, Kb);
-        Sb = blk_sum(sb, scr);
-        Sa = blk_sum(sa, scr);
-        if (fs.on) blk_sum8_add(cf8, s_fit, scr);
-        Wc = (long long)s_nc;
-        fail = fail || Wc <= 0 || Wc > CAP;
     }
     __syncthreads();
     WINP_T(2);
     FinalIn in;
     in.N = n;
     in.lam = lamv;
-    in.S0 = S0 + Sb;
-    in.K0 = K0 + Kb;
+    in.S0 = S0;
+    in.K0 = K0;
     in.U = 0.0;
     in.fs = fs;
     in.fsum = s_fit;
     ScanOut rs{INFINITY, 0x7fffffffffffffffLL, 0, 0, 0.0};
     __shared__ u64 s_aux[3];
-    const bool small = Wc <= SMALL_C;  // (its rank loop is O(c) per row: 492 rows took 17.6 us)
+    const bool small = Wt <= SMALL_C;  // (its rank loop is O(c) per row: 492 rows took 17.6 us)
     if (!fail) {
         if (small) {
-            rs = win_scan_small((unsigned)Wc, in, lk, lo, lr, (uint16_t *)(sm + LY::POS), scr, s_aux);
+            rs = win_scan_small((unsigned)Wt, in, lk, lo, lr, (uint16_t *)(sm + LY::POS), scr, s_aux);
         } else {
             const Cand none{nullptr, nullptr, nullptr, nullptr};
-            rs = lds_sort_scan<CAP, true, true>(none, (unsigned)Wc, in.K0, in.S0, in, sm, scr);
+            rs = lds_sort_scan<CAP, true, true>(none, (unsigned)Wt, in.K0, in.S0, in, sm, scr);
         }
         fail = rs.bk == 0x7fffffffffffffffLL;
     }
     WINP_T(3);
-    // the minimum is global: every coarse bucket's lower bound of h exceeds U (the fine
-    // buckets left out have lower bounds above the fine U, itself >= the minimum + kMarg)
+    // the minimum is global: every coarse bucket's lower bound of h exceeds U
     double U = INFINITY;
     if (!fail) {
         // S at the minimum: s_aux (small) or lds_sort_scan's prefix sums by position in lr
@@ -2744,20 +2597,14 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
             s_tko[0] = rs.tk;
             s_tko[1] = (u64)rs.to;
         }
-        // the buckets above the window: the rows before them are the window's and the
-        // coarse buckets' before them (C0 counts the K0 rows below the window), their lower
-        // sum is S0 + the window's sum + the brackets before them above the window
-        if (t >= NCS && t < NCB && cc)
-            lbv = block_lb(C0 + Wt, (long long)cc, ((S0 + Sb) + rs.total + Sa) + Pa,
-                           lo_r(win_bucket_lo(m, t)), p);
     }
     const bool ok = lbok && (lbv > U);  // (empty buckets: lbv = inf)
     fail = fail || blk_max_ll(ok ? 0 : 1, scr) != 0 || force_retry;  // (its barriers publish s_tko)
     WINP_T(4);
 #ifdef FICP_WIN_PROF
     if (fail && t == 0)
-        printf("WINPROF W=%lld Wc=%lld big=%d K0=%lld fail=1 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | acc %llu rows %llu sort %llu bounds %llu (10 ns)\n",
-               Wt, Wc, (int)big, K0, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
+        printf("WINPROF W=%lld K0=%lld fail=1 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | acc %llu rows %llu sort %llu bounds %llu (10 ns)\n",
+               Wt, K0, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
                g_winp[5] - g_winp[4], g_winp[2] - g_winp[5], g_winp[6] - g_winp[2], wt_[0] - g_winp[6],
                wt_[6] - wt_[0], wt_[2] - wt_[6], wt_[3] - wt_[2], wt_[4] - wt_[3]);
 #endif
@@ -2766,14 +2613,19 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
         return;
     }
     // the fit of the selected candidates, in sorted order (positions t, t + HT, ...; a
-    // fixed tree: deterministic), their pairs from the window rows' pair array
+    // fixed tree: deterministic): their pairs from LDS (small windows) or the pair array
     const uint32_t nsel = (uint32_t)(rs.bk - in.K0);
     if (fs.on) {
         const uint16_t *pos = (const uint16_t *)(sm + LY::POS);
         double cf8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (uint32_t q = t; q < nsel; q += HT) {
-            const double *pp = w.wp + 4 * (int64_t)lrow[pos[q]];
-            fit_add(cf8, win_ld(pp), win_ld(pp + 1), win_ld(pp + 2), win_ld(pp + 3), fs.px, fs.py);
+            if (pin) {
+                const double4 v = lpair[pos[q]];
+                fit_add(cf8, v.x, v.y, v.z, v.w, fs.px, fs.py);
+            } else {
+                const double *pp = w.wp + 4 * (int64_t)lrow[pos[q]];
+                fit_add(cf8, win_ld(pp), win_ld(pp + 1), win_ld(pp + 2), win_ld(pp + 3), fs.px, fs.py);
+            }
         }
         blk_sum8_add(cf8, s_fit, scr);
     }
@@ -2800,8 +2652,8 @@ __device__ __forceinline__ void win_tail(SelWS w, int nwb, int64_t n, const WMap
     WINP_T(5);
     // (printed after the last stamp: a device printf is a host round trip)
     if (t == 0)
-        printf("WINPROF W=%lld Wc=%lld big=%d K0=%lld fail=0 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | acc %llu rows %llu sort %llu bounds %llu fit %llu step %llu store %llu (10 ns)\n",
-               Wt, Wc, (int)big, K0, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
+        printf("WINPROF W=%lld K0=%lld fail=0 | b0 load %llu cls %llu red %llu app %llu atom %llu wait %llu -> tail +%llu | acc %llu rows %llu sort %llu bounds %llu fit %llu step %llu store %llu (10 ns)\n",
+               Wt, K0, g_winp[1] - g_winp[0], g_winp[3] - g_winp[1], g_winp[4] - g_winp[3],
                g_winp[5] - g_winp[4], g_winp[2] - g_winp[5], g_winp[6] - g_winp[2], wt_[0] - g_winp[6],
                wt_[6] - wt_[0], wt_[2] - wt_[6], wt_[3] - wt_[2], wt_[4] - wt_[3], wt_[8] - wt_[4],
                wt_[9] - wt_[8], wt_[5] - wt_[9]);
@@ -2874,8 +2726,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
         if (blockIdx.x == 0 && t == 0) win_retry(st, host_flag);
         return;
     }
-    const bool big = win_big(m0, n);  // (uniform)
-    const int fsh = win_fsh(m0);
+    const int ewin = win_key_exp(m0.whi - 1ULL);  // r < 2^ewin in the window
     // an LDS-only barrier: __syncthreads() would also wait for every row's load
     // (vmcnt(0)); this way the rows are classified as their loads land
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -2887,6 +2738,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     double c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     u64 kk[WI];
     unsigned inw = 0;
+    u64 swfx = 0;  // the window rows' floor sum of r (unit 2^(ewin - fxb): an order-free lower bound)
     unsigned *my_cc = s_cc + (lane % WREP) * WRS;
     u64 *my_cf = s_cf + (lane % WREP) * WRS;
 #pragma unroll
@@ -2913,13 +2765,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
                 atomicAdd(&my_cf[b], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL);
             } else if (k < m0.whi) {
                 inw |= 1u << q;
-                if (big) {  // the fine buckets (one copy: window rows spread over NFB words)
-                    const int f = (int)((k - m0.wlo) >> fsh);
-                    const int e = win_fine_exp(m0, fsh, f);
-                    __hip_atomic_fetch_add(&w.gfc[f], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(&w.gff[f], e < 1024 ? (u64)ldexp(v, m0.fxb - e) : 0ULL,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                swfx += ewin < 1024 ? (u64)ldexp(v, m0.fxb - ewin) : 0ULL;
             } else {
                 const int b = NCS + win_cq((k - m0.whi) >> m0.su);
                 const int e = s_ce[b];
@@ -2932,7 +2778,6 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     // the window rows appended to this XCD copy's region (one atomic per wave that has
     // any; the tail orders them by (key, caller index), so the append order is free)
     const int cp = (int)(blockIdx.x % kWinCopies);
-    __shared__ unsigned s_wcb[NWAVE];
     u64 masks[WI];
     unsigned wtot = 0;
 #pragma unroll
@@ -2940,8 +2785,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
         masks[q] = __ballot((inw >> q) & 1u);
         wtot += (unsigned)__popcll(masks[q]);
     }
-    if (lane == 0) s_wcb[wave] = wtot;
-    if (!big) {
+    {
         if (wtot) {  // (uniform per wave)
             unsigned wb = 0;
             if (lane == 0)
@@ -2972,6 +2816,8 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
 #pragma unroll
     for (int e = 0; e < 8; ++e) c8[e] = wave_sum63(c8[e]);
     const u64 cnt = wave_sum63_u64((u64)nbel | ((u64)nbad << 32));
+    const u64 swv = wave_sum63_u64(swfx);
+    __shared__ u64 s_swin[NWAVE];
     u64 pka = ~kmn, pkb = kmx;
     wave_range_reduce(pka, pkb);  // (max of ~kmin and of kmax, lane 63)
     __shared__ u64 s_kr[NWAVE][2];
@@ -2982,39 +2828,10 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
 #pragma unroll
         for (int e = 0; e < 8; ++e) s_red[wave][1 + e] = c8[e];
         s_cnt[wave] = cnt;
+        s_swin[wave] = swv;
     }
     __syncthreads();  // (the LDS atomics, the wave counts and sums are complete)
     WINP_B(4);
-    // big windows: the window rows into this workgroup's WSB slots in row order (wave, row
-    // slot, lane), their count beside them; a workgroup with more than WSB fails the launch
-    unsigned wall = 0;
-    if (big) {
-        unsigned wpos = 0;
-#pragma unroll
-        for (int q = 0; q < NWAVE; ++q) {
-            wpos += q < wave ? s_wcb[q] : 0u;
-            wall += s_wcb[q];
-        }
-        if (t == 0)
-            __hip_atomic_store(&w.wgc[blockIdx.x], min(wall, (unsigned)WSB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (wtot && wall <= (unsigned)WSB) {
-            const u64 lt = (1ULL << lane) - 1ULL;
-#pragma unroll
-            for (int q = 0; q < WI; ++q) {
-                if ((inw >> q) & 1u) {
-                    const int64_t s = (int64_t)blockIdx.x * WSB + wpos + (unsigned)__popcll(masks[q] & lt);
-                    __hip_atomic_store(&w.wk[s], kk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&w.wr[s], rr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&w.wo[s], oo[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&w.wp[4 * s], xs[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&w.wp[4 * s + 1], ys[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&w.wp[4 * s + 2], xt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&w.wp[4 * s + 3], yt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                wpos += (unsigned)__popcll(masks[q]);
-            }
-        }
-    }
     // the coarse buckets first: their atomics complete while the rest is added
     if (t < NCB) {
         unsigned c = 0;
@@ -3032,8 +2849,8 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     }
     // the workgroup's totals into the accumulators (the last wave: wave 0 flushed the
     // buckets): lane 0 the sum of r below (grid 2^g0), lanes 1-8 the fit sums (2^56),
-    // lane 9 the counts, lane 10 the key range
-    if (wave == NWAVE - 1 && lane < 11) {
+    // lane 9 the counts, lane 10 the key range, lane 11 the window rows' floor sum
+    if (wave == NWAVE - 1 && lane < 12) {
         u64 *acc = w.wacc + cp * WACC;
         if (lane < 9) {
             double v = s_red[0][lane];
@@ -3047,11 +2864,14 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
         } else if (lane == 9) {
             u64 cv = 0;
             for (int q = 0; q < NWAVE; ++q) cv += s_cnt[q];
-            if (wall > (unsigned)WSB) cv += 1ULL << 32;  // (big: the slots overflowed)
             if (cv & 0xffffffffULL)
                 __hip_atomic_fetch_add(&acc[WA_BEL], cv & 0xffffffffULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (cv >> 32)
                 __hip_atomic_fetch_add(&acc[WA_BAD], cv >> 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (lane == 11) {
+            u64 sv = 0;
+            for (int q = 0; q < NWAVE; ++q) sv += s_swin[q];
+            if (sv) __hip_atomic_fetch_add(&acc[WA_SWIN], sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             u64 a = s_kr[0][0], b = s_kr[0][1];
             for (int q = 1; q < NWAVE; ++q) {
@@ -3083,7 +2903,7 @@ __global__ __launch_bounds__(HT) void k_sel_win(const double *r, const uint32_t 
     }
     __syncthreads();
     if (!s_last) return;
-    win_tail(w, (int)gridDim.x, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
+    win_tail(w, n, m0, lamv, st, lc, host_flag, fs, force_retry, scr);
 }
 
 __global__ void k_sel_init(SelWS w) {
@@ -3105,10 +2925,6 @@ __global__ void k_sel_init(SelWS w) {
         __hip_atomic_exchange(&w.wacc[b], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int b = threadIdx.x; b < kWinCopies * WCNT_S; b += blockDim.x)
         __hip_atomic_exchange(&w.wcnt[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int b = threadIdx.x; b < NFB; b += blockDim.x) {
-        __hip_atomic_exchange(&w.gfc[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_exchange(&w.gff[b], (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 // ---- distributed selection (source rows split over ranks) -------

@@ -498,10 +498,18 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         for (int q = 0; q < nsub; ++q)
             if (!subs[q].finished) return fail(FICP_EHIP, "batch did not converge within its bound");
     }  // JoinGuard: the sub-streams join c->stream here
-    // the moved XY back into the caller's rows (k_scatter_xy: sx[worig[w]] = wx[w])
-    if (work)
-        HIPCHK(launch_scatter_xy(b.worig.as<uint32_t>(), b.wx.as<double>(), b.wy.as<double>(), n, sx, sy,
-                                 c->stream));
+    // the moved XY back into the caller's rows (sx[worig[w]] = wx[w]): per plot through LDS
+    // when the plots fit one workgroup, else k_scatter_xy
+    if (work) {
+        int64_t max_rows = 0;
+        for (int32_t p = 0; p < nplots; ++p) max_rows = std::max(max_rows, so_h[p + 1] - so_h[p]);
+        if (plot_sort_fits(max_rows, 0))
+            HIPCHK(launch_plot_scatter_xy(b.worig.as<uint32_t>(), b.wx.as<double>(), b.wy.as<double>(),
+                                          b.so.as<int64_t>(), nplots, sx, sy, c->stream));
+        else
+            HIPCHK(launch_scatter_xy(b.worig.as<uint32_t>(), b.wx.as<double>(), b.wy.as<double>(), n, sx,
+                                     sy, c->stream));
+    }
     // one report kernel copies the plot states into coherent pinned memory and raises a
     // flag the host polls (a pageable D2H copy + stream sync left ~40 us of idle device)
     const size_t sbytes = (size_t)nplots * sizeof(PlotState);

@@ -961,6 +961,11 @@ struct PlotSortJob {
     uint32_t *worig;
 };
 bool plot_sort_fits(int64_t max_points, int64_t max_keys);
+// the work order's XY back into caller order, one workgroup per plot (plots that fit the
+// plot sort): sx[worig[w]] = wx[w] within each plot's rows
+hipError_t launch_plot_scatter_xy(const uint32_t *worig, const double *wx, const double *wy,
+                                  const int64_t *off, int nplots, double *sx, double *sy,
+                                  hipStream_t s);
 hipError_t launch_plot_sort(const PlotSortJob &a, const PlotSortJob *b, const PlotGrid *grids,
                             int nplots, hipStream_t s);
 // plot chunks of the batch fit (k_batch_fit) for plots of at most max_rows rows

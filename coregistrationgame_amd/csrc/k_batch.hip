@@ -1195,6 +1195,39 @@ __global__ __launch_bounds__(PS_T) void k_plot_sort(PlotSortJob A, PlotSortJob B
     }
 }
 
+// The batch's moved XY back into the caller's rows, one workgroup per plot: the plot's work
+// rows (caller row worig, wx, wy) read coalesced, each value placed at its caller position in
+// an LDS stage, then written coalesced (k_scatter_xy's scattered 8-B stores: 166 us at C4).
+__global__ __launch_bounds__(PS_T) void k_plot_scatter_xy(const uint32_t *worig, const double *wx,
+                                                          const double *wy, const int64_t *off,
+                                                          double *sx, double *sy) {
+    const int p = blockIdx.x;
+    const int64_t b = off[p], e = off[p + 1];
+    const int N = (int)(e - b);
+    if (N > PS_MAXN) return;  // (the host checks every plot: never)
+    __shared__ double s_v[PS_MAXN];
+    const int t = threadIdx.x;
+    int dst[PS_R];
+    double vx[PS_R], vy[PS_R];
+#pragma unroll
+    for (int u = 0; u < PS_R; ++u) {
+        const int i = t + u * PS_T;
+        const bool in = i < N;
+        dst[u] = in ? (int)(worig[b + i] - (uint32_t)b) : -1;
+        vx[u] = in ? wx[b + i] : 0.0;
+        vy[u] = in ? wy[b + i] : 0.0;
+    }
+    for (int c = 0; c < 2; ++c) {
+        if (c) __syncthreads();  // (the x column is written out)
+#pragma unroll
+        for (int u = 0; u < PS_R; ++u)
+            if (dst[u] >= 0) s_v[dst[u]] = c ? vy[u] : vx[u];
+        __syncthreads();
+        double *out = c ? sy : sx;
+        for (int r = t; r < N; r += PS_T) out[b + r] = s_v[r];
+    }
+}
+
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
@@ -1267,6 +1300,14 @@ hipError_t launch_plot_sort(const PlotSortJob &a, const PlotSortJob *b, const Pl
     const PlotSortJob bb = b ? *b : a;
     hipLaunchKernelGGL(k_plot_sort, dim3((unsigned)nplots * (b ? 2u : 1u)), dim3(PS_T), 0, s, a, bb,
                        grids, nplots);
+    return hipGetLastError();
+}
+
+hipError_t launch_plot_scatter_xy(const uint32_t *worig, const double *wx, const double *wy,
+                                  const int64_t *off, int nplots, double *sx, double *sy,
+                                  hipStream_t s) {
+    if (nplots <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_plot_scatter_xy, dim3((unsigned)nplots), dim3(PS_T), 0, s, worig, wx, wy, off, sx, sy);
     return hipGetLastError();
 }
 

@@ -1811,6 +1811,9 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
     const char *qe = getenv("FICP_BATCH_QPT");
     const char *qm = getenv("FICP_BATCH_QPT_MIN");
     const int64_t qpt_min = qm ? atoll(qm) : (int64_t)2000000;
+    // (the cold call stays on the per-row kernel: through this one, with the batch work
+    // order, C4 measured 1.25M against 1.29M plot-it/s -- its long cold scans want the
+    // parallelism of one query per thread)
     if (!(qe && atoi(qe) == 0) && a.n >= qpt_min && a.warm_c && a.gap && a.cert_block) {
         PlotState *stw = const_cast<PlotState *>(st);
         const dim3 gq(nblk(a.n, 256 * QPT));

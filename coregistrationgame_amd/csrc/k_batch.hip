@@ -1341,7 +1341,8 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
         bs.worig = step->worig;
     }
     // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
-    // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers)
+    // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers; round 5
+    // with 16 cached rows per thread: 131 VGPRs spilled, not run)
     if (max_rows <= (int64_t)ST * RPT)
         hipLaunchKernelGGL((k_batch_select<true, ST, RPT>), dim3(nplots), dim3(ST), 0, s, key, r, so,
                            lambdas, st, ws, bs);

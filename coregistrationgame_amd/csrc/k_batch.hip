@@ -409,10 +409,15 @@ struct BatchStep {
 // thread 0 of plot p's workgroup, its state final for this call: one agent-scope atomic
 // adds (1 << 32) + live; the workgroup that completes the count stores the number of live
 // plots into the host's flag and resets the counter for the next launch (stream-ordered)
-__device__ __forceinline__ void batch_arrive(const BatchStep &bs, int live) {
-    if (!bs.arrive) return;
+// (in two halves: the fused step issues the add before its fit and tests the returned
+// count after it, so the atomic's round trip is off the workgroup's chain)
+__device__ __forceinline__ u64 batch_arrive_add(const BatchStep &bs, int live) {
+    if (!bs.arrive) return 0ULL;
     const u64 add = (1ULL << 32) | (u64)(unsigned)live;
-    const u64 old = __hip_atomic_fetch_add(bs.arrive, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_fetch_add(bs.arrive, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void batch_arrive_last(const BatchStep &bs, u64 old, int live) {
+    if (!bs.arrive) return;
     if ((int)(old >> 32) + 1 == bs.nplots) {
         const int tot = (int)(old & 0xffffffffULL) + live;
         __hip_atomic_exchange(bs.arrive, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -420,15 +425,21 @@ __device__ __forceinline__ void batch_arrive(const BatchStep &bs, int live) {
         __hip_atomic_store(bs.flag, tot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
+__device__ __forceinline__ void batch_arrive(const BatchStep &bs, int live) {
+    batch_arrive_last(bs, batch_arrive_add(bs, live), live);
+}
 
 template <int NW>
-__device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, double frmsd,
-                              u64 tkey, long long trow, int64_t b, int64_t e, const u64 *key,
-                              const BatchStep &bs, double *s8, int *s_flag, int wrows = -1) {
+__device__ void plot_step_fit(PlotState *st, const PlotState *ps, int p, long long k, double frac,
+                              double frmsd, u64 tkey, long long trow, int64_t b, int64_t e,
+                              const u64 *key, const BatchStep &bs, double *s8, int *s_flag,
+                              int wrows = -1) {
     const int t = threadIdx.x;
     constexpr int NT = NW * 64;
+    u64 arr = 0ULL;  // (thread 0) the arrival add's returned word
+    int live = 0;
     if (t == 0) {
-        PlotState s = st[p];
+        PlotState s = *ps;  // (the workgroup's LDS copy, loaded with its rows)
         // the threshold's move since the previous loop-body call (the window's half-width)
         const bool prev = s.phase == PH_LOOP && s.k > 0 && k > 0;
         const u64 mv = prev ? (tkey > s.tkey ? tkey - s.tkey : s.tkey - tkey) : 0ULL;
@@ -449,10 +460,14 @@ __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, do
                   bs.trace ? bs.trace + (int64_t)p * bs.max_trace : nullptr, bs.max_trace);
         s_flag[0] = s.phase == PH_LOOP && s.k > 0;  // a loop body (fit -> apply -> NN) follows
         st[p] = s;
-        batch_arrive(bs, s.phase != PH_DONE ? 1 : 0);
+        live = s.phase != PH_DONE ? 1 : 0;
+        arr = batch_arrive_add(bs, live);
     }
     __syncthreads();
-    if (!s_flag[0]) return;
+    if (!s_flag[0]) {
+        if (t == 0) batch_arrive_last(bs, arr, live);
+        return;
+    }
     const PlotGrid g = bs.grids[p];
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifndef FICP_BFIT_FU
@@ -495,6 +510,7 @@ __device__ void plot_step_fit(PlotState *st, int p, long long k, double frac, do
     }
     fit_solve_T(c, (double)k, g.px, g.py, bs.allow_refl, st[p].T);
     st[p].apply = 1;
+    batch_arrive_last(bs, arr, live);
 }
 
 // every row of the plot with its key and r: CACHED keeps them in registers (RPT per
@@ -541,8 +557,8 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     constexpr bool BSEL_RCACHE = KRC;
     constexpr int SPER = SB / ST;          // buckets per thread in the scans
     constexpr int BMAXACT = ST / SPER;     // active bound chunks evaluated one bucket per lane
-    __shared__ unsigned s_cnt[SB];  // counts, then exclusive bucket starts
-    __shared__ double s_sum[SB];    // sums, then per-bucket fill counters (as unsigned)
+    __shared__ unsigned s_cnt[SB];  // exclusive bucket starts
+    __shared__ double s_sum[SB];    // (count, sum) words, then per-bucket fill counters (as unsigned)
     __shared__ SelRed<ST / 64> red;
     __shared__ double s_fit8[8 * (ST / 64)];
     __shared__ int s_fitflag[1];
@@ -565,6 +581,12 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
         if (t == 0) batch_arrive(bs, 0);
         return;
     }
+    // the plot's state for the step (thread 0, plot_step_fit), loaded with the rows: a load
+    // there was one more round trip on the workgroup's chain
+    __shared__ PlotState s_ps;
+    constexpr int PSW = (int)(sizeof(PlotState) / 4);
+    static_assert(PSW <= KST, "one state word per thread");
+    if (t < PSW) reinterpret_cast<uint32_t *>(&s_ps)[t] = reinterpret_cast<const uint32_t *>(st + p)[t];
 #ifdef FICP_BSEL_PROF
     long long bt_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -601,7 +623,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     blk_max2_sum(amin, kmax, nfin, red);
     if (nfin == 0) {  // every distance inf / NaN: the reference keeps (0.0, 0)
         if (bs.fuse) {
-            plot_step_fit<ST / 64>(st, p, 0, 0.0, INFINITY, 0, 0, b, e, key, bs, s_fit8, s_fitflag);
+            plot_step_fit<ST / 64>(st, &s_ps, p, 0, 0.0, INFINITY, 0, 0, b, e, key, bs, s_fit8, s_fitflag);
         } else if (t == 0) {
             st[p].k = 0;
             st[p].frac = 0.0;
@@ -617,23 +639,24 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     // the split between S_base and the window's scan).  r < 2^e1 for every finite row
     // (d <= dmax, d = sqrt(r) rounded), so nfin rows fit in 62 bits; a bucket's true sum
     // lies in [lo, lo + count) units.
+    // Each bucket is one u64 LDS word: its count in the top HB_CB bits, its sum in the low
+    // HB_SB (one atomic per row instead of two): nfin < 2^15 rows below 2^HB_SB units.
     const double dmax = __longlong_as_double((long long)(kmax & 0x7fffffffffffffffULL));
     const int e1 = dmax > 0.0 ? 2 * (ilogb(dmax) + 1) : 0;
-    const int Lq = e1 - (62 - fb::bits_of((u64)nfin));
+    constexpr int HB_SB = 49;
+    constexpr u64 HB_SM = (1ULL << HB_SB) - 1ULL;
+    static_assert(KST * KRPT < (1 << (64 - HB_SB)), "bucket counts in the top bits");
+    const int Lq = e1 - (HB_SB - fb::bits_of((u64)nfin));
     u64 *s_fx = reinterpret_cast<u64 *>(s_sum);
     BSEL_T(1);
     // 2. histogram
 #pragma unroll
-    for (int j = 0; j < SPER; ++j) {
-        s_cnt[t * SPER + j] = 0u;
-        s_fx[t * SPER + j] = 0ULL;
-    }
+    for (int j = 0; j < SPER; ++j) s_fx[t * SPER + j] = 0ULL;
     if (t == 0) s_nact = 0;
     __syncthreads();
     SEL_ROWS(if (rv < INFINITY) {
         const int bk = (int)((kk - kmin) >> sh);
-        atomicAdd(&s_cnt[bk], 1u);
-        atomicAdd(&s_fx[bk], fx_floor(rv, Lq));
+        atomicAdd(&s_fx[bk], (1ULL << HB_SB) | fx_floor(rv, Lq));
     })
     __syncthreads();
     BSEL_T(2);
@@ -645,8 +668,9 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     double ts = 0.0;
 #pragma unroll
     for (int j = 0; j < SPER; ++j) {
-        c[j] = s_cnt[t * SPER + j];
-        sm[j] = ldexp((double)s_fx[t * SPER + j], Lq);
+        const u64 hv = s_fx[t * SPER + j];
+        c[j] = (unsigned)(hv >> HB_SB);
+        sm[j] = ldexp((double)(hv & HB_SM), Lq);
         tc += c[j];
         ts = ts + sm[j];
     }
@@ -694,14 +718,15 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
         const int q = t;
         const bool has = q < nact * SPER;
         const int bk = has ? s_act[q / SPER] * SPER + (q % SPER) : 0;
-        const unsigned cq = has ? s_cnt[bk] : 0u;
+        const u64 hq = has ? s_fx[bk] : 0ULL;
+        const unsigned cq = (unsigned)(hq >> HB_SB);
         const long long C0 = has ? s_eC[q] : 0;
         const double P0 = has ? s_eP[q] : 0.0;
         // the same additions in the same order as the chunk walk: same bits; the bucket's
         // end value and its lower bound in one round of independent log2
         double lb = INFINITY;
         if (cq) {
-            U = fb::h_of(C0 + cq, (P0 + ldexp((double)s_fx[bk], Lq)) + (double)(C0 + cq) * unit, pe) +
+            U = fb::h_of(C0 + cq, (P0 + ldexp((double)(hq & HB_SM), Lq)) + (double)(C0 + cq) * unit, pe) +
                 fb::kMarg;
             lb = fb::block_lb(C0, cq, P0, fb::lo_r(kmin + ((u64)bk << sh)), pe);
         }
@@ -845,7 +870,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
 #endif
     if (bs.fuse) {
         const bool none = bk == 0x7fffffffffffffffLL;  // every FRMSD NaN: (0.0, 0)
-        plot_step_fit<ST / 64>(st, p, none ? 0 : bk, none ? 0.0 : (double)bk / (double)N,
+        plot_step_fit<ST / 64>(st, &s_ps, p, none ? 0 : bk, none ? 0.0 : (double)bk / (double)N,
                                none ? INFINITY : bf, none ? 0ULL : sk[bk - K0 - 1],
                                none ? 0LL : (long long)srw[bk - K0 - 1], b, e, key, bs, s_fit8,
                                s_fitflag);

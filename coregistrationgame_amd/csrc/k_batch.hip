@@ -429,11 +429,14 @@ __device__ __forceinline__ void batch_arrive(const BatchStep &bs, int live) {
     batch_arrive_last(bs, batch_arrive_add(bs, live), live);
 }
 
-template <int NW>
-__device__ void plot_step_fit(PlotState *st, const PlotState *ps, int p, long long k, double frac,
-                              double frmsd, u64 tkey, long long trow, int64_t b, int64_t e,
-                              const u64 *key, const BatchStep &bs, double *s8, int *s_flag,
-                              int wrows = -1) {
+// KR > 1: the caller's registers hold the keys of rows b + t + q NT (q < KR; ~0 past the
+// plot), so the fit loads only the pairs, FU rows at a time
+template <int NW, int KR>
+__device__ __forceinline__ void plot_step_fit(PlotState *st, const PlotState *ps, int p, long long k,
+                                              double frac, double frmsd, u64 tkey, long long trow,
+                                              int64_t b, int64_t e, const u64 *key, const u64 (&kc)[KR],
+                                              const BatchStep &bs, double *s8, int *s_flag,
+                                              int wrows = -1, long long *pt = nullptr) {
     const int t = threadIdx.x;
     constexpr int NT = NW * 64;
     u64 arr = 0ULL;  // (thread 0) the arrival add's returned word
@@ -464,6 +467,7 @@ __device__ void plot_step_fit(PlotState *st, const PlotState *ps, int p, long lo
         arr = batch_arrive_add(bs, live);
     }
     __syncthreads();
+    if (pt && t == 0) pt[13] = wall_clock64();  // (FICP_BSEL_PROF)
     if (!s_flag[0]) {
         if (t == 0) batch_arrive_last(bs, arr, live);
         return;
@@ -473,6 +477,35 @@ __device__ void plot_step_fit(PlotState *st, const PlotState *ps, int p, long lo
 #ifndef FICP_BFIT_FU
 #define FICP_BFIT_FU 8
 #endif
+    // (the tie at the threshold key: the caller's row, loaded only then)
+    auto sel = [&](u64 kk, int64_t i) {
+        return kk < tkey || (kk == tkey && (bs.worig ? (long long)bs.worig[i] : i) <= trow);
+    };
+    if constexpr (KR > 1) {
+        // cached keys: 10 rows' pairs in flight per thread (C4's 10k-row plots: two round
+        // trips, the key-loading loop below took three), the rows in the same order
+        constexpr int FK = 10;
+#pragma unroll
+        for (int q0 = 0; q0 < KR; q0 += FK) {
+            if (b + t + (int64_t)q0 * NT >= e) break;
+            double xs[FK], ys[FK], xt[FK], yt[FK];
+#pragma unroll
+            for (int u = 0; u < FK; ++u) {
+                const int64_t i = b + t + (int64_t)(q0 + u) * NT;
+                const bool in = q0 + u < KR && i < e;
+                xs[u] = in ? bs.sx[i] : 0.0;
+                ys[u] = in ? bs.sy[i] : 0.0;
+                xt[u] = in ? bs.cx[i] : 0.0;
+                yt[u] = in ? bs.cy[i] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < FK; ++u) {
+                const int64_t i = b + t + (int64_t)(q0 + u) * NT;
+                if (q0 + u < KR && i < e && sel(kc[q0 + u < KR ? q0 + u : 0], i))
+                    fit_add(c, xs[u], ys[u], xt[u], yt[u], g.px, g.py);
+            }
+        }
+    } else {
     constexpr int FU = FICP_BFIT_FU;  // rows in flight per thread (every load before its predicate)
     for (int64_t i0 = b + t; i0 < e; i0 += (int64_t)FU * NT) {
         u64 kv[FU];
@@ -490,11 +523,11 @@ __device__ void plot_step_fit(PlotState *st, const PlotState *ps, int p, long lo
 #pragma unroll
         for (int u = 0; u < FU; ++u) {
             const int64_t i = i0 + (int64_t)u * NT;
-            // (the tie at the threshold key: the caller's row, loaded only then)
-            if (i < e && (kv[u] < tkey || (kv[u] == tkey && (bs.worig ? (long long)bs.worig[i] : i) <= trow)))
-                fit_add(c, xs[u], ys[u], xt[u], yt[u], g.px, g.py);
+            if (i < e && sel(kv[u], i)) fit_add(c, xs[u], ys[u], xt[u], yt[u], g.px, g.py);
         }
     }
+    }
+    if (pt && t == 0) pt[14] = wall_clock64();
 #pragma unroll
     for (int q = 0; q < 8; ++q) c[q] = wave_sum63(c[q]);
     if ((t & 63) == 63)
@@ -511,6 +544,11 @@ __device__ void plot_step_fit(PlotState *st, const PlotState *ps, int p, long lo
     fit_solve_T(c, (double)k, g.px, g.py, bs.allow_refl, st[p].T);
     st[p].apply = 1;
     batch_arrive_last(bs, arr, live);
+    if (pt) {
+        pt[15] = wall_clock64();
+        printf("BSELF p=%d pre %lld sel %lld step %lld fit %lld solve %lld (10 ns)\n", p, pt[0] - pt[12],
+               pt[7] - pt[0], pt[13] - pt[7], pt[14] - pt[13], pt[15] - pt[14]);
+    }
 }
 
 // every row of the plot with its key and r: CACHED keeps them in registers (RPT per
@@ -572,6 +610,9 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     __shared__ double s_eP[BMAXACT * SPER];      // sum of r before it
     const int p = blockIdx.x;
     const int t = threadIdx.x;
+#ifdef FICP_BSEL_PROF
+    const long long t_entry = wall_clock64();
+#endif
     // the phase, the stage and the plot's row range load together (one latency, not two)
     const int ph = st[p].phase, stg = st[p].stage, s_it = st[p].it, s_wfl = st[p].wfloor;
     const long long s_kprev = st[p].k;
@@ -589,6 +630,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     if (t < PSW) reinterpret_cast<uint32_t *>(&s_ps)[t] = reinterpret_cast<const uint32_t *>(st + p)[t];
 #ifdef FICP_BSEL_PROF
     long long bt_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    __shared__ long long s_bt[16];
 #endif
     const double lam = lams[stg];
     const double pe = 2.0 * lam + 1.0;
@@ -623,7 +665,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     blk_max2_sum(amin, kmax, nfin, red);
     if (nfin == 0) {  // every distance inf / NaN: the reference keeps (0.0, 0)
         if (bs.fuse) {
-            plot_step_fit<ST / 64>(st, &s_ps, p, 0, 0.0, INFINITY, 0, 0, b, e, key, bs, s_fit8, s_fitflag);
+            plot_step_fit<ST / 64>(st, &s_ps, p, 0, 0.0, INFINITY, 0, 0, b, e, key, kc, bs, s_fit8, s_fitflag);
         } else if (t == 0) {
             st[p].k = 0;
             st[p].frac = 0.0;
@@ -868,12 +910,20 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
                bt_[6] - bt_[5], bt_[7] - bt_[6], bt_[8] - bt_[2], bt_[9] - bt_[8], bt_[10] - bt_[9],
                bt_[11] - bt_[10], bt_[3] - bt_[11]);
 #endif
+    long long *pt = nullptr;
+#ifdef FICP_BSEL_PROF
+    if (t == 0) {
+        for (int q = 0; q < 12; ++q) s_bt[q] = bt_[q];
+        s_bt[12] = t_entry;
+    }
+    if ((p % 97) == 5) pt = s_bt;
+#endif
     if (bs.fuse) {
         const bool none = bk == 0x7fffffffffffffffLL;  // every FRMSD NaN: (0.0, 0)
         plot_step_fit<ST / 64>(st, &s_ps, p, none ? 0 : bk, none ? 0.0 : (double)bk / (double)N,
                                none ? INFINITY : bf, none ? 0ULL : sk[bk - K0 - 1],
-                               none ? 0LL : (long long)srw[bk - K0 - 1], b, e, key, bs, s_fit8,
-                               s_fitflag);
+                               none ? 0LL : (long long)srw[bk - K0 - 1], b, e, key, kc, bs, s_fit8,
+                               s_fitflag, -1, pt);
         return;
     }
     if (t == 0) {

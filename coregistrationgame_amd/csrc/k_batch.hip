@@ -220,29 +220,6 @@ __device__ __forceinline__ void blk_max2_sum(u64 &a, u64 &b, unsigned &c, SelRed
     __syncthreads();
 }
 
-// {min lo, max hi} over the block
-template <int NW>
-__device__ __forceinline__ void blk_minmax_ll(long long &lo, long long &hi, SelRed<NW> &r) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = min(lo, (long long)__shfl_xor(lo, o, 64));
-        hi = max(hi, (long long)__shfl_xor(hi, o, 64));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        r.l[threadIdx.x >> 6] = lo;
-        r.a[threadIdx.x >> 6] = (u64)hi;
-    }
-    __syncthreads();
-    lo = r.l[0];
-    hi = (long long)r.a[0];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) {
-        lo = min(lo, r.l[w]);
-        hi = max(hi, (long long)r.a[w]);
-    }
-    __syncthreads();
-}
-
 // exclusive scan over the block (thread order) of a count and a sum; fixed schedule
 template <int NW>
 __device__ __forceinline__ void blk_excl_scan2(unsigned &c, double &x, SelRed<NW> &r) {
@@ -566,7 +543,9 @@ __device__ __forceinline__ void plot_step_fit(PlotState *st, const PlotState *ps
         for (int64_t i = b + t; i < e; i += ST) {                                   \
             const u64 kk = key[i];                                                  \
             const double rv = r[i];                                                 \
+            constexpr int q = 0;                                                    \
             (void)i;                                                                \
+            (void)q;                                                                \
             BODY                                                                    \
         }                                                                           \
     }
@@ -637,12 +616,17 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     const long long N = e - b;
     u64 kc[CACHED ? RPT : 1];
     double rc[CACHED && BSEL_RCACHE ? RPT : 1];
+    // the rows' caller rows too when the registers allow (the 20-row form): the window
+    // rows' tie-break words were a dependent load inside the S_base pass (~1.5 us)
+    constexpr bool OCACHE = CACHED && RPT <= 20;
+    uint32_t oc[OCACHE ? RPT : 1];
     if (CACHED) {
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
             const int64_t i = b + t + (int64_t)q * ST;
             kc[q] = i < e ? key[i] : ~0ULL;
             if (BSEL_RCACHE) rc[q] = i < e ? r[i] : INFINITY;
+            if (OCACHE) oc[q] = (i < e && ws.worig) ? ws.worig[i] : (uint32_t)i;
         }
     }
     BSEL_T(0);
@@ -810,7 +794,13 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
             }
         }
     }
-    blk_minmax_ll(bmin, bmax, red);
+    {  // {min bmin, max bmax} as two maxima of non-negative words (DPP, blk_max2_sum)
+        u64 ma = (u64)(SB - bmin), mb = (u64)(bmax + 1);
+        unsigned mc = 0;
+        blk_max2_sum(ma, mb, mc, red);
+        bmin = SB - (long long)ma;
+        bmax = (long long)mb - 1;
+    }
     BSEL_T(11);
     // bucket starts (rows before each bucket) replace the counts; fill counters zeroed
     unsigned *fill = reinterpret_cast<unsigned *>(s_sum);
@@ -847,7 +837,8 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
         } else if (bk <= bmax) {
             const int64_t slot = (int64_t)s_cnt[bk] - K0 + atomicAdd(&fill[bk], 1u);
             wk[slot] = kk;
-            wrw[slot] = ws.worig ? ws.worig[i] : (uint32_t)i;  // (ties: the caller's row)
+            // (ties: the caller's row)
+            wrw[slot] = OCACHE ? oc[q < RPT ? q : 0] : (ws.worig ? ws.worig[i] : (uint32_t)i);
             wr[slot] = rv;
         }
     })

@@ -314,14 +314,18 @@ def test_partitioned_2d_and_tiny_shards(mode):
     np.testing.assert_allclose(out, single, atol=1e-6, rtol=0)
 
 
-def test_batch_large_and_degenerate_plots(oracle):
-    """Plots above the selection kernel's register-cached size (> 16384 trees: every pass
-    re-reads the rows), a plot whose trees sit exactly on stems (all distances 0: one
-    bucket holds the whole plot) and one with many exactly equal distances (a lattice
-    shifted by a fixed offset), vs the oracle run of each plot alone."""
+@pytest.mark.parametrize("sizes", [(20_000, 17_000), (14_000, 10_500), (10_000, 9_000)],
+                         ids=["uncached", "cached32", "cached20"])
+def test_batch_large_and_degenerate_plots(oracle, sizes):
+    """The selection kernel's three forms, picked by the batch's largest plot: above its
+    register-cached size (> 16384 trees: every pass re-reads the rows), 32 cached rows per
+    thread (<= 16384) and 20 (<= 10240, C4's plots); with a plot whose trees sit exactly on
+    stems (all distances 0: one bucket holds the whole plot) and one with many exactly
+    equal distances (a lattice shifted by a fixed offset), vs the oracle run of each plot
+    alone."""
     from coregistrationgame_amd import FractionalICPBatch, synth
     srcs, tgts = [], []
-    for n, seed in ((20_000, 501), (17_000, 502)):
+    for n, seed in zip(sizes, (501, 502)):
         pl = synth.make_plot(n, n, 0.7, seed=seed, md=3)
         srcs.append(pl.source)
         tgts.append(pl.target)

@@ -822,22 +822,42 @@ __device__ __forceinline__ void reduce_tail(const SelWS &w, int b, int bl, unsig
 // chunks of PER consecutive buckets; the per-bucket work (two or four log2 each) runs
 // only for the chunks that can hold the minimum, one bucket per lane (a chunk walked by
 // its own thread serialised ~16 dependent evaluations: ~10 us at C3).
+// an sc1 store (agent scope: written through for another workgroup of the same launch)
+template <class T>
+__device__ __forceinline__ void stc(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int MAXACT = HT / (NB / HT);  // active chunks evaluated one bucket per lane
 // returns the candidate bucket range [b0, b1] packed as (b0 << 16) | b1 (every thread)
 // (kBoundsSkipped when *skip: the launch is a no-op).  Every load that does not depend on
 // another (skip flag, lambda, bucket map, chunk totals) issues before the first wait.
 constexpr unsigned kBoundsSkipped = 0xffffffffu;
+constexpr int BPER = NB / HT;
+// bounds_body's LDS (its caller's: k_sel_bgf lays it over the final's buffer)
+struct BoundsLds {
+    Scr scr;
+    int s_act[MAXACT];
+    int s_nact;
+    long long eC[MAXACT * BPER];  // rows before bucket j of active chunk a
+    double eLo[MAXACT * BPER];    // lower sum before it
+    double eHi[MAXACT * BPER];    // upper sum through it
+    unsigned eN[MAXACT * BPER];   // its count
+};
+// The outputs (b0, b1, kbase, U) are stored sc1 and drained by the closing barrier, so a
+// workgroup of the same launch that saw the published range may read them with sc1 loads
+// (k_sel_bgf's final).
 __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
                                                 const double *lam_dev, const int *skip,
-                                                int fixb, bool reset_ccount = true) {
-    constexpr int PER = NB / HT;
-    __shared__ Scr scr;
-    __shared__ int s_act[MAXACT];
-    __shared__ int s_nact;
-    __shared__ long long eC[MAXACT * PER];  // rows before bucket j of active chunk a
-    __shared__ double eLo[MAXACT * PER];    // lower sum before it
-    __shared__ double eHi[MAXACT * PER];    // upper sum through it
-    __shared__ unsigned eN[MAXACT * PER];   // its count
+                                                int fixb, BoundsLds &L, bool reset_ccount = true) {
+    constexpr int PER = BPER;
+    Scr &scr = L.scr;
+    int *s_act = L.s_act;
+    int &s_nact = L.s_nact;
+    long long *eC = L.eC;
+    double *eLo = L.eLo;
+    double *eHi = L.eHi;
+    unsigned *eN = L.eN;
     const int t = threadIdx.x;
     static_assert(PER == 16, "chunk totals of k_sel_reduce");
     // this thread's chunk of PER consecutive buckets: totals from k_sel_reduce; the
@@ -991,17 +1011,20 @@ __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
     if (bmax < 0) {  // no bucket qualifies (non-finite r): every row is a candidate
         bmin = 0;
         bmax = NB - 1;
-        if (t == 0) w.ctl->kbase = 0;
+        if (t == 0) __hip_atomic_store(&w.ctl->kbase, 0LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if (my_bmin == bmin) {
-        w.ctl->kbase = kb;  // rows in buckets < b0
+        // rows in buckets < b0
+        __hip_atomic_store(&w.ctl->kbase, (long long)kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t == 0) {
-        w.ctl->b0 = (int)bmin;
-        w.ctl->b1 = (int)bmax;
-        w.ctl->U = U;
+        __hip_atomic_store(&w.ctl->b0, (int)bmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&w.ctl->b1, (int)bmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&w.ctl->U, U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (reset_ccount)
             __hip_atomic_exchange(&w.ctl->ccount, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // (every output drained before the caller publishes the range)
     SELPROF(14);
     return ((unsigned)bmin << 16) | (unsigned)bmax;
 }
@@ -1009,7 +1032,8 @@ __device__ __forceinline__ unsigned bounds_body(SelWS w, int64_t N, double lam,
 __global__ __launch_bounds__(HT) void k_sel_bounds(SelWS w, int64_t N, double lam,
                                                    const double *lam_dev, const int *skip,
                                                    int fixb) {
-    bounds_body(w, N, lam, lam_dev, skip, fixb);
+    __shared__ BoundsLds L;
+    bounds_body(w, N, lam, lam_dev, skip, fixb, L);
 }
 
 // gen != 0: the candidate buckets come from block 0 of the same launch (k_sel_bounds_gather),
@@ -1132,15 +1156,16 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
                 const unsigned p = pos + (unsigned)__popcll(masks[q] & lt);
                 if ((int64_t)p >= n) continue;  // the buffers hold n candidates (never hit
                                                 // unless ccount was stale: ERR_SPIN)
-                w.ka[p] = kk[q];
-                w.oa[p] = orig ? orig[i] : (uint32_t)i;
-                w.ra[p] = rr[q];
-                w.pa[p] = (uint32_t)i;
+                // (sc1 stores: k_sel_bgf's final reads them in this launch)
+                stc(w.ka + p, kk[q]);
+                stc(w.oa + p, orig ? orig[i] : (uint32_t)i);
+                stc(w.ra + p, rr[q]);
+                stc(w.pa + p, (uint32_t)i);
                 if (fs.on && p < (unsigned)CAP) {  // the final's pairs, no row lookup
-                    w.fpre[4 * p] = fxs[q];
-                    w.fpre[4 * p + 1] = fys[q];
-                    w.fpre[4 * p + 2] = fxt[q];
-                    w.fpre[4 * p + 3] = fyt[q];
+                    stc(w.fpre + 4 * p, fxs[q]);
+                    stc(w.fpre + 4 * p + 1, fys[q]);
+                    stc(w.fpre + 4 * p + 2, fxt[q]);
+                    stc(w.fpre + 4 * p + 3, fyt[q]);
                 }
             }
             pos += (unsigned)__popcll(masks[q]);
@@ -1168,12 +1193,12 @@ __device__ __forceinline__ void gather_body(const u64 *key, const uint32_t *orig
     if (threadIdx.x == 0) {
         double t = 0.0;
         for (int q = 0; q < GT / 64; ++q) t = t + s_w[q];
-        w.parts[blk] = t;
+        stc(w.parts + blk, t);
     }
     if (fs.on && threadIdx.x < 8) {
         double t = 0.0;
         for (int q = 0; q < GT / 64; ++q) t = t + s_f[8 * q + threadIdx.x];
-        w.fparts[8 * blk + threadIdx.x] = t;
+        stc(w.fparts + 8 * blk + threadIdx.x, t);
     }
     GPROF(29);
 }
@@ -1197,7 +1222,8 @@ __global__ __launch_bounds__(GT) void k_sel_bounds_gather(const u64 *key, const 
     if (blockIdx.x == 0) {
         // (ccount was reset by k_sel_hist, a launch earlier: nothing to drain before the
         // flag; b0, b1, U and kbase are read by k_sel_final, a later launch)
-        const unsigned bb = bounds_body(w, n, lam, lam_dev, skip, fixb, false);
+        __shared__ BoundsLds L;
+        const unsigned bb = bounds_body(w, n, lam, lam_dev, skip, fixb, L, false);
         if (bb != kBoundsSkipped && threadIdx.x == 0) {
             // (pub_gen == gen except under the test-only fault injection FICP_FAULT_SPIN,
             // ficp_set_fault)
@@ -1210,6 +1236,15 @@ __global__ __launch_bounds__(GT) void k_sel_bounds_gather(const u64 *key, const 
 }
 
 // ---------------------------------------------------------- the final workgroup
+// Every load of the gather's outputs (candidates, their pairs, the part sums) and of the
+// bounds' outputs is sc1 (agent scope, past this CU's L1): k_sel_bgf runs the final in the
+// gather's last workgroup, in the same launch as the sc1 stores that wrote them
+// (MI355X_MICROARCH.md hand-off table; the same loads serve the separate k_sel_final).
+template <class T>
+__device__ __forceinline__ T ldc(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double2 ldc2(const double *p) { return make_double2(ldc(p), ldc(p + 1)); }
 struct Cand {
     u64 *k;
     uint32_t *o;
@@ -1332,12 +1367,12 @@ __device__ ScanOut lds_sort_scan(const Cand &src, unsigned c, long long K0, doub
     u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
     for (unsigned i = t; i < c; i += HT) {
         // (PRE: the caller staged the candidates in LDS and passed a barrier)
-        const u64 k = PRE ? lk[i] : src.k[i];
-        const uint32_t o = PRE ? lo[i] : src.o[i];
+        const u64 k = PRE ? lk[i] : ldc(src.k + (i));
+        const uint32_t o = PRE ? lo[i] : ldc(src.o + (i));
         if (!PRE) {
             lk[i] = k;
             lo[i] = o;
-            if (RL) lr[i] = src.r[i];
+            if (RL) lr[i] = ldc(src.r + (i));
         }
         kmn = k < kmn ? k : kmn;
         kmx = k > kmx ? k : kmx;
@@ -1403,7 +1438,7 @@ __device__ ScanOut lds_sort_scan(const Cand &src, unsigned c, long long K0, doub
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
         const unsigned p = (unsigned)(t * PP + q);
-        v[q] = p < c ? (RL ? lr[pos[p]] : src.r[pos[p]]) : 0.0;
+        v[q] = p < c ? (RL ? lr[pos[p]] : ldc(src.r + (pos[p]))) : 0.0;
         tsum = tsum + v[q];
     }
     double all;
@@ -1436,7 +1471,7 @@ __device__ ScanOut lds_sort_scan(const Cand &src, unsigned c, long long K0, doub
     ScanOut r{bf, bk, 0, 0, all};
     if (t == 0 && bk != 0x7fffffffffffffffLL) {
         const unsigned e = pos[(unsigned)(bk - K0 - 1)];
-        r.tk = RL ? lk[e] : src.k[e];
+        r.tk = RL ? lk[e] : ldc(src.k + (e));
         r.to = lo[e];
     }
     return r;
@@ -1464,15 +1499,15 @@ __device__ void final_lds(const Cand &src, unsigned c, const FinalIn &in, unsign
                 for (int j = 0; j < 4; ++j) {
                     const unsigned q = q0 + (unsigned)j * HT;
                     const unsigned e = pos[q < nsel ? q : q0];
-                    a[j] = *reinterpret_cast<const double2 *>(fpre + 4 * e);
-                    b[j] = *reinterpret_cast<const double2 *>(fpre + 4 * e + 2);
+                    a[j] = ldc2(fpre + 4 * e);
+                    b[j] = ldc2(fpre + 4 * e + 2);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     if (q0 + (unsigned)j * HT < nsel) fit_add(cf, a[j].x, a[j].y, b[j].x, b[j].y, in.fs.px, in.fs.py);
             }
         } else {
-            for (unsigned q = threadIdx.x; q < nsel; q += HT) fit_row(cf, in.fs, src.p[pos[q]]);
+            for (unsigned q = threadIdx.x; q < nsel; q += HT) fit_row(cf, in.fs, ldc(src.p + (pos[q])));
         }
         blk_sum8_add(cf, in.fsum, scr);
     }
@@ -1579,8 +1614,8 @@ __device__ bool final_chunked(const Cand &src, const Cand &dst, unsigned c, cons
     const int t = threadIdx.x;
     u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
     for (unsigned i = t; i < c; i += HT) {
-        const u64 k = src.k[i];
-        const uint32_t o = src.o[i];
+        const u64 k = ldc(src.k + (i));
+        const uint32_t o = ldc(src.o + (i));
         kmn = k < kmn ? k : kmn;
         kmx = k > kmx ? k : kmx;
         omn = o < omn ? o : omn;
@@ -1598,7 +1633,7 @@ __device__ bool final_chunked(const Cand &src, const Cand &dst, unsigned c, cons
     const Comp cmp = make_comp(kmn, kmx, (uint32_t)omn, (uint32_t)omx);
     const int vb = bits_of(cmp(kmx, (uint32_t)omx));
     const int sh = vb > NS_LOG ? vb - NS_LOG : 0;
-    for (unsigned i = t; i < c; i += HT) atomicAdd(&cnt[(int)(cmp(src.k[i], src.o[i]) >> sh)], 1u);
+    for (unsigned i = t; i < c; i += HT) atomicAdd(&cnt[(int)(cmp(ldc(src.k + (i)), ldc(src.o + (i))) >> sh)], 1u);
     __syncthreads();
     {
         constexpr int PB = NS / HT;
@@ -1649,14 +1684,14 @@ __device__ bool final_chunked(const Cand &src, const Cand &dst, unsigned c, cons
         g_beg[ng] = c;
     }
     for (unsigned i = t; i < c; i += HT) {
-        const u64 k = src.k[i];
-        const uint32_t o = src.o[i];
+        const u64 k = ldc(src.k + (i));
+        const uint32_t o = ldc(src.o + (i));
         const int b = (int)(cmp(k, o) >> sh);
         const unsigned q = off[b] + atomicAdd(&fil[b], 1u);
         dst.k[q] = k;
         dst.o[q] = o;
-        dst.r[q] = src.r[i];
-        dst.p[q] = src.p[i];
+        dst.r[q] = ldc(src.r + (i));
+        dst.p[q] = ldc(src.p + (i));
     }
     __threadfence_block();
     __syncthreads();
@@ -1743,13 +1778,13 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
     double rmax = 0.0;
     for (unsigned i = t; i < c; i += HT) {
-        const u64 k = src.k[i];
-        const uint32_t o = src.o[i];
+        const u64 k = ldc(src.k + (i));
+        const uint32_t o = ldc(src.o + (i));
         kmn = k < kmn ? k : kmn;
         kmx = k > kmx ? k : kmx;
         omn = o < omn ? o : omn;
         omx = o > omx ? o : omx;
-        rmax = fmax(rmax, src.r[i]);
+        rmax = fmax(rmax, ldc(src.r + (i)));
     }
     for (int b = t; b < NS; b += HT) {
         rc[b] = 0u;
@@ -1771,9 +1806,9 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     const int e = rmax > 0.0 ? ilogb(rmax) : 0;
     const int Lq = e + 1 - (62 - bits_of((u64)c));
     for (unsigned i = t; i < c; i += HT) {
-        const int b = (int)(cmp(src.k[i], src.o[i]) >> sh);
+        const int b = (int)(cmp(ldc(src.k + (i)), ldc(src.o + (i))) >> sh);
         atomicAdd(&rc[b], 1u);
-        atomicAdd(&rs[b], fx_floor(src.r[i], Lq));
+        atomicAdd(&rs[b], fx_floor(ldc(src.r + (i)), Lq));
     }
     __syncthreads();
     constexpr int PB = NS / HT;  // 4 sub-bins per thread
@@ -1842,14 +1877,14 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
     long long below = 0;
     u128 cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (unsigned i = t; i < c; i += HT) {
-        const u64 k = src.k[i];
-        const uint32_t o = src.o[i];
-        const double rv = src.r[i];
+        const u64 k = ldc(src.k + (i));
+        const uint32_t o = ldc(src.o + (i));
+        const double rv = ldc(src.r + (i));
         const int b = (int)(cmp(k, o) >> sh);
         if (b < bmin) {
             below += 1;
             if (in.fs.on) {
-                const uint32_t wr = src.p[i];
+                const uint32_t wr = ldc(src.p + (i));
                 double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                 fit_add(v, in.fs.sx[wr], in.fs.sy[wr], in.fs.cx[wr], in.fs.cy[wr], in.fs.px,
                         in.fs.py);
@@ -1874,7 +1909,7 @@ __device__ bool refine(Cand &src, Cand &dst, unsigned &c, FinalIn &in, unsigned 
             dst.k[slot] = k;
             dst.o[slot] = o;
             dst.r[slot] = rv;
-            dst.p[slot] = src.p[i];
+            dst.p[slot] = ldc(src.p + (i));
         }
     }
     // integer sums are order-free: reduce hi/lo with carries through LDS
@@ -1922,8 +1957,8 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     u64 kmn = ~0ULL, kmx = 0ULL, omn = ~0ULL, omx = 0ULL;
     for (unsigned i = t; i < c; i += HT) {
-        const u64 k = src.k[i];
-        const uint32_t o = src.o[i];
+        const u64 k = ldc(src.k + (i));
+        const uint32_t o = ldc(src.o + (i));
         kmn = k < kmn ? k : kmn;
         kmx = k > kmx ? k : kmx;
         omn = o < omn ? o : omn;
@@ -1939,8 +1974,8 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
                       : (unsigned)(((k - kmn) >> (8 * (p - po))) & 0xffu);
     };
     for (unsigned i = t; i < c; i += HT) {
-        const u64 k = src.k[i];
-        const uint32_t o = src.o[i];
+        const u64 k = ldc(src.k + (i));
+        const uint32_t o = ldc(src.o + (i));
         for (int p = 0; p < np; ++p) atomicAdd(&hist[p * 256 + digit(k, o, p)], 1u);
     }
     __syncthreads();
@@ -1960,10 +1995,10 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
             double rv = 0.0;
             unsigned d = 0;
             if (valid) {
-                k = src.k[i];
-                o = src.o[i];
-                rv = src.r[i];
-                pw = src.p[i];
+                k = ldc(src.k + (i));
+                o = ldc(src.o + (i));
+                rv = ldc(src.r + (i));
+                pw = ldc(src.p + (i));
                 d = digit(k, o, p);
             }
             u64 m = __ballot(valid);
@@ -2010,7 +2045,7 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
     long long bk = 0x7fffffffffffffffLL;
     for (unsigned t0 = 0; t0 < c; t0 += HT) {
         const unsigned i = t0 + t;
-        const double v = i < c ? src.r[i] : 0.0;
+        const double v = i < c ? ldc(src.r + (i)) : 0.0;
         double all;
         const double ex = blk_excl_scan_d(v, scr, all);
         if (i < c) {
@@ -2027,7 +2062,7 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
     blk_argmin(bf, bk, scr);
     if (in.fs.on && bk != 0x7fffffffffffffffLL) {  // fused fit: the selected candidates
         double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (unsigned q = t; q < (unsigned)(bk - in.K0); q += HT) fit_row(cf, in.fs, src.p[q]);
+        for (unsigned q = t; q < (unsigned)(bk - in.K0); q += HT) fit_row(cf, in.fs, ldc(src.p + (q)));
         blk_sum8_add(cf, in.fsum, scr);
     }
     if (t == 0) {
@@ -2035,8 +2070,8 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
         uint32_t to = 0;
         if (bk != 0x7fffffffffffffffLL) {
             const unsigned e = (unsigned)(bk - in.K0 - 1);
-            tk = src.k[e];
-            to = src.o[e];
+            tk = ldc(src.k + (e));
+            to = ldc(src.o + (e));
         }
         publish(st, in, bf, bk, tk, to);
     }
@@ -2044,10 +2079,12 @@ __device__ void final_radix(Cand &src, Cand &dst, unsigned c, const FinalIn &in,
 
 // With fuse_loop, thread 0 also runs the loop step of k_loop_update (ficp.py:122-154)
 // and, with host_flag, stores the state's done flag to that (coherent pinned) host word.
-__global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N, double lam,
-                                                  const double *lam_dev, IterState *st,
-                                                  const int *skip, LoopCtl lc, int fuse_loop,
-                                                  int *host_flag, FitSrc fs, int64_t cap) {
+// The final selection of one call (one HT-thread workgroup): k_sel_final, or the last
+// gather workgroup of k_sel_bgf.  sm: SMEM bytes of LDS.
+__device__ __forceinline__ void final_body(SelWS w, int nparts, int64_t N, double lam,
+                                           const double *lam_dev, IterState *st, const int *skip,
+                                           const LoopCtl &lc, int fuse_loop, int *host_flag,
+                                           const FitSrc &fs, int64_t cap, unsigned char *sm) {
     // the independent loads (skip flag, lambda, the candidate count and the bounds'
     // outputs, and the first SMALL_C candidate slots whatever the count) issue together,
     // before the first wait
@@ -2058,17 +2095,17 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     const unsigned errv = __hip_atomic_fetch_or(&w.ctl->err, 0u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
     [[maybe_unused]] const unsigned c_in = c;
-    const long long kbase = w.ctl->kbase;
-    const double Ub = w.ctl->U;
+    const long long kbase = ldc(&w.ctl->kbase);
+    const double Ub = ldc(&w.ctl->U);
     CandPre pre{};
     const bool pfc = (int64_t)threadIdx.x < cap && threadIdx.x < (unsigned)SMALL_C;
     if (pfc) {
-        pre.k = w.ka[threadIdx.x];
-        pre.o = w.oa[threadIdx.x];
-        pre.r = w.ra[threadIdx.x];
+        pre.k = ldc(w.ka + threadIdx.x);
+        pre.o = ldc(w.oa + threadIdx.x);
+        pre.r = ldc(w.ra + threadIdx.x);
         if (fs.on) {  // the gather stored the pairs of the first SMALL_C slots
-            const double2 a01 = *reinterpret_cast<const double2 *>(w.fpre + 4 * threadIdx.x);
-            const double2 a23 = *reinterpret_cast<const double2 *>(w.fpre + 4 * threadIdx.x + 2);
+            const double2 a01 = ldc2(w.fpre + 4 * threadIdx.x);
+            const double2 a23 = ldc2(w.fpre + 4 * threadIdx.x + 2);
             pre.f[0] = a01.x;
             pre.f[1] = a01.y;
             pre.f[2] = a23.x;
@@ -2081,7 +2118,6 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
         return;
     }
     lam = lamv;
-    __shared__ __align__(16) unsigned char sm[SMEM];
     __shared__ Scr scr;
     __shared__ IterState s_st;  // thread 0's working copy of the state (one load, one store)
     __shared__ double s_fit[8];  // fused fit sums (thread 0)
@@ -2095,7 +2131,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
     for (int q = t; q < SW; q += HT) ((uint32_t *)&s_st)[q] = ((const uint32_t *)st)[q];
     if (t < 8) s_fit[t] = 0.0;
     double a = 0.0;
-    for (int p = t; p < nparts; p += HT) a = a + w.parts[p];  // fixed order per thread
+    for (int p = t; p < nparts; p += HT) a = a + ldc(w.parts + p);  // fixed order per thread
     FinalIn in;
     in.N = N;
     in.lam = lam;
@@ -2106,7 +2142,7 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
         double cf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int p = t; p < nparts; p += HT)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) cf[e] = cf[e] + w.fparts[8 * p + e];
+            for (int e = 0; e < 8; ++e) cf[e] = cf[e] + ldc(w.fparts + 8 * p + e);
         blk_sum8_add(cf, s_fit, scr);
     }
     in.K0 = kbase;
@@ -2134,11 +2170,11 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
         } else if (c <= (unsigned)SMALL_C) {  // after refinement: the candidates moved
             CandPre q{};
             if (t < c) {
-                q.k = src.k[t];
-                q.o = src.o[t];
-                q.r = src.r[t];
+                q.k = ldc(src.k + (t));
+                q.o = ldc(src.o + (t));
+                q.r = ldc(src.r + (t));
                 if (fs.on) {
-                    const uint32_t wr = src.p[t];
+                    const uint32_t wr = ldc(src.p + (t));
                     q.f[0] = fs.sx[wr];
                     q.f[1] = fs.sy[wr];
                     q.f[2] = fs.cx[wr];
@@ -2211,6 +2247,57 @@ __global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N
                    (long long)(g[20] - g[3]), (long long)(g[4] - g[20]), (long long)(g[5] - g[4]));
     }
 #endif
+}
+
+__global__ __launch_bounds__(HT) void k_sel_final(SelWS w, int nparts, int64_t N, double lam,
+                                                  const double *lam_dev, IterState *st,
+                                                  const int *skip, LoopCtl lc, int fuse_loop,
+                                                  int *host_flag, FitSrc fs, int64_t cap) {
+    __shared__ __align__(16) unsigned char sm[SMEM];
+    final_body(w, nparts, N, lam, lam_dev, st, skip, lc, fuse_loop, host_flag, fs, cap, sm);
+}
+
+// k_sel_bounds_gather and k_sel_final in one launch (round 5; three launches per full-path
+// call instead of four): block 0 computes and publishes the candidate buckets, blocks 1..
+// gather, and the last gather workgroup to arrive runs the final.  The hand-off is
+// k_fit_sums' / k_sel_win's: the gather's outputs are sc1 stores, every storing wave drains
+// them, one lane arrives at its group counter (blockIdx % 8) and the group's last at the
+// top counter; the final reads them with sc1 loads.  Block 0's LDS is laid over the
+// final's buffer (block 0 never runs the final).
+static_assert(sizeof(BoundsLds) <= (size_t)SMEM, "bounds LDS inside the final's buffer");
+__global__ __launch_bounds__(GT) void k_sel_bgf(const u64 *key, const uint32_t *orig, const double *r,
+                                               int64_t n, SelWS w, double lam, const double *lam_dev,
+                                               const int *skip, int fixb, FitSrc fs, unsigned gen,
+                                               unsigned pub_gen, IterState *st, LoopCtl lc,
+                                               int fuse_loop, int *host_flag, int64_t cap) {
+    __shared__ __align__(16) unsigned char sm[SMEM];
+    __shared__ int s_last;
+    if (blockIdx.x == 0) {
+        const unsigned bb = bounds_body(w, n, lam, lam_dev, skip, fixb, *reinterpret_cast<BoundsLds *>(sm), false);
+        if (bb != kBoundsSkipped && threadIdx.x == 0)
+            __hip_atomic_store(&w.ctl->bpub, ((u64)pub_gen << 32) | bb, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const unsigned ngb = gridDim.x - 1u, bid = blockIdx.x - 1u;
+    gather_body(key, orig, r, n, w, fs, (int)bid, gen, skip);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned grp = bid & 7u, ng = min(ngb, 8u);
+        const unsigned gsz = (ngb - grp + 7u) / 8u;
+        unsigned *gc = w.wctr + WCTR * (1 + grp);
+        bool last = false;
+        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsz - 1) {
+            __hip_atomic_exchange(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = __hip_atomic_fetch_add(w.wctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+            if (last) __hip_atomic_exchange(w.wctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    final_body(w, (int)ngb, n, lam, lam_dev, st, skip, lc, fuse_loop, host_flag, fs, cap, sm);
 }
 
 // ======================================================== window path (one launch)
@@ -3093,6 +3180,18 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
     const bool split = sp && atoi(sp) != 0;
     hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, s, w, hist_blocks(n), skip,
                        hp, (long long *)nullptr);
+    //  * round 5, the default: k_sel_bgf -- k_sel_bounds_gather with the final in its last
+    //    gather workgroup (FICP_SEL_BGF=0: the final as its own launch).
+    const char *bg = getenv("FICP_SEL_BGF");
+    const bool bgf = !split && !(bg && atoi(bg) == 0);
+    LoopCtl lc{};
+    if (loop) lc = *loop;
+    if (bgf) {
+        hipLaunchKernelGGL(k_sel_bgf, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n, w, lam, lam_dev,
+                           skip, hp.fixb, fs, gen, pub, st, lc, loop ? 1 : 0, host_flag,
+                           std::max<int64_t>(n, 1));
+        return hipGetLastError();
+    }
     if (split) {
         hipLaunchKernelGGL(k_sel_bounds, dim3(1), dim3(HT), 0, s, w, n, lam, lam_dev, skip,
                            hp.fixb);
@@ -3101,8 +3200,6 @@ hipError_t launch_select(const unsigned long long *key, const uint32_t *orig, co
         hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, s, key, orig, r, n,
                            w, lam, lam_dev, skip, hp.fixb, fs, gen, pub);
     }
-    LoopCtl lc{};
-    if (loop) lc = *loop;
     hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, s, w, gb, n, lam, lam_dev, st, skip, lc,
                        loop ? 1 : 0, host_flag, fs, std::max<int64_t>(n, 1));
     return hipGetLastError();

@@ -153,8 +153,18 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(k_sel_reduce, dim3(NB / RBPB), dim3(1024), 0, 0, w, hist_blocks(n),
                            (const int *)nullptr, hist_pack(n), (long long *)nullptr);
         CK(hipEventRecord(ev[1], 0));
-        if (it & 2) {  // reps 2, 3 of every 4 (both maps): the library's one-launch form
-            static unsigned gen = 0;
+        static unsigned gen = 0;
+        LoopCtl lc{};
+        const bool bgf = (it % 8) >= 6;  // reps 6, 7 of every 8 (both maps): the library's
+                                         // default, bounds + gather + final in one launch
+        if (bgf) {
+            CK(hipEventRecord(ev[2], 0));
+            hipLaunchKernelGGL(k_sel_bgf, dim3(gb + 1), dim3(GT), 0, 0, dkey, dorig, dr, n, w, lam,
+                               (const double *)nullptr, (const int *)nullptr, hist_pack(n).fixb,
+                               FitSrc{}, gen + 1, gen + 1, st, lc, 0, (int *)nullptr,
+                               (int64_t)std::max<int64_t>(n, 1));
+            ++gen;
+        } else if (it & 2) {  // reps 2, 3 of every 4: bounds + gather in one launch
             CK(hipEventRecord(ev[2], 0));
             hipLaunchKernelGGL(k_sel_bounds_gather, dim3(gb + 1), dim3(GT), 0, 0, dkey, dorig, dr,
                                n, w, lam, (const double *)nullptr, (const int *)nullptr,
@@ -168,10 +178,10 @@ int main(int argc, char **argv) {
                                (const int *)nullptr, FitSrc{});
         }
         CK(hipEventRecord(ev[3], 0));
-        LoopCtl lc{};
-        hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, 0, w, gb, n, lam,
-                           (const double *)nullptr, st, (const int *)nullptr, lc, 0, (int *)nullptr,
-                           FitSrc{}, (int64_t)std::max<int64_t>(n, 1));
+        if (!bgf)
+            hipLaunchKernelGGL(k_sel_final, dim3(1), dim3(HT), 0, 0, w, gb, n, lam,
+                               (const double *)nullptr, st, (const int *)nullptr, lc, 0, (int *)nullptr,
+                               FitSrc{}, (int64_t)std::max<int64_t>(n, 1));
         CK(hipEventRecord(ev[4], 0));
         CK(hipEventSynchronize(ev[4]));
         for (int q = 0; q < 4; ++q) {

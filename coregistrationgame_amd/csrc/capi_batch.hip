@@ -38,7 +38,7 @@ struct BatchBufs {
     PinBuf rep{nullptr, 0, hipHostMallocCoherent};  // report kernel target: states + flag
     static constexpr int kSubMax = 4;
     hipStream_t ss[kSubMax] = {};          // sub-batch streams 1.. (0 is the context's)
-    hipEvent_t fork = nullptr, join[kSubMax] = {}, stag[kSubMax] = {};
+    hipEvent_t fork = nullptr, join[kSubMax] = {};
 };
 constexpr int kBatchRing = 4;
 constexpr int kMaxSub = BatchBufs::kSubMax;  // sub-batches on their own streams (h_flag: kMaxSub rings)
@@ -59,7 +59,6 @@ void batch_release(BatchBufs *b) {
     for (int q = 0; q < kMaxSub; ++q) {
         if (b->ss[q]) (void)hipStreamDestroy(b->ss[q]);
         if (b->join[q]) (void)hipEventDestroy(b->join[q]);
-        if (b->stag[q]) (void)hipEventDestroy(b->stag[q]);
     }
     if (b->fork) (void)hipEventDestroy(b->fork);
     if (b->h_flag) (void)hipHostFree(b->h_flag);
@@ -427,13 +426,6 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                            allow_refl, nstages, max_iter, threshold};
         if (trace) step.max_trace = c->btrace_max;
         step.worig = worig;
-        // FICP_BATCH_STAGGER=1: sub-batch q's first NN launch waits for sub-batch q-1's, so
-        // the sub-batches start one NN call apart (one's NN beside another's selection)
-        const char *sg = getenv("FICP_BATCH_STAGGER");
-        const bool stagger = nsub > 1 && sg && atoi(sg) != 0;
-        if (stagger)
-            for (int q = 0; q + 1 < nsub; ++q)
-                if (!b.stag[q]) HIPCHK(hipEventCreateWithFlags(&b.stag[q], hipEventDisableTiming));
         auto enqueue = [&](Sub &u, int64_t bit) -> int {
             const int qi = (int)(&u - subs);
             int *flag = &u.ring[bit % kBatchRing];
@@ -464,14 +456,12 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             au.out_bp = a.out_bp + u.r0;
             au.gap = a.gap + u.r0;
             au.dz2 = a.dz2 ? a.dz2 + u.r0 : nullptr;
-            if (stagger && bit == 0 && qi > 0) HIPCHK(hipStreamWaitEvent(u.s, b.stag[qi - 1], 0));
             {
                 ProfScope ps(c, prof ? P_NN : 0, "nn_grid_batch", u.s);
                 HIPCHK(launch_nn_grid_batch(au, b.plot_of.as<int32_t>() + u.r0, b.grids.as<PlotGrid>(),
                                             b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
                                             md, u.s));
             }
-            if (stagger && bit == 0 && qi + 1 < nsub) HIPCHK(hipEventRecord(b.stag[qi], u.s));
             BatchStepArgs su_step = step;  // this sub-batch's grids, counter, flag and trace
             su_step.grids = gu;  // indexed by the plot within the sub-batch (fit pivot)
             su_step.trace = trace ? trace + (size_t)u.p0 * (size_t)step.max_trace : nullptr;

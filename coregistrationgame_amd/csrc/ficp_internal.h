@@ -560,7 +560,9 @@ __device__ __forceinline__ void loop_set_flags(IterState &s) {
 }
 
 __device__ __forceinline__ void loop_end_stage(IterState &s, const LoopCtl &c) {
-    if (s.stage < 2) s.iters[s.stage] = s.it;
+    // (constant indices: a caller's register copy of the state stays in registers)
+    if (s.stage == 0) s.iters[0] = s.it;
+    else if (s.stage == 1) s.iters[1] = s.it;
     s.stage += 1;
     s.it = 0;
     if (s.stage < c.nstages) {  // ficp.py:152-153: next lambda, next _iterate
@@ -589,7 +591,8 @@ __device__ __forceinline__ void loop_step(IterState *st, const LoopCtl &c) {
             loop_end_stage(s, c);  // ficp.py:125-126: nothing selected, the stage returns
         } else {
             s.cur = s.frmsd;
-            if (s.stage < 2) s.frmsd_last[s.stage] = s.cur;
+            if (s.stage == 0) s.frmsd_last[0] = s.cur;
+            else if (s.stage == 1) s.frmsd_last[1] = s.cur;
             s.phase = PH_LOOP;
             s.it = 0;
             if (c.max_iter <= 0) loop_end_stage(s, c);
@@ -605,7 +608,8 @@ __device__ __forceinline__ void loop_step(IterState *st, const LoopCtl &c) {
                                s.T[3 * i + 2] * s.Ttot[6 + j];
         for (int e = 0; e < 9; ++e) s.Ttot[e] = R[e];
         const double nw = s.frmsd;
-        if (s.stage < 2) s.frmsd_last[s.stage] = nw;
+        if (s.stage == 0) s.frmsd_last[0] = nw;
+        else if (s.stage == 1) s.frmsd_last[1] = nw;
         if (s.cur - nw <= c.threshold) {  // ficp.py:142 (the transform is already applied)
             loop_end_stage(s, c);
         } else {

@@ -2195,22 +2195,25 @@ __device__ __forceinline__ void final_body(SelWS w, int nparts, int64_t N, doubl
     }
     SELPROF(5);
     if (t == 0) {
+        // thread 0's step on a register copy (every field access of the LDS copy was a
+        // dependent LDS round trip)
+        IterState L = s_st;
         // the window path could not decide this call (k_sel_win): the NN launch queued
         // behind it was a no-op by nn_reuse, which the state machine restores here
-        if (s_st.win_fail) {
-            s_st.win_fail = 0;
-            s_st.nn_reuse = 0;
+        if (L.win_fail) {
+            L.win_fail = 0;
+            L.nn_reuse = 0;
         }
-        if (fuse_loop) loop_step(&s_st, lc);
+        if (fuse_loop) loop_step(&L, lc);
         // a sticky selection error (ERR_SPIN, ERR_CAP): this call's result is invalid, so
         // the device loop ends here and the host reports the flag (no further calls)
         if (fuse_loop && errv) {
-            s_st.phase = PH_DONE;
-            loop_set_flags(s_st);
+            L.phase = PH_DONE;
+            loop_set_flags(L);
         }
         // fused fit: T of the next loop body from this selection (k_fit_sums' work)
-        if (fs.on && !s_st.no_fit && s_st.k > 0)
-            fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
+        if (fs.on && !L.no_fit && L.k > 0) fit_solve(s_fit, (double)L.k, fs.px, fs.py, fs.allow_refl, &L);
+        s_st = L;
     }
     __syncthreads();
     for (int q = t; q < SW; q += HT) ((uint32_t *)st)[q] = ((const uint32_t *)&s_st)[q];
@@ -2718,16 +2721,17 @@ __device__ __forceinline__ void win_tail(SelWS w, int64_t n, const WMap &m0, dou
     }
     WINP_T(8);
     if (t == 0) {
-        publish(&s_st, in, rs.bf, rs.bk, s_tko[0], (uint32_t)s_tko[1]);
+        IterState L = s_st;  // (thread 0's step on a register copy, as k_sel_final)
+        publish(&L, in, rs.bf, rs.bk, s_tko[0], (uint32_t)s_tko[1]);
         // the next window's smallest half-width from this one's row count (2^lh keys)
         {
-            const int f = win_floor(s_st.wfloor, n);
-            if (Wt > 384) s_st.wfloor = max(kWinHMinLog, min(f, m.su + 2) - 1);
-            else if (Wt < 48) s_st.wfloor = min(win_start_log(n), f + 1);
+            const int f = win_floor(L.wfloor, n);
+            if (Wt > 384) L.wfloor = max(kWinHMinLog, min(f, m.su + 2) - 1);
+            else if (Wt < 48) L.wfloor = min(win_start_log(n), f + 1);
         }
-        loop_step(&s_st, lc);
-        if (fs.on && !s_st.no_fit && s_st.k > 0)
-            fit_solve(s_fit, (double)s_st.k, fs.px, fs.py, fs.allow_refl, &s_st);
+        loop_step(&L, lc);
+        if (fs.on && !L.no_fit && L.k > 0) fit_solve(s_fit, (double)L.k, fs.px, fs.py, fs.allow_refl, &L);
+        s_st = L;
     }
     __syncthreads();
     WINP_T(9);

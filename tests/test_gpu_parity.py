@@ -378,7 +378,7 @@ def test_run_vs_oracle_100k(oracle):
 KNOBS = [{}, {"FICP_FUSE_FIT": "0"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
          {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "0"},
          {"FICP_GRID_PER_CELL": "4"}, {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_SPLIT": "1", "FICP_FUSE_FIT": "0"},
-         {"FICP_NN_KEYS": "1"}]
+         {"FICP_SEL_BGF": "0"}, {"FICP_NN_KEYS": "1"}]
 
 
 @pytest.mark.parametrize("knobs,md", [(k, 3) for k in KNOBS] + [({}, 2), ({"FICP_GRID_ATOMIC": "1"}, 2)],

@@ -1408,7 +1408,8 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
     }
     // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
     // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers; round 5
-    // with 16 cached rows per thread: 131 VGPRs spilled, not run)
+    // with 16 cached rows per thread: 131 VGPRs spilled, with 10: 200 B of scratch per lane
+    // at the 128-VGPR cap, since the uncached form alone holds 141; not run)
     // cached rows per thread by plot size: 20 (plots up to 10,240 rows: C4's 10k) or RPT (the
     // unrolled row loops skip no padding slot, so a 10k-row plot ran 32 iterations per pass)
     constexpr int RPT_S = 20;

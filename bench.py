@@ -405,8 +405,9 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
     lam = [3.0, 0.95 if md == 3 else 1.3]
 
     def step():
-        src.copy_from(src0, cols=2)  # x, y restored in one copy
+        # the target first: its bbox report lands while the source's reset copy is queued
         ctx.set_target_device(tgt.col(0), tgt.col(1), tgt.col(2) if md == 3 else 0, m, md)
+        src.copy_from(src0, cols=2)  # x, y restored in one copy
         return ctx.run_device(src.col(0), src.col(1), src.col(2) if md == 3 else 0, n, lam, thr, max_it)
 
     def barrier():

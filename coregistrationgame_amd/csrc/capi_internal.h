@@ -139,6 +139,7 @@ struct HostReport {
     double bb[4];      // CHM bbox
     unsigned long long t[2];  // device clock (100 MHz) at run start / at the final report
     int flag;          // -1 while pending, 1 when the segments have landed
+    int bflag;         // the same for set_target_device's early bbox report (bb)
 };
 
 struct ficp_ctx {
@@ -168,6 +169,7 @@ struct ficp_ctx {
     DevBuf bp;  // grid slot of each query's last match (warm start of the next NN call)
     DevBuf dz2; // dz^2 of each query's last match (warm start from (ccx, ccy, dz2))
     bool bbox_dev = false;  // the bbox is in mm_out already (set_target_device), not read yet
+    bool bbox_pending = false;  // set_target_device's bbox report is queued (h_rep->bflag)
     DevBuf gap; // certified-reuse bound of each query's match (k_grid_nn.hip nn_query_cert)
     DevBuf lams, tr_k, tr_f, tr_l, tr_T, tr_idx;  // device loop: lambdas and traces
     DevBuf sel_tmp, sel_stats;  // bucketed fraction selection (k_select.hip)

@@ -486,6 +486,60 @@ def test_device_resident_path_matches_host_path(md):
         ctx.close()
 
 
+@pytest.mark.gpu
+def test_target_replaced_while_bbox_report_pending():
+    """ficp_set_target_device queues its bbox report at once (capi.hip bbox_collect).  A
+    second target set before any run -- device or host -- must collect that report first,
+    so the run plans its grid on the second target's bbox: the bits of a fresh context
+    given only the second target."""
+    from coregistrationgame_amd import _lib, synth
+    C = _lib.C
+    lib = _lib.lib()
+    md = 3
+    lam = [3.0, 0.95]
+    p = synth.make_plot(40_000, 50_000, 0.7, seed=11, md=md)
+    decoy = p.target.copy()
+    decoy[:, :2] = decoy[:, :2] * 3.0 + 5000.0  # another bbox entirely
+    ref = _lib.Context(0)
+    want = p.source.copy()
+    ref.set_target(p.target, md)
+    ref.run(want, lam, 1e-6, 1000, False)
+    ref.close()
+    ctx = _lib.Context(0)
+    bufs = []
+
+    def dev(a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        q = C.c_void_p()
+        _lib._check(lib.ficp_dev_alloc(ctx.h, a.nbytes, C.byref(q)))
+        _lib._check(lib.ficp_memcpy_h2d(ctx.h, q, a.ctypes.data_as(C.c_void_p), a.nbytes))
+        bufs.append(q)
+        return q.value
+
+    try:
+        cols = [dev(decoy[:, j]) for j in range(3)]
+        real = [dev(p.target[:, j]) for j in range(3)]
+        # device then device
+        ctx.set_target_device(cols[0], cols[1], cols[2], len(decoy), md)
+        ctx.set_target_device(real[0], real[1], real[2], len(p.target), md)
+        sx, sy, sz = (dev(p.source[:, j]) for j in range(3))
+        ctx.run_device(sx, sy, sz, len(p.source), lam, 1e-6, 1000)
+        for j, s in ((0, sx), (1, sy)):
+            out = np.empty(len(p.source))
+            _lib._check(lib.ficp_memcpy_d2h(ctx.h, out.ctypes.data_as(C.c_void_p), C.c_void_p(s), out.nbytes))
+            np.testing.assert_array_equal(bits(out), bits(want[:, j]))
+        # device then host
+        ctx.set_target_device(cols[0], cols[1], cols[2], len(decoy), md)
+        ctx.set_target(p.target, md)
+        got = p.source.copy()
+        ctx.run(got, lam, 1e-6, 1000, False)
+        np.testing.assert_array_equal(bits(got[:, :2]), bits(want[:, :2]))
+    finally:
+        for b in bufs:
+            lib.ficp_dev_free(ctx.h, b)
+        ctx.close()
+
+
 def test_run_many_stages_matches_split_runs():
     """Six stages in one ficp_run (lambdas past the fourth come from the device array, the
     first four from the kernel arguments) equal the same stages run as two calls."""

@@ -34,7 +34,7 @@ struct BatchBufs {
     DevBuf arrive;                         // fused step: per sub-batch arrival/live counter
     unsigned fctr_init_gen = 0;            // fctr allocation whose counters are zeroed
     int *h_flag = nullptr;                 // coherent pinned ring: plots still running
-    PinBuf up;                             // pinned staging of the small per-run uploads
+    PinBuf up{nullptr, 0, hipHostMallocCoherent};  // the small per-run uploads (k_batch_init reads them)
     PinBuf rep{nullptr, 0, hipHostMallocCoherent};  // report kernel target: states + flag
     static constexpr int kSubMax = 4;
     hipStream_t ss[kSubMax] = {};          // sub-batch streams 1.. (0 is the context's)
@@ -270,21 +270,34 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
     CHK(b.to.ensure((size_t)(nplots + 1) * 8));
     CHK(b.st.ensure((size_t)nplots * sizeof(PlotState)));
     CHK(b.lams.ensure((size_t)std::max(nstages, 1) * 8));
+    CHK(b.arrive.ensure(kMaxSub * 8));
     {
-        // offsets and lambdas through pinned staging (three pageable copies were three
-        // host-blocking calls); the previous run of this context has finished with it
+        // offsets and lambdas through coherent pinned staging, read by k_batch_init itself
+        // (three staged copies were three runtime blit launches); the previous run of this
+        // context has finished with it
         const size_t off = (size_t)(nplots + 1) * 8, nl = (size_t)std::max(nstages, 0) * 8;
         CHK(b.up.ensure(2 * off + nl + 64));
         char *u = b.up.as<char>();
         memcpy(u, so_h, off);
         memcpy(u + off, to_h, off);
         if (nl) memcpy(u + 2 * off, lambdas, nl);
-        HIPCHK(hipMemcpyAsync(b.so.p, u, off, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(b.to.p, u + off, off, hipMemcpyHostToDevice, c->stream));
-        if (nl) HIPCHK(hipMemcpyAsync(b.lams.p, u + 2 * off, nl, hipMemcpyHostToDevice, c->stream));
+        BatchInitArgs ia{};
+        ia.so_h = (const int64_t *)u;
+        ia.to_h = (const int64_t *)(u + off);
+        ia.lam_h = (const double *)(u + 2 * off);
+        ia.so = b.so.as<int64_t>();
+        ia.to = b.to.as<int64_t>();
+        ia.lams = b.lams.as<double>();
+        // the fused step's arrival counters start at zero (each launch's last workgroup
+        // resets its own); zeroed here, so an earlier failed run leaves none
+        ia.arrive = b.arrive.as<unsigned long long>();
+        ia.nplots = nplots;
+        ia.nstages = nstages;
+        ia.nl = (int)(nl / 8);
+        ia.narrive = kMaxSub;
+        ia.st = b.st.as<PlotState>();
+        HIPCHK(launch_batch_init(ia, c->stream));
     }
-    HIPCHK(launch_batch_init(b.so.as<int64_t>(), b.to.as<int64_t>(), nplots, nstages,
-                             b.st.as<PlotState>(), c->stream));
     bool work = false;  // the trees run in the batch work order (b.wx, wy, wz, worig)
     if (n > 0 && m > 0 && nstages > 0) {
         std::vector<PlotGrid> grids;
@@ -359,10 +372,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         // forces the count.
         int nsub = nplots >= 64 ? 2 : 1;
         if (const char *e = getenv("FICP_BATCH_STREAMS")) nsub = std::max(1, std::min(kMaxSub, atoi(e)));
-        // the fused step's arrival counters start at zero (each launch's last workgroup
-        // resets its own); zeroed here, before the fork, so an earlier failed run leaves none
-        CHK(b.arrive.ensure(kMaxSub * 8));
-        HIPCHK(hipMemsetAsync(b.arrive.p, 0, kMaxSub * 8, c->stream));
+        // (the fused step's arrival counters were zeroed by k_batch_init, before the fork)
         // the per-call k trace is cleared here too, before the fork: the sub-streams write
         // their plots' rows as soon as the fork event lets them run
         long long *trace = nullptr;  // per-call k of every plot (ficp_set_batch_trace), -1 = none

@@ -950,8 +950,18 @@ hipError_t launch_batch_grid_count(const double *tx, const double *ty, int64_t m
 hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
                                 const TPt *pts, int64_t m, const int32_t *cell_start,
                                 const PlotState *st, int md, hipStream_t s);
-hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
-                             PlotState *st, hipStream_t s);
+// k_batch_init: the offsets and lambdas from coherent pinned staging (so_h, to_h, lam_h)
+// into their device copies, the arrival counters zeroed, every plot's state initialised
+struct BatchInitArgs {
+    const int64_t *so_h, *to_h;
+    const double *lam_h;
+    int64_t *so, *to;
+    double *lams;
+    unsigned long long *arrive;
+    int nplots, nstages, nl, narrive;
+    PlotState *st;
+};
+hipError_t launch_batch_init(const BatchInitArgs &a, hipStream_t s);
 // Per-plot LDS counting sort (k_batch.hip k_plot_sort): mode 0 the batch grid (TPt records
 // + cell_start, as k_bsort.hip mode 2), mode 1 the batch work order (wx, wy, wz, worig, as
 // mode 3), the same (key, row) order; one workgroup per plot and job (b: a second job).

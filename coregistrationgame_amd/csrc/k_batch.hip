@@ -96,10 +96,19 @@ __global__ __launch_bounds__(256) void k_batch_grid_count(const double *tx, cons
     atomicAdd(&counts[c], 1);
 }
 
-__global__ void k_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
-                             PlotState *st) {
+// The run's offsets and lambdas come straight from the host's coherent pinned staging
+// (so_h, to_h, lam_h): this kernel stores the device copies the later kernels read, zeroes
+// the fused step's arrival counters and initialises every plot's state.  Three staged
+// copies and a memset were four runtime blit launches (~20 us at the head of a run).
+__global__ void k_batch_init(BatchInitArgs a) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= nplots) return;
+    if (p <= a.nplots) {
+        a.so[p] = a.so_h[p];
+        a.to[p] = a.to_h[p];
+    }
+    if (p < a.nl) a.lams[p] = a.lam_h[p];
+    if (p < a.narrive) a.arrive[p] = 0ULL;
+    if (p >= a.nplots) return;
     PlotState z{};
     for (int e = 0; e < 9; ++e) {
         z.T[e] = (e % 4 == 0) ? 1.0 : 0.0;
@@ -110,9 +119,9 @@ __global__ void k_batch_init(const int64_t *so, const int64_t *to, int nplots, i
     z.wfloor = 0;  // (win_start_log of the plot's rows)
     // empty layers: find_correspondences returns nothing, k = 0, nothing moves
     // (ficp.py:66-68, 75-77, 125-126)
-    const bool empty = (so[p + 1] == so[p]) || (to[p + 1] == to[p]);
-    z.phase = (empty || nstages <= 0) ? PH_DONE : PH_HEAD;
-    st[p] = z;
+    const bool empty = (a.so_h[p + 1] == a.so_h[p]) || (a.to_h[p + 1] == a.to_h[p]);
+    z.phase = (empty || a.nstages <= 0) ? PH_DONE : PH_HEAD;
+    a.st[p] = z;
 }
 
 // ---------------------------------------------------------------- per-plot selection
@@ -1320,11 +1329,9 @@ hipError_t launch_batch_grid_count(const double *tx, const double *ty, int64_t m
     return hipGetLastError();
 }
 
-hipError_t launch_batch_init(const int64_t *so, const int64_t *to, int nplots, int nstages,
-                             PlotState *st, hipStream_t s) {
-    if (nplots <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_batch_init, dim3(nblk(nplots)), dim3(256), 0, s, so, to, nplots, nstages,
-                       st);
+hipError_t launch_batch_init(const BatchInitArgs &a, hipStream_t s) {
+    const int nt = std::max(a.nplots + 1, std::max(a.nl, a.narrive));
+    hipLaunchKernelGGL(k_batch_init, dim3(nblk(nt)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

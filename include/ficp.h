@@ -100,6 +100,10 @@ int ficp_path_stats(ficp_ctx *ctx, int64_t out[4]);
 /* Replaces the per-call cKDTree(target) of ficp.py:69: uploads the target once and
    builds its uniform grid; reused by every later NN call of this context. */
 int ficp_set_target(ficp_ctx *ctx, const double *tgt, int64_t m, int64_t ld, int32_t md);
+/* The same from device columns (z may be NULL when md == 2): stream-ordered, returns
+   without waiting.  It copies the columns, reduces their bbox and queues the bbox's
+   report to the host, which the next run collects; queue other work (a source reset)
+   after this call and the report lands while it runs. */
 int ficp_set_target_device(ficp_ctx *ctx, const double *x, const double *y, const double *z,
                            int64_t m, int32_t md);
 

@@ -2,20 +2,23 @@
 """Benchmark: FICP iterations/s (BASELINE.json metric) on MI355X.
 
 Workloads (`--workload`, default by GPU count):
-  c3     (default at N=1) one 1M-tree vs 1M-stem plot per GPU, f=0.6, md=3, run() to
-         convergence.  A step = one complete FractionalICP.run() (ficp.py:149-154) on
+  c3     (default at every N) one 1M-tree vs 1M-stem plot per GPU, f=0.6, md=3, run()
+         to convergence.  A step = one complete FractionalICP.run() (ficp.py:149-154) on
          layers already resident in HBM: grid build, copy of the pristine source, the
          device-resident two-stage loop.  value = loop bodies (ficp.py:132-145) per second
          over all ranks ("scaling": "weak", one independent plot per GPU).
-  batch  (default at N>1) C4: 1024 plots of 10k x 10k dealt over the ranks
-         (shard.deal_plots), each rank runs its share in one ficp_run_batch_device per
-         step; value = plot loop bodies per second of the whole job ("scaling": "strong":
-         the 1024 plots are fixed as N grows).  The north star's 1/2/4/8-GPU line.
+  batch  C4: 1024 plots of 10k x 10k dealt over the ranks (shard.deal_plots), each rank
+         runs its share in one ficp_run_batch_device per step; value = plot loop bodies
+         per second of the whole job ("scaling": "strong": the 1024 plots are fixed as N
+         grows).  The north star's 1/2/4/8-GPU batch line.
   c2     100k x 100k, f=0.8, exactly 2 x 25 loop bodies.
   c5     one 8M x 8M plot whose CHM layer is split over the GPUs (RCCL merge per NN call).
 
-Every line carries the other scale's figure as an extra key: at N=1 `batch` (the
-1-GPU point of the batch curve), at N>1 `c3_replicas` (the weak-scaling C3 figure).
+The default line is the same workload at every N: `value` is C3 (BASELINE.json's metric
+config, one plot per GPU), and the C4 strong-scaling batch rides along as the `batch` key
+at every N (1024 plots dealt over the N ranks), so a 1/2/4/8 series holds two consistent
+curves: `value` (C3, weak) and `batch.value` (C4, strong).  At N=1 `batch_shares` adds
+the per-rank shares of N=2/4/8 timed on the one GPU.
 
 Launch: `python bench.py --gpus N` starts N rank processes itself (before anything in
 the parent touches a GPU) and exits with the first failing rank's code; under
@@ -698,22 +701,13 @@ def bench_c5(args, rank, world, local, D, steps, warmup):
     }
 
 
-def bench_dry(args, wl, rank, world, D, steps, warmup):
-    """No GPU work: the launcher, the process group, the plot deal, the timed-region
-    bracket with max-over-ranks, the end-of-run all-gather and the report."""
+def _dry_deal(args, rank, world, D):
+    """The batch's plot deal, checked: every plot dealt once, the end-of-run all-gather
+    of the per-plot records back in batch order.  Returns rank 0's config fields."""
     from coregistrationgame_amd import shard
     nplots = args.plots or BATCH_PLOTS
     deal = shard.deal_plots(np.full(nplots, 1.0), world)
     mine = deal[rank]
-    if D is not None:
-        D.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        pass
-    if D is not None:
-        D.barrier()
-    dt = max(time.perf_counter() - t0, 1e-9)
-    dt_max = D.max([dt])[0] if D is not None else dt
     counts = D.sum([len(mine)]) if D is not None else [len(mine)]
     per_rank = [len(mine)]
     gather_ok = True
@@ -736,15 +730,38 @@ def bench_dry(args, wl, rank, world, D, steps, warmup):
         gather_ok = bool(np.array_equal(allrec["k_last"], np.arange(nplots))
                          and np.array_equal(allrec["n_nn_calls"], owner))
         assert gather_ok
+    return {"workload": "batch", "plots": nplots, "plots_dealt": int(counts[0]),
+            "plots_per_rank": per_rank, "gather_in_order": gather_ok}
+
+
+def bench_dry(args, wl, rank, world, D, steps, warmup):
+    """No GPU work: the launcher, the process group, the plot deal, the timed-region
+    bracket with max-over-ranks, the end-of-run all-gather and the report -- with the
+    same keys as the real line (c3: `value` + the `batch` key at every N)."""
+    if D is not None:
+        D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pass
+    if D is not None:
+        D.barrier()
+    dt = max(time.perf_counter() - t0, 1e-9)
+    dt_max = D.max([dt])[0] if D is not None else dt
+    deal = _dry_deal(args, rank, world, D) if wl in ("batch", "c3") else None
     if rank != 0:
         return None
-    return {"metric": METRIC, "value": 0.0, "unit": "iterations/s", "n_gpus": world, "steps": steps,
+    base = {"metric": METRIC, "value": 0.0, "unit": "iterations/s", "n_gpus": world, "steps": steps,
             "warmup": warmup, "ms_per_step": 1e3 * dt_max / max(steps, 1), "higher_is_better": True,
-            "scaling": "strong" if wl == "batch" else "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "none (dry run)", "dry_run": True,
-            "config": {"workload": wl, "plots": nplots, "plots_dealt": int(counts[0]),
-                       "plots_per_rank": per_rank, "gather_in_order": gather_ok},
+            "vs_baseline": None, "dtype": "f64", "data": "none (dry run)", "dry_run": True,
             "roofline": None, "cpu_baseline": None}
+    if wl == "batch":
+        return dict(base, scaling="strong", config=deal)
+    out = dict(base, scaling="weak",
+               config={"workload": wl, "plots_per_rank": 1,
+                       "parallelism": f"{world} independent plots (1 per GPU)"})
+    if deal is not None and not args.no_extra:
+        out["batch"] = dict(base, scaling="strong", config=deal)
+    return out
 
 
 # ----------------------------------------------------------------------------- main
@@ -753,10 +770,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)  # (C3: ~1.2 ms per step; 10 were noisy)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
-                    help="default: c3 at 1 GPU, batch at more")
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
+                    help="default: c3 at every N (the C4 batch rides along as the `batch` key)")
     ap.add_argument("--no-extra", action="store_true",
-                    help="skip the other scale's figure (batch at N=1, c3_replicas at N>1)")
+                    help="skip the extra figures (`batch`/`batch_shares` on the c3 line, "
+                         "`c3_replicas` on the batch line)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = $OMP_NUM_THREADS or min(16, host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nn-timing", default="first", choices=["first", "all", "none"],
@@ -777,7 +795,7 @@ def main():
     if world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
         sys.exit(2)
-    wl = args.workload or ("c3" if world == 1 else "batch")
+    wl = args.workload
     backend = args.backend if args.backend != "auto" else ("gloo" if args.dry_run else "nccl")
     D = Dist(world, local, backend) if world > 1 else None
     ranks_seen = D.world if D is not None else 1
@@ -796,13 +814,15 @@ def main():
     else:
         out = bench_single(args, wl, rank, world, local, D, args.steps, args.warmup, not args.no_cpu_baseline)
         if not args.no_extra and wl == "c3":
+            # the C4 strong-scaling batch at every N: the 1024 plots dealt over the ranks
             b = bench_batch(args, rank, world, local, D, max(3, args.steps // 2), 1, False)
             if out is not None:
-                out["batch"] = {k: b[k] for k in ("value", "unit", "n_gpus", "ms_per_step", "scaling", "config",
-                                                  "iterations_per_step", "nn_calls_per_step",
+                out["batch"] = {k: b[k] for k in ("metric", "value", "unit", "n_gpus", "ms_per_step", "scaling",
+                                                  "config", "iterations_per_step", "nn_calls_per_step",
                                                   "correspondences_per_s", "roofline", "iteration_roofline",
                                                   "kernel_ms")}
-                out["batch_shares"] = batch_shares(args, local, b)
+                if world == 1:
+                    out["batch_shares"] = batch_shares(args, local, b)
     if out is not None:
         out["ranks_seen"] = ranks_seen
         print(json.dumps(out), flush=True)

@@ -27,9 +27,12 @@ __device__ __forceinline__ double lo_r(unsigned long long klo) {
     return d * d * (1.0 - 1e-15);
 }
 
-// lg2 is the fp64 log2 (ocml, ~1 ulp).  kMarg (log2 units) covers its rounding, the
-// rounding of p log2 k and that of the fp64 prefix sums of the bucket sums the bounds are
-// built from (relative ~1e-12 at 2^13 buckets or 16k rows): 1e-9 leaves a factor ~100.
+// lg2 is fast_log2 below (round 5; before it ocml's fp64 log2, ~1 ulp): absolute error
+// ~1e-13 at |e| ~ 1000, measured over every exponent including subnormals by
+// `tools/selcheck log2` (tests/test_gpu_parity.py::test_fast_log2_error_bound, which fails
+// above kMarg / 100).  kMarg (log2 units) covers that error, the rounding of p log2 k and
+// that of the fp64 prefix sums of the bucket sums the bounds are built from (relative
+// ~1e-12 at 2^13 buckets or 16k rows): 1e-9 leaves a factor ~100.
 // (The float log of round 1 forced 1e-5, which kept every position within ~3.5e-6 of the
 // minimum FRMSD a candidate: 700-2200 rows at C3 whatever the bucket width.)
 constexpr double kMarg = 1e-9;

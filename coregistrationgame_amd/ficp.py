@@ -31,7 +31,8 @@ _PREFETCH = None  # worker threads of the constructor's target prefetch (see __i
 # Instances holding a prefetched (pooled) context that run() has not taken yet: each holds
 # one device context, so constructing many instances before running them would otherwise
 # create that many contexts.  Past the limit the constructor skips the prefetch.
-_PREFETCH_MAX = int(os.environ.get("FICP_PREFETCH_MAX", "4"))
+# FICP_PREFETCH_MAX <= 0 turns the prefetch off (as FICP_PREFETCH=0 does).
+_PREFETCH_MAX = max(int(os.environ.get("FICP_PREFETCH_MAX", "4")), 0)
 _PREFETCH_SLOTS = threading.BoundedSemaphore(max(_PREFETCH_MAX, 1))
 
 
@@ -73,6 +74,20 @@ def _writable_again(arr):
 
 
 class FractionalICP:
+    """ficp.py:5-154's FractionalICP on the MI355X engine.
+
+    Deliberate deviation (the constructor's CHM prefetch): when both layers are plain
+    float64 row arrays, the constructor starts uploading its copy of ``target`` to the
+    device and marks ``self.target`` read-only until ``run()`` takes that upload.  Any
+    other method, ``close()`` or replacing the attribute drops the prefetch and makes the
+    array writable again, so only an in-place edit of ``icp.target`` between the
+    constructor and ``run()`` behaves differently from the reference (it raises
+    ``ValueError: assignment destination is read-only`` instead of being run on).
+    Comparing the layer against a private copy at ``run()`` instead would cost a second
+    24 MB copy and a 24 MB compare per C3 call (~2 ms of a ~3 ms call).
+    ``FICP_PREFETCH=0`` or ``FICP_PREFETCH_MAX=0`` turns the prefetch off.
+    """
+
     def __init__(
         self,
         source,
@@ -101,14 +116,16 @@ class FractionalICP:
         # upload to a pooled context (+ the grid's inputs) starts on a worker thread while
         # the source is copied: run() then finds the CHM layer on the device.
         # FICP_PREFETCH=0: no prefetch.
-        # While the prefetch is pending (until run() takes it, or close()), self.target is
-        # read-only: the device copy must stay the layer run() would read (ficp.py:123), so
-        # an in-place edit raises instead of running on a stale layer.  Assigning a new
-        # array to icp.target (or changing device / nn_mode / match dims) discards the
-        # prefetch, and run() uploads what it finds then.
+        # While the prefetch is pending (until run() takes it, another method or close()
+        # drops it), self.target is read-only: the device copy must stay the layer run()
+        # would read (ficp.py:123), so an in-place edit raises instead of running on a stale
+        # layer (a deliberate deviation, see the class docstring).  Assigning a new array to
+        # icp.target (or changing device / nn_mode / match dims) discards the prefetch, and
+        # run() uploads what it finds then.
         self._prefetch = None
         if (_plain_rows(source) and _plain_rows(target) and len(source) and len(target)
-                and os.environ.get("FICP_PREFETCH", "1") != "0" and _PREFETCH_SLOTS.acquire(blocking=False)):
+                and os.environ.get("FICP_PREFETCH", "1") != "0" and _PREFETCH_MAX > 0
+                and _PREFETCH_SLOTS.acquire(blocking=False)):
             try:
                 self.target = _lib.copy_array(target)
                 self.target.flags.writeable = False
@@ -141,7 +158,10 @@ class FractionalICP:
     def _borrow(self):
         """A pooled library context for one call (_lib.borrowed): the instance holds no
         device state between calls, so a new instance per Join (app.py:658) costs no
-        context creation or device allocation."""
+        context creation or device allocation.  A method other than run() drops a pending
+        prefetch first (self.target must not stay read-only when run() never
+        comes)."""
+        self.close()
         return _lib.borrowed(self.device, self.nn_mode)
 
     def _take_prefetch(self):
@@ -165,16 +185,23 @@ class FractionalICP:
         fut.add_done_callback(_release_done)
         fut.add_done_callback(lambda _f: _writable_again(tgt))
 
-    def close(self):
-        """Releases the constructor's prefetched context, if run() has not used it."""
+    def close(self, wait=True):
+        """Releases the constructor's prefetched context, if run() has not used it, and
+        (wait=True: after the upload has read it) makes self.target writable again."""
         pf, self._prefetch = getattr(self, "_prefetch", None), None
         if pf is not None:
             _PREFETCH_SLOTS.release()
+            if wait:
+                try:
+                    pf[0].exception()  # the upload has finished reading the array
+                except BaseException:
+                    pass
+                _writable_again(pf[1])
             self._discard(pf[0], pf[1])
 
     def __del__(self):
         try:
-            self.close()
+            self.close(wait=False)
         except Exception:
             pass
 

@@ -68,11 +68,27 @@ def test_serpentine_deal_balances_ragged_plots():
     assert sorted(len(d) for d in deal) == [128] * 8
 
 
-def test_default_workload_is_batch_above_one_gpu():
-    r = _run(["--gpus", "3", "--dry-run", "--steps", "1", "--warmup", "0", "--plots", "10"])
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = _json_lines(r.stdout)[0]
-    assert d["config"]["workload"] == "batch" and d["ranks_seen"] == 3
+def test_default_workload_is_the_same_at_every_n():
+    """One headline workload at every N: `value` is C3 (BASELINE.json's
+    metric config, one plot per GPU) at N=1 and N=8, and the C4 strong-scaling batch
+    rides along as the same `batch` key at both, dealt over the N ranks."""
+    lines = {}
+    for n in (1, 8):
+        r = _run(["--gpus", str(n), "--dry-run", "--steps", "1", "--warmup", "0", "--plots", "1024"],
+                 timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = _json_lines(r.stdout)
+        assert len(d) == 1, r.stdout
+        lines[n] = d[0]
+    for n, d in lines.items():
+        assert d["ranks_seen"] == n
+        assert d["config"]["workload"] == "c3" and d["scaling"] == "weak"
+        assert d["batch"]["scaling"] == "strong"
+        assert d["batch"]["config"]["workload"] == "batch"
+        assert d["batch"]["config"]["plots_dealt"] == 1024
+    assert lines[1]["batch"]["config"]["plots_per_rank"] == [1024]
+    assert lines[8]["batch"]["config"]["plots_per_rank"] == [128] * 8
+    assert set(lines[1]) - {"batch_shares"} == set(lines[8]) - {"batch_shares"}
 
 
 def test_gpus_world_size_mismatch_is_an_error():

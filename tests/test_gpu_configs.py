@@ -149,6 +149,12 @@ def test_c5_8M_partitioned_vs_oracle_and_single(oracle):
     k_gpu = np.asarray(icp.last_stats["k"])
     off = np.flatnonzero(k_gpu != otr["k"])
     assert np.all(otr["gap"][off] < K_GAP_PIN_LARGE), (off, otr["gap"][off])
+    # and lands within a few positions of the oracle's k (measured: one k apart; bound
+    # 1e-6 N = 8 positions at 8M rows), so a regression in the size of near-tie
+    # deviations fails here even when the trajectory rejoins
+    if off.size:
+        assert np.abs(k_gpu[off] - otr["k"][off]).max() <= max(2, len(p.source) // 1_000_000), \
+            (off, k_gpu[off], otr["k"][off])
     assert np.all(off + 1 < len(k_gpu)), off
     np.testing.assert_array_equal(k_gpu[off + 1], otr["k"][off + 1])
     assert k_gpu[-1] == otr["k"][-1]

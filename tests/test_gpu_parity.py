@@ -155,6 +155,20 @@ def test_selection_selfcheck():
         assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_fast_log2_error_bound():
+    """The selection bounds' fast fp64 log2 (frmsd_bounds.h fast_log2: frexp, rcp + one
+    Newton step, atanh series) against long-double log2 on the host over 2M random
+    positive doubles of every exponent, all 2098 powers of two (subnormals included) and
+    the mantissa split point: max |error| below kMarg / 100."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "tools" / "selcheck"
+    if not exe.exists():
+        pytest.skip("tools/selcheck not built (make -C coregistrationgame_amd/csrc selcheck)")
+    r = subprocess.run([str(exe), "log2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and " ok" in r.stdout, r.stdout + r.stderr
+
+
 WINCHECK_CASES = [("1000000", "0", "3.0"), ("1000000", "0", "0.95"), ("1000000", "0", "1.3"),
                   ("100000", "1", "3.0"), ("200000", "2", "3.0"), ("300000", "3", "0.95"),
                   ("1000000", "4", "3.0"), ("1000000", "5", "3.0"), ("3000", "0", "3.0"),
@@ -371,14 +385,14 @@ def test_run_vs_oracle_100k(oracle):
     np.testing.assert_array_equal(bits(final[:, 2]), bits(p.source[:, 2]))
 
 
-# every environment switch of libficp.so that changes which kernels run (the only ones
-# left): the fused fit, the two fallback paths the bucket sort takes for
-# layers it cannot plan (global-atomic grid build, 64-bit radix work order), forced here,
-# and the grid density (points per cell: more per cell, more cells per disk scan)
-KNOBS = [{}, {"FICP_FUSE_FIT": "0"}, {"FICP_GRID_ATOMIC": "1"}, {"FICP_WORK_RADIX": "1"},
+# the switches DESIGN.md names as fallbacks: the separate fit pass (FICP_FUSE_FIT=0), the
+# sorts the grid build and the work order fall back to for layers the bucket sort cannot
+# plan (global-atomic grid build, 64-bit radix work order), and the two launch forms that
+# avoid the selection's in-launch hand-offs (FICP_SEL_SPLIT=1: bounds and gather as two
+# kernels; FICP_SEL_BGF=0: the final as its own launch) -- DESIGN §4.2, §4.3, §4.5
+KNOBS = [{}, {"FICP_FUSE_FIT": "0"},
          {"FICP_GRID_ATOMIC": "1", "FICP_WORK_RADIX": "1", "FICP_FUSE_FIT": "0"},
-         {"FICP_GRID_PER_CELL": "4"}, {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_SPLIT": "1", "FICP_FUSE_FIT": "0"},
-         {"FICP_SEL_BGF": "0"}, {"FICP_NN_KEYS": "1"}]
+         {"FICP_SEL_SPLIT": "1"}, {"FICP_SEL_BGF": "0"}]
 
 
 @pytest.mark.parametrize("knobs,md", [(k, 3) for k in KNOBS] + [({}, 2), ({"FICP_GRID_ATOMIC": "1"}, 2)],

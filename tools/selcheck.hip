@@ -38,7 +38,58 @@ static double hfrmsd(long long k, long long N, double S, double lam) {
     return (1.0 / pow(frac, lam)) * sqrt(S / (double)k);
 }
 
+// `selcheck log2`: the bounds' fast log2 (frmsd_bounds.h fb::lg2 / fast_log2) against the
+// host's long-double log2 over random doubles of every exponent (subnormals, |e| ~ 1000),
+// the mantissa split point sqrt(1/2), powers of two and the extremes.  The selection's
+// margin kMarg (1e-9, log2 units) assumes an absolute error far below it: the check
+// fails above kMarg / 100.
+__global__ void k_lg2_probe(const double *x, double *y, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = fb::lg2(x[i]);
+}
+
+static int log2_check() {
+    std::mt19937_64 rng(2025);
+    std::vector<double> x;
+    const double edge[] = {1.0, 2.0, 0.5, 0.70710678118654752, 0.7071067811865475, 0.7071067811865476,
+                           1.4142135623730951, 1.4142135623730950, 1.0 + 1e-16, 1.0 - 1e-16,
+                           1.7976931348623157e308, 2.2250738585072014e-308, 2.2250738585072009e-308,
+                           4.9406564584124654e-324, 1e-320, 3.0, 1e300, 1e-300};
+    for (double v : edge) x.push_back(v);
+    for (int e = -1074; e <= 1023; ++e) x.push_back(ldexp(1.0, e));
+    for (int i = 0; i < 2000000; ++i) {
+        unsigned long long u = rng();
+        u &= 0x7fffffffffffffffULL;                    // positive
+        if ((u >> 52) == 0x7ff) u &= ~(1ULL << 62);    // finite
+        double v;
+        memcpy(&v, &u, 8);
+        if (v > 0.0) x.push_back(v);
+    }
+    const int n = (int)x.size();
+    double *dx, *dy;
+    CK(hipMalloc(&dx, 8 * (size_t)n));
+    CK(hipMalloc(&dy, 8 * (size_t)n));
+    CK(hipMemcpy(dx, x.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+    k_lg2_probe<<<(n + 255) / 256, 256>>>(dx, dy, n);
+    CK(hipGetLastError());
+    std::vector<double> y(n);
+    CK(hipMemcpy(y.data(), dy, 8 * (size_t)n, hipMemcpyDeviceToHost));
+    CK(hipFree(dx));
+    CK(hipFree(dy));
+    double worst = 0.0, worst_x = 0.0, worst_sub = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double err = (double)fabsl((long double)y[i] - log2l((long double)x[i]));
+        if (!(err <= worst)) { worst = err; worst_x = x[i]; }
+        if (x[i] < 2.2250738585072014e-308 && err > worst_sub) worst_sub = err;
+    }
+    const double bound = fb::kMarg / 100.0;
+    printf("log2 n=%d max_abs_err=%.3e at x=%.17g (subnormal max %.3e) bound=%.1e %s\n", n, worst, worst_x,
+           worst_sub, bound, worst < bound ? "ok" : "FAIL");
+    return worst < bound ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && strcmp(argv[1], "log2") == 0) return log2_check();
     const int64_t n = argc > 1 ? atoll(argv[1]) : 1000000;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     const int mode = argc > 3 ? atoi(argv[3]) : 0;

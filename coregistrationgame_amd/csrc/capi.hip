@@ -237,7 +237,8 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             bool want_keys, int warm = 0, const int *skip = nullptr,
             const int *apply_flag = nullptr, bool reduce_range = true, bool want_idx = true,
             const int *reuse = nullptr, bool store_key = true, bool multi = false,
-            const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr) {
+            const uint32_t *fin_orig = nullptr, double *fin_x = nullptr, double *fin_y = nullptr,
+            bool gap_cold = false) {
     NNArgs a{};
     a.fin_orig = fin_orig;
     a.fin_x = fin_x;
@@ -275,6 +276,7 @@ int nn_call(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, co
             a.gap = c->gap.as<gap_t>();
             a.out_bp = c->bp.as<int32_t>();
             a.cert_block = 8;
+            a.gap_cold = gap_cold ? 1 : 0;
         }
         {
             KernelEvents ke(c, P_NN, "nn_grid");  // the NN kernel alone (bench roofline)
@@ -603,7 +605,7 @@ int run_core(ficp_ctx *c, double *sx, double *sy, const double *sz, int64_t n, i
         // (a launch queued behind the loop's end writes the caller-order XY: fin_*)
         CHK(nn_call(c, wx, wy, wz, n, dst->T, true, i == 0 ? 1 : 2, &dst->done, &dst->apply,
                     false, tidx != nullptr, &dst->nn_reuse, !keys_from_r, i >= nn_multi_from,
-                    worig, sx, sy));
+                    worig, sx, sy, i <= 1));
         last_a = i;
         return FICP_OK;
     };

@@ -318,7 +318,6 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         double *qy = work ? b.wy.as<double>() : sy;
         const double *qz = (md == 3) ? (work ? b.wz.as<double>() : sz) : nullptr;
         const uint32_t *worig = work ? b.worig.as<uint32_t>() : nullptr;
-        CHK(b.key.ensure(n * 8));
         CHK(b.gap.ensure(n * sizeof(gap_t)));
         CHK(b.dz2.ensure(n * 8));
         CHK(b.r.ensure(n * 8));
@@ -343,13 +342,22 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
         a.n = n;
         a.idx = nullptr;  // the batch returns XY and per-plot records, not the NN index
         a.r = b.r.as<double>();
-        a.key = b.key.as<unsigned long long>();
+        // the NN stores no sort keys: the selection and the fit derive each from its row's r
+        // (key_of_r, the NN's own operations), 8 B per tree and call less written and read.
+        // FICP_BATCH_KEYS=1: stored keys.
+        const char *bke = getenv("FICP_BATCH_KEYS");
+        const bool keys_stored = bke && atoi(bke) != 0;
+        a.key = nullptr;
         a.cx = b.ccx.as<double>();
         a.cy = b.ccy.as<double>();
         a.tx = tx;
         a.ty = ty;
         a.range = nullptr;
         a.out_bp = b.bp.as<int32_t>();
+        if (keys_stored) {
+            CHK(b.key.ensure(n * 8));
+            a.key = b.key.as<unsigned long long>();
+        }
         // certified reuse of each query's match (k_grid_nn.hip cert_try): the first call
         // of the batch is cold (every plot starts there), the rest are warm
         a.gap = b.gap.as<gap_t>();
@@ -449,18 +457,19 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             if (!bfuse) {
                 ProfScope ps(c, prof ? P_FIT : 0, "batch_fit", u.s);
                 HIPCHK(launch_batch_fit(qx, qy, b.ccx.as<double>(), b.ccy.as<double>(),
-                                        b.key.as<unsigned long long>(), sou, gu, u.np, max_rows,
+                                        a.key, b.r.as<double>(), sou, gu, u.np, max_rows,
                                         allow_refl, su, b.fpart.as<double>() + (size_t)u.p0 * fch,
                                         b.fctr.as<unsigned>() + u.p0, u.s, worig));
             }
             NNArgs au = a;  // this sub-batch's trees: the per-tree arrays from its first row
             au.warm_c = bit > 0 ? 1 : 0;
+            au.gap_cold = bit <= 1 ? 1 : 0;  // (every plot's calls 0 and 1 are batch iterations 0 and 1)
             au.sx = qx + u.r0;
             au.sy = qy + u.r0;
             au.sz = a.sz ? a.sz + u.r0 : nullptr;
             au.n = u.nr;
             au.r = a.r + u.r0;
-            au.key = a.key + u.r0;
+            au.key = a.key ? a.key + u.r0 : nullptr;
             au.cx = a.cx + u.r0;
             au.cy = a.cy + u.r0;
             au.out_bp = a.out_bp + u.r0;
@@ -470,7 +479,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
                 ProfScope ps(c, prof ? P_NN : 0, "nn_grid_batch", u.s);
                 HIPCHK(launch_nn_grid_batch(au, b.plot_of.as<int32_t>() + u.r0, b.grids.as<PlotGrid>(),
                                             b.pts.as<TPt>(), m, b.cell_start.as<int32_t>(), st,
-                                            md, u.s));
+                                            md, u.s, bit));
             }
             BatchStepArgs su_step = step;  // this sub-batch's grids, counter, flag and trace
             su_step.grids = gu;  // indexed by the plot within the sub-batch (fit pivot)
@@ -479,7 +488,7 @@ int batch_core(ficp_ctx *c, int32_t nplots, const int64_t *so_h, double *sx, dou
             su_step.flag = flag;
             {
                 ProfScope ps(c, prof ? P_FRAC : 0, "batch_select", u.s);
-                HIPCHK(launch_batch_select(b.key.as<unsigned long long>(), b.r.as<double>(), sou, u.np,
+                HIPCHK(launch_batch_select(a.key, b.r.as<double>(), sou, u.np,
                                            max_rows, b.lams.as<double>(), su, ws, u.s,
                                            bfuse ? &su_step : nullptr));
             }

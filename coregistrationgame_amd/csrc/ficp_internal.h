@@ -323,6 +323,10 @@ struct NNArgs {
     // fin_x[fin_orig[p]] = sx[p] (k_scatter_xy's work, no launch or host round trip of its own)
     const uint32_t *fin_orig;
     double *fin_x, *fin_y;
+    // grid kernels with gap: the cold call stores no G and the first warm call loads none
+    // (every G would be 0: that call scans every query with its cover anyway), 4 B per
+    // query less written and read.  Set on both calls or on neither.
+    int gap_cold;
 };
 
 // k_scatter_xy's work for rows [p0, p0 + cnt) of the work order
@@ -946,10 +950,11 @@ hipError_t launch_batch_grid_count(const double *tx, const double *ty, int64_t m
                                    const int32_t *tplot, const PlotGrid *grids, int32_t *cell_of,
                                    int32_t *counts, hipStream_t s);
 // NN of every live plot's trees against its own CHM grid; idx = index in the concatenated
-// CHM layer.  Applies states[p].T first where states[p].apply.
+// CHM layer.  Applies states[p].T first where states[p].apply.  call: the batch iteration
+// (0 = the cold call; the first warm calls scan most queries and run one query per thread)
 hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
                                 const TPt *pts, int64_t m, const int32_t *cell_start,
-                                const PlotState *st, int md, hipStream_t s);
+                                const PlotState *st, int md, hipStream_t s, int64_t call = 0);
 // k_batch_init: the offsets and lambdas from coherent pinned staging (so_h, to_h, lam_h)
 // into their device copies, the arrival counters zeroed, every plot's state initialised
 struct BatchInitArgs {
@@ -986,10 +991,11 @@ hipError_t launch_plot_sort(const PlotSortJob &a, const PlotSortJob *b, const Pl
 int batch_fit_chunks(int64_t max_rows);
 // part: nplots * batch_fit_chunks(max_rows) * 8 doubles; ctr: nplots arrival counters
 // (atomics only: zero them once per allocation with launch_batch_fit_ctr_zero)
+// key == nullptr: each row's key is derived from r (key_of_r)
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
-                            const double *cy, const unsigned long long *key, const int64_t *so,
-                            const PlotGrid *grids, int nplots, int64_t max_rows, int allow_refl,
-                            PlotState *st, double *part, unsigned *ctr, hipStream_t s,
+                            const double *cy, const unsigned long long *key, const double *r,
+                            const int64_t *so, const PlotGrid *grids, int nplots, int64_t max_rows,
+                            int allow_refl, PlotState *st, double *part, unsigned *ctr, hipStream_t s,
                             const uint32_t *worig = nullptr);
 hipError_t launch_batch_fit_ctr_zero(unsigned *ctr, int n, hipStream_t s);
 // Per-plot FRMSD-optimal fraction (ficp.py:73-86), one workgroup per live plot: bucket
@@ -1021,6 +1027,7 @@ struct BatchStepArgs {
     const uint32_t *worig = nullptr;  // the fit's tie-break at the threshold key (as above)
 };
 hipError_t launch_batch_live(int nplots, const PlotState *st, int *flag, hipStream_t s);
+// key == nullptr: the keys are derived from r (key_of_r), as the NN that stored r computed them
 hipError_t launch_batch_select(const unsigned long long *key, const double *r, const int64_t *so,
                                int nplots, int64_t max_rows, const double *lambdas,
                                PlotState *st, BatchSelScratch ws, hipStream_t s,

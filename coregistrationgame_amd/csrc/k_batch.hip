@@ -390,6 +390,8 @@ struct BatchStep {
     long long *trace;            // per-call k trace, max_trace per plot of this launch (nullable)
     int max_trace;
     const uint32_t *worig;       // caller row of each work row (nullable: caller order)
+    const double *r;             // the NN call's r (the keys are derived from it when the
+                                 // NN stored none: key == nullptr)
 };
 
 // thread 0 of plot p's workgroup, its state final for this call: one agent-scope atomic
@@ -500,7 +502,7 @@ __device__ __forceinline__ void plot_step_fit(PlotState *st, const PlotState *ps
         for (int u = 0; u < FU; ++u) {
             const int64_t i = i0 + (int64_t)u * NT;
             const bool in = i < e;
-            kv[u] = in ? key[i] : ~0ULL;
+            kv[u] = in ? (key ? key[i] : key_of_r(bs.r[i])) : ~0ULL;
             xs[u] = in ? bs.sx[i] : 0.0;
             ys[u] = in ? bs.sy[i] : 0.0;
             xt[u] = in ? bs.cx[i] : 0.0;
@@ -550,8 +552,8 @@ __device__ __forceinline__ void plot_step_fit(PlotState *st, const PlotState *ps
         }                                                                           \
     } else {                                                                        \
         for (int64_t i = b + t; i < e; i += ST) {                                   \
-            const u64 kk = key[i];                                                  \
             const double rv = r[i];                                                 \
+            const u64 kk = key ? key[i] : key_of_r(rv);                             \
             constexpr int q = 0;                                                    \
             (void)i;                                                                \
             (void)q;                                                                \
@@ -630,12 +632,21 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
     constexpr bool OCACHE = CACHED && RPT <= 20;
     uint32_t oc[OCACHE ? RPT : 1];
     if (CACHED) {
+        // (key == nullptr: the NN stored no keys, each is derived from its row's r --
+        // key_of_r, the NN's own operations -- once the loads have issued)
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
             const int64_t i = b + t + (int64_t)q * ST;
-            kc[q] = i < e ? key[i] : ~0ULL;
+            kc[q] = (key && i < e) ? key[i] : ~0ULL;
             if (BSEL_RCACHE) rc[q] = i < e ? r[i] : INFINITY;
             if (OCACHE) oc[q] = (i < e && ws.worig) ? ws.worig[i] : (uint32_t)i;
+        }
+        if (!key) {
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                const int64_t i = b + t + (int64_t)q * ST;
+                if (i < e) kc[q] = key_of_r(BSEL_RCACHE ? rc[q] : r[i]);
+            }
         }
     }
     BSEL_T(0);
@@ -953,7 +964,7 @@ __global__ __launch_bounds__(KST) BSEL_WPE void k_batch_select(const u64 *__rest
 constexpr int FCH = BB * 8;
 __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double *sy,
                                                   const double *cx, const double *cy,
-                                                  const unsigned long long *key,
+                                                  const unsigned long long *key, const double *r,
                                                   const int64_t *so, const PlotGrid *grids,
                                                   int allow_refl, PlotState *st, double *part,
                                                   unsigned *ctr, int gmax, const uint32_t *worig) {
@@ -984,7 +995,7 @@ __global__ __launch_bounds__(BB) void k_batch_fit(const double *sx, const double
         for (int u = 0; u < FU; ++u) {
             const int64_t i = i0 + (int64_t)u * BB;
             const bool in = i < e;
-            kv[u] = in ? key[i] : ~0ULL;
+            kv[u] = in ? (key ? key[i] : key_of_r(r[i])) : ~0ULL;
             xs[u] = in ? sx[i] : 0.0;
             ys[u] = in ? sy[i] : 0.0;
             xt[u] = in ? cx[i] : 0.0;
@@ -1340,14 +1351,14 @@ int batch_fit_chunks(int64_t max_rows) {
 }
 
 hipError_t launch_batch_fit(const double *sx, const double *sy, const double *cx,
-                            const double *cy, const unsigned long long *key, const int64_t *so,
-                            const PlotGrid *grids, int nplots, int64_t max_rows, int allow_refl,
-                            PlotState *st, double *part, unsigned *ctr, hipStream_t s,
+                            const double *cy, const unsigned long long *key, const double *r,
+                            const int64_t *so, const PlotGrid *grids, int nplots, int64_t max_rows,
+                            int allow_refl, PlotState *st, double *part, unsigned *ctr, hipStream_t s,
                             const uint32_t *worig) {
     if (nplots <= 0) return hipSuccess;
     const int gmax = batch_fit_chunks(max_rows);
     hipLaunchKernelGGL(k_batch_fit, dim3((unsigned)nplots * (unsigned)gmax), dim3(BB), 0, s, sx, sy,
-                       cx, cy, key, so, grids, allow_refl, st, part, ctr, gmax, worig);
+                       cx, cy, key, r, so, grids, allow_refl, st, part, ctr, gmax, worig);
     return hipGetLastError();
 }
 
@@ -1412,6 +1423,7 @@ hipError_t launch_batch_select(const unsigned long long *key, const double *r, c
         bs.trace = step->trace;
         bs.max_trace = step->max_trace;
         bs.worig = step->worig;
+        bs.r = r;
     }
     // (1024-thread workgroups for plots fewer than the CUs measured slower: 128 plots 0.53 vs
     // 0.38 ms of selection per batch run -- 128 VGPRs with spills, 16-wave barriers; round 5

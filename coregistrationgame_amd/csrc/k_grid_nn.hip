@@ -632,7 +632,7 @@ __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, con
     const double d2w = warm_d2<MD>(a, i, qx, qy);
     const double mx = qx - ox, my = qy - oy;
     mv = sqrt(mx * mx + my * my);
-    const double G = a.gap[i] - mv - eps;
+    const double G = (a.gap_cold ? 0.0 : (double)a.gap[i]) - mv - eps;
     if (!(d2w < INFINITY && sqrt(d2w) + eps < G)) return false;
     NNST(2);
     a.gap[i] = gap_rd(G);
@@ -898,7 +898,7 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
         wx[q] = v ? a.cx[i] : 0.0;
         wy[q] = v ? a.cy[i] : 0.0;
         wz[q] = (v && MD == 3) ? a.dz2[i] : 0.0;
-        gp[q] = v ? a.gap[i] : 0.0f;
+        gp[q] = (v && !a.gap_cold) ? a.gap[i] : 0.0f;
     }
     unsigned pend = 0;
 #pragma unroll
@@ -1002,7 +1002,7 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g,
                 // call, which scans every query with its cover.  A cold scan with the cover
                 // cost more than that first warm call saved (C3: +1.8 % without it)
                 nn_query<MD>(a, g, S, i, T, kmin_c, kmax);
-                a.gap[i] = 0;
+                if (!a.gap_cold) a.gap[i] = 0;
             } else if (a.gap) {
                 nn_query_cert<MD>(a, g, S, i, T, kmin_c, kmax);
             } else {
@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
             // call, which scans every query with its cover.  A cold scan with the cover
             // cost more than that first warm call saved (C3: +1.8 % without it)
             nn_query<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
-            a.gap[i] = 0;
+            if (!a.gap_cold) a.gap[i] = 0;
         } else if (a.gap) {
             nn_query_cert<MD>(a, g, stems_of(g.pts, g.m), i, T, kmin_c, kmax);
         } else {
@@ -1198,7 +1198,7 @@ __device__ __forceinline__ void nn_batch_rows(const NNArgs &a, const int32_t *__
     } else if (live) {
         const GridView g = plot_view(grids[p], pts, cell_start, m);
         nn_query<MD>(a, g, S, i, T, kmin_c, kmax);
-        if (a.gap) a.gap[i] = 0;  // the cold call stores no certificate (k_nn_grid)
+        if (a.gap && !a.gap_cold) a.gap[i] = 0;  // the cold call stores no certificate (k_nn_grid)
     }
 }
 
@@ -1210,6 +1210,36 @@ __global__ __launch_bounds__(256) NNB_WPE void k_nn_grid_batch(NNArgs a, const i
                                                        const PlotState *__restrict__ st) {
     nn_batch_rows<MD>(a, plot_of, grids, pts, m, cell_start, st,
                       xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x);
+}
+
+// The cold batch call, one query per thread: a workgroup whose 256 trees belong to one plot
+// (10k-tree plots: ~39 in 40) reads that plot's state and grid once, as scalars, and runs
+// the single-plot kernel's body against it (k_nn_grid's cold form: the plain scan, G = 0);
+// a workgroup that straddles plots takes k_nn_grid_batch's per-row form.  The per-row
+// form kept every lane's grid view in VGPRs behind two dependent per-lane loads (plot id,
+// then grid): the cold launch ran ~2x the single-plot cold call's time per query.
+#ifndef FICP_NNBU_WPE
+#define FICP_NNBU_WPE 7
+#endif
+template <int MD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FICP_NNBU_WPE, FICP_NNBU_WPE)))
+void k_nn_grid_batch_u(NNArgs a, const int32_t *__restrict__ plot_of, const PlotGrid *__restrict__ grids,
+                       const TPt *__restrict__ pts, int64_t m, const int32_t *__restrict__ cell_start,
+                       PlotState *__restrict__ st) {
+    const int64_t i0 = xcd_block(blockIdx.x, gridDim.x) * 256;
+    const int64_t ilast = min(i0 + 256, a.n) - 1;
+    const int p0 = plot_of[i0], p1 = plot_of[ilast];
+    if (p0 == p1) {  // (uniform)
+        if (st[p0].phase == PH_DONE) return;
+        NNArgs b = a;
+        b.T = st[p0].T;
+        b.apply_flag = &st[p0].apply;
+        b.skip = nullptr;
+        b.reuse = nullptr;
+        nn_grid_body<MD, true, 1, FICP_NN_SKIP_SAME != 0>(b, plot_view(grids[p0], pts, cell_start, m), i0);
+        return;
+    }
+    nn_batch_rows<MD>(a, plot_of, grids, pts, m, cell_start, st, i0 + threadIdx.x);
 }
 
 // Warm batch calls, QPT queries per thread (the single-plot k_nn_grid_q's form): a
@@ -1802,20 +1832,26 @@ hipError_t launch_scatter_xy(const uint32_t *worig, const double *wx, const doub
 
 hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const PlotGrid *grids,
                                 const TPt *pts, int64_t m, const int32_t *cell_start,
-                                const PlotState *st, int md, hipStream_t s) {
+                                const PlotState *st, int md, hipStream_t s, int64_t call) {
     if (a.n == 0) return hipSuccess;
     // warm calls: QPT queries per thread from FICP_BATCH_QPT_MIN trees per launch on (default
     // 2M: ~2,000 workgroups of 1024 trees, enough to hide their latency chains; at 128 plots
     // of 10k, 640k trees per sub-batch, the 1-query form measured 39 vs 55 us per launch,
-    // at 1024 plots the QPT form 264 vs 316 us); FICP_BATCH_QPT=0: never
+    // at 1024 plots the QPT form 264 vs 316 us), and from the batch iteration
+    // FICP_BATCH_QPT_FROM on: the first warm calls scan most queries with their cover, which
+    // wants one query per thread (the single-plot loop's FICP_NN_QPT_FROM); FICP_BATCH_QPT=0:
+    // never.  The other calls run k_nn_grid_batch_u (one query per thread, the plot's grid
+    // read once per workgroup); FICP_BATCH_COLD_U=0: the per-row k_nn_grid_batch instead.
     const char *qe = getenv("FICP_BATCH_QPT");
     const char *qm = getenv("FICP_BATCH_QPT_MIN");
+    const char *qf = getenv("FICP_BATCH_QPT_FROM");
+    const char *ue = getenv("FICP_BATCH_COLD_U");
     const int64_t qpt_min = qm ? atoll(qm) : (int64_t)2000000;
-    // (the cold call stays on the per-row kernel: through this one, with the batch work
-    // order, C4 measured 1.25M against 1.29M plot-it/s -- its long cold scans want the
-    // parallelism of one query per thread)
-    if (!(qe && atoi(qe) == 0) && a.n >= qpt_min && a.warm_c && a.gap && a.cert_block) {
-        PlotState *stw = const_cast<PlotState *>(st);
+    const int64_t qpt_from = qf ? atoll(qf) : (int64_t)4;  // C4 1,024 plots: 1.373M vs 1.351M (1)
+    const bool use_u = !(ue && atoi(ue) == 0);
+    PlotState *stw = const_cast<PlotState *>(st);
+    if (!(qe && atoi(qe) == 0) && a.n >= qpt_min && call >= qpt_from && a.warm_c && a.gap &&
+        a.cert_block) {
         const dim3 gq(nblk(a.n, 256 * QPT));
         if (md == 3)
             hipLaunchKernelGGL(k_nn_grid_batch_q<3>, gq, dim3(256), 0, s, a, plot_of, grids, pts, m,
@@ -1823,6 +1859,13 @@ hipError_t launch_nn_grid_batch(const NNArgs &a, const int32_t *plot_of, const P
         else
             hipLaunchKernelGGL(k_nn_grid_batch_q<2>, gq, dim3(256), 0, s, a, plot_of, grids, pts, m,
                                cell_start, stw);
+    } else if (use_u) {
+        if (md == 3)
+            hipLaunchKernelGGL(k_nn_grid_batch_u<3>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
+                               pts, m, cell_start, stw);
+        else
+            hipLaunchKernelGGL(k_nn_grid_batch_u<2>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
+                               pts, m, cell_start, stw);
     } else if (md == 3)
         hipLaunchKernelGGL(k_nn_grid_batch<3>, dim3(nblk(a.n)), dim3(256), 0, s, a, plot_of, grids,
                            pts, m, cell_start, st);

@@ -10,7 +10,7 @@ for rep in 1 2; do
     case "$v" in
       default) ;;
       *=*) envs="$v" ;;  # NAME=VALUE: the default library under that environment
-      *) export FICP_LIB=$PWD/tools/ab/libficp_$v.so ;;
+      *) export FICP_LIB=$PWD/tools/abv/libficp_$v.so ;;
     esac
     env $envs timeout -k 10 200 python bench.py --no-cpu-baseline ${BENCH_ARGS} > "gpurun_out/ab/$v.log" 2>&1 || { echo "$v failed"; tail -5 "gpurun_out/ab/$v.log"; exit 1; }
     python3 -c "

@@ -2,7 +2,7 @@
 # Batch (C4) A/B on one GPU: for every plot count in $PLOTS (default "128 1024") run the
 # batch bench under the default library and each variant, alternating, twice.
 # A variant is NAME=VALUE (the default library under that environment) or a name of
-# tools/ab/libficp_<name>.so (tools/build_variant.sh).
+# tools/abv/libficp_<name>.so (tools/build_variant.sh).
 # usage: PLOTS="128 256" tools/batch_ab.sh FICP_BATCH_STREAMS=1 myvariant
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 out=gpurun_out/batch_ab
@@ -15,7 +15,7 @@ for rep in 1 2; do
       case "$v" in
         default) ;;
         *=*) envs="$v" ;;
-        *) export FICP_LIB=$PWD/tools/ab/libficp_$v.so ;;
+        *) export FICP_LIB=$PWD/tools/abv/libficp_$v.so ;;
       esac
       log="$out/b${p}_${v//[^A-Za-z0-9_]/_}.log"
       env $envs timeout -k 10 200 python bench.py --workload batch --plots "$p" --steps ${STEPS:-10} \

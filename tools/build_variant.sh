@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
 out=tools/ab/build_$name
-mkdir -p $out
+mkdir -p $out tools/abv
 # VARIANT_SRC=<dir>: build from another copy of csrc (e.g. a git checkout of an older round)
 cd "${VARIANT_SRC:-coregistrationgame_amd/csrc}"
 SRCS=$(sed -n 's/^SRCS = //p' Makefile)
@@ -17,5 +17,5 @@ for f in $SRCS; do
 done
 for p in $pids; do wait $p || { echo "compile failed"; exit 1; }; done
 cd "$OLDPWD"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o tools/ab/libficp_$name.so $out/*.o
-echo tools/ab/libficp_$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o tools/abv/libficp_$name.so $out/*.o
+echo tools/abv/libficp_$name.so

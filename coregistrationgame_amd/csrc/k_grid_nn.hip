@@ -1219,7 +1219,7 @@ __global__ __launch_bounds__(256) NNB_WPE void k_nn_grid_batch(NNArgs a, const i
 // form kept every lane's grid view in VGPRs behind two dependent per-lane loads (plot id,
 // then grid): the cold launch ran ~2x the single-plot cold call's time per query.
 #ifndef FICP_NNBU_WPE
-#define FICP_NNBU_WPE 7
+#define FICP_NNBU_WPE 6  // 72 VGPRs with 73 spilled at 7; 6: 128 plots +1.5-2.8 %, 1024 +0.4 % (5: -3 %)
 #endif
 template <int MD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FICP_NNBU_WPE, FICP_NNBU_WPE)))

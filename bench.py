@@ -445,6 +445,25 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
     ps1 = ctx.path_stats()
     ctx.profile_enable(0)
     prof = json.loads(ctx.profile_report())
+    # sustained: the same step back to back for --sustain-s seconds after the timed region
+    # (not part of `value`): its rate beside the K-step one, and seconds of busy GPU that a
+    # sampling utilisation monitor can see (the K timed steps last ~1.2 ms each)
+    sus = None
+    if args.sustain_s > 0 and wl == "c3":
+        barrier()
+        t1 = time.perf_counter()
+        k_s = f_s = 0
+        while True:
+            f_s += step()["n_fits"]
+            k_s += 1
+            if k_s % 64 == 0:
+                ctx.synchronize()
+                if time.perf_counter() - t1 >= args.sustain_s:
+                    break
+        barrier()
+        ds = time.perf_counter() - t1
+        sus = {"value": f_s / ds, "unit": "iterations/s", "seconds": ds, "steps": k_s,
+               "note": "rank-local: the timed step back to back after the timed region, not part of value"}
     dt_max, fits_all, calls_all, reused_all = dt, fits, calls, reused
     if D is not None:
         dt_max = D.max([dt])[0]
@@ -487,6 +506,7 @@ def bench_single(args, wl, rank, world, local, D, steps, warmup, with_cpu):
                 "launches": timed_calls, "timed_launches_incl_noop": nn["count"],
                 "algorithmic_bytes_per_launch": bytes_launch}),
             "kernel_ms": prof,
+            "sustained": sus,
             # the whole loop body against SURVEY.md §8(d)'s per-iteration bytes (k = n: the
             # upper bound of the fit term), beside the dominant kernel's line
             "iteration_roofline": {"bytes_per_iteration": ib, "achieved": ib * fits_all / dt_max / 1e9,
@@ -770,6 +790,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)  # (C3: ~1.2 ms per step; 10 were noisy)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sustain-s", type=float, default=4.0,
+                    help="C3: seconds of back-to-back steps after the timed region (`sustained`; 0: none)")
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
                     help="default: c3 at every N (the C4 batch rides along as the `batch` key)")
     ap.add_argument("--no-extra", action="store_true",

@@ -19,6 +19,6 @@ fi
 timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS} > "$out/bench.log" 2>&1 || { echo "bench rc=$?"; tail -20 "$out/bench.log"; exit 1; }
 tail -1 "$out/bench.log" | cut -c1-400
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
-    python3 bench.py --no-cpu-baseline ${BENCH_ARGS} > "$out/bench_rocprof.log" 2>&1 || { echo "rocprof rc=$?"; exit 1; }
+    python3 bench.py --no-cpu-baseline --sustain-s 0 ${BENCH_ARGS} > "$out/bench_rocprof.log" 2>&1 || { echo "rocprof rc=$?"; exit 1; }
 python3 tools/timeline.py "$out/prof/run_kernel_trace.csv" > "$out/timeline.txt" 2>&1
 cat "$out/timeline.txt" | head -30

@@ -13,7 +13,7 @@ IFS='|' read -ra GROUPS_ARR <<< "$groups"
 for ctr in "${GROUPS_ARR[@]}"; do
     i=$((i + 1))
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$out/p$i" -o run -- \
-        python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" > "$out/p$i.log" 2>&1 || exit $?
+        python3 bench.py --no-cpu-baseline --sustain-s 0 --steps 2 --warmup 1 "$@" > "$out/p$i.log" 2>&1 || exit $?
 done
 python3 tools/pmc_summary.py "$out" > "$out/summary.json"
 cat "$out/summary.json"

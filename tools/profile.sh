@@ -7,7 +7,7 @@ out=gpurun_out/$name
 mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- \
-    python3 bench.py --no-cpu-baseline "$@" > "$out/bench.log" 2>&1
+    python3 bench.py --no-cpu-baseline --sustain-s 0 "$@" > "$out/bench.log" 2>&1
 rc=$?
 grep '^{' "$out/bench.log" | tail -1
 find "$out" -name '*kernel_stats.csv' -exec head -30 {} \;

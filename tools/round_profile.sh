@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 timeout -k 10 900 python3 bench.py > "$out/bench.log" 2>&1 || { echo "bench failed"; tail -5 "$out/bench.log"; exit 1; }
 grep '^{' "$out/bench.log" | tail -1 > "$out/bench.json"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
-    python3 bench.py --no-cpu-baseline > "$out/bench_under_rocprof.log" 2>&1 || { echo "rocprof bench failed"; exit 1; }
+    python3 bench.py --no-cpu-baseline --sustain-s 0 > "$out/bench_under_rocprof.log" 2>&1 || { echo "rocprof bench failed"; exit 1; }
 find "$out/prof" -name '*kernel_stats.csv' -exec cp {} "$out/kernel_stats.csv" \;
 PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|TCC_HIT_sum TCC_MISS_sum TA_TA_BUSY_sum TD_TD_BUSY_sum|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU|SQ_ACTIVE_INST_VMEM SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU SQ_LEVEL_WAVES SQ_INST_LEVEL_VMEM SQ_INSTS_VALU_FLOPS_FP64" \
     bash tools/pmc.sh "$tag/pmc" --no-extra > "$out/pmc.log" 2>&1 || { echo "pmc failed"; tail -5 "$out/pmc.log"; exit 1; }

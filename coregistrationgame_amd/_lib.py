@@ -348,11 +348,21 @@ class Context:
                                    C.byref(st)))
         return _stats_dict(st, keep, len(src))
 
+    def _lam_arg(self, lambdas):
+        """(count, pointer) of the stage lambdas, the converted array cached while the same
+        values come again (a ctypes pointer costs ~4 us of host time per call)."""
+        key = tuple(float(v) for v in lambdas)
+        c = getattr(self, "_lam_cache", None)
+        if c is None or c[0] != key:
+            arr = np.array(key, dtype=np.float64)
+            c = self._lam_cache = (key, arr, _p(arr))
+        return len(key), c[2]
+
     def run_device(self, x_ptr: int, y_ptr: int, z_ptr: int, n: int, lambdas, threshold: float,
                    max_iterations: int, allow_reflection: bool = False):
-        lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+        nl, lp = self._lam_arg(lambdas)
         st, keep = _make_stats(n, False, False, 0)
-        _check(lib().ficp_run_device(self.h, _vp(x_ptr), _vp(y_ptr), _vp(z_ptr or 0), int(n), len(lam), _p(lam),
+        _check(lib().ficp_run_device(self.h, _vp(x_ptr), _vp(y_ptr), _vp(z_ptr or 0), int(n), nl, lp,
                                      float(threshold), int(max_iterations), int(bool(allow_reflection)),
                                      C.byref(st)))
         return _stats_dict(st, keep, n)
@@ -693,7 +703,7 @@ def _stats_dict(st, keep, n):
     nf = st.n_fits
     out = dict(n_nn_calls=nc, n_nn_reused=st.n_nn_reused, n_fits=nf, iters=(st.iters[0], st.iters[1]), k_last=st.k_last,
                frmsd_last=(st.frmsd_last[0], st.frmsd_last[1]),
-               T_total=np.array(st.T_total[:]).reshape(3, 3), gpu_ms=st.gpu_ms,
+               T_total=np.frombuffer(st.T_total, dtype=np.float64).reshape(3, 3).copy(), gpu_ms=st.gpu_ms,
                lib_host_ms=dict(upload=st.host_ms[0], loop=st.host_ms[1], result=st.host_ms[2]),
                path=("small" if st.path == 1 else "loop"))
     if keep:

@@ -186,7 +186,10 @@ __global__ __launch_bounds__(BT) void k_bs_scatter(BSPair P) {
     if (sl == 0 && threadIdx.x == 0) base_out[p.nbk] = (uint32_t)n;
     __syncthreads();
     const int64_t i0 = (int64_t)sl * p.per, i1 = min(n, i0 + p.per);
-    constexpr int U = 8;  // points in flight per thread (the loop was load-latency bound)
+#ifndef FICP_BS_SU
+#define FICP_BS_SU 8
+#endif
+    constexpr int U = FICP_BS_SU;  // points in flight per thread (the loop was load-latency bound)
     for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)U * BT) {
         double xv[U], yv[U], zv[U];
 #pragma unroll
@@ -360,10 +363,17 @@ BSortPlan bsort_plan(int64_t n, int64_t nkeys) {
     p.nkeys = nkeys;
     int kb = 0;
     while (kb < 40 && (((int64_t)1) << kb) < nkeys) ++kb;
-    // FICP_BS_BPTS / FICP_BS_SLICE: bucket and slice sizes (A/B runs)
+    // -DFICP_BS_BPTS / -DFICP_BS_SLICE (and -DFICP_BS_SU, k_bs_scatter's points in flight
+    // per thread): compile-time sizes for A/B builds (tools/build_variant.sh)
     // ~256 points per coarse bucket, slices of 4096 points (512-1024 and 8K-16K within 1 %)
-    constexpr int64_t bpts = 256;
-    constexpr int64_t slice = 4096;
+#ifndef FICP_BS_BPTS
+#define FICP_BS_BPTS 256
+#endif
+    constexpr int64_t bpts = FICP_BS_BPTS;
+#ifndef FICP_BS_SLICE
+#define FICP_BS_SLICE 4096
+#endif
+    constexpr int64_t slice = FICP_BS_SLICE;
     int want = 0;
     while (want < BMAXB_LOG && (bpts << want) < n) ++want;
     p.fs = std::max(0, kb - want);

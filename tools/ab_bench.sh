@@ -1,5 +1,5 @@
 #!/bin/bash
-# Bench the default library against variants (tools/ab/libficp_<name>.so), alternating
+# Bench the default library against variants (tools/abv/libficp_<name>.so), alternating
 # runs; prints it/s and NN launch time.  usage: tools/ab_bench.sh name1 [name2 ...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out/ab

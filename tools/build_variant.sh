@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a variant of libficp.so with extra compile flags, for A/B runs through FICP_LIB:
-# usage: tools/build_variant.sh <name> <flags...>  ->  tools/ab/libficp_<name>.so
+# usage: tools/build_variant.sh <name> <flags...>  ->  tools/abv/libficp_<name>.so (objects in tools/ab/)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift

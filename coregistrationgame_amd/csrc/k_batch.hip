@@ -1144,6 +1144,10 @@ __device__ __forceinline__ uint32_t ps_st_key(int cx, int cy, int gx) {  // (k_b
     return (stl << 6) | ((uint32_t)(cy & 7) << 3) | (uint32_t)(cx & 7);
 }
 
+// an LDS-only barrier: __syncthreads() also waits for every outstanding global access
+// (vmcnt(0)), stores included, so each stage hand-off below waited for the previous
+// column's global stores to complete
+#define PS_LDS_SYNC() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 __global__ __launch_bounds__(PS_T) void k_plot_sort(PlotSortJob A, PlotSortJob B, const PlotGrid *grids,
                                                     int nplots) {
     const bool jb = (int)blockIdx.x >= nplots;
@@ -1207,21 +1211,40 @@ __global__ __launch_bounds__(PS_T) void k_plot_sort(PlotSortJob A, PlotSortJob B
         for (int j = 0; j < PS_KPT; ++j) {
             const int k = t * PS_KPT + j;
             s_start[k] = run;
-            // the grid's cell starts (global rows; the cell after the plot's last one is the
-            // next plot's first: the same value from both plots)
-            if (J.mode == 0 && k <= nk) J.cell_start[g.cell_base + k] = (int32_t)(b + run);
             run += c[j];
         }
     }
     __syncthreads();
+    // the grid's cell starts (global rows; the cell after the plot's last one is the next
+    // plot's first: the same value from both plots), coalesced from LDS before the bins
+    // fill: stored from the scan's registers, each lane's 12 consecutive keys put every
+    // lane of a store 48 B from its neighbour (~5 us per plot of uncoalesced stores)
+    if (J.mode == 0) {  // (uniform per workgroup)
+        for (int k = t; k <= nk; k += PS_T) J.cell_start[g.cell_base + k] = (int32_t)(b + s_start[k]);
+        PS_LDS_SYNC();
+    }
+    // a point alone in its bin (most of them) has its final position already: the slot
+    // its atomic returned (re-reading the bin's bounds for every point took ~4 us per plot)
+    int slot[PS_R];
 #pragma unroll
-    for (int u = 0; u < PS_R; ++u)
-        if (key[u] >= 0) s_idx[atomicAdd(&s_start[key[u]], 1u)] = (uint16_t)(t + u * PS_T);
+    for (int u = 0; u < PS_R; ++u) {
+        slot[u] = -1;
+        if (key[u] >= 0) {
+            const uint32_t c = cnt_of(key[u]);
+            const uint32_t sl = atomicAdd(&s_start[key[u]], 1u);
+            s_idx[sl] = (uint16_t)(t + u * PS_T);
+            slot[u] = c == 1u ? (int)sl : -2;
+        }
+    }
     __syncthreads();
     // final position of each point (its rank inside its bin by row), in key[]'s registers
 #pragma unroll
     for (int u = 0; u < PS_R; ++u) {
         if (key[u] < 0) continue;
+        if (slot[u] >= 0) {
+            key[u] = slot[u];
+            continue;
+        }
         const int i = t + u * PS_T;
         const uint32_t be = s_start[key[u]], bs = be - cnt_of(key[u]);
         uint32_t rank = 0;
@@ -1232,46 +1255,64 @@ __global__ __launch_bounds__(PS_T) void k_plot_sort(PlotSortJob A, PlotSortJob B
     // the outputs field by field through the stage: each point's value reloaded (coalesced,
     // L2-hot) and stored into the stage at its final position, then coalesced global stores
     // (scattered 8-B global stores: every lane of a store on its own cache line).  Grid
-    // records (32 B: x, y, z, row) in two halves of positions, 16 B per record per pass.
+    // records (32 B: x, y, z, row) in two halves of positions, 16 B per record per pass: the
+    // columns of a field pair are loaded once for both halves (reloaded per half, every
+    // grid workgroup waited for four load round trips more).
     double *sd = (double *)s_mem;
     uint32_t *su = (uint32_t *)s_mem;
     const int half = PS_MAXN / 2;
-    const int npass = J.mode == 0 ? 4 : 4;  // mode 0: (xy | zr) x 2 halves; mode 1: x, y, z, row
-    for (int ps = 0; ps < npass; ++ps) {
-        if (J.mode == 1 && ps == 2 && !J.wz) continue;  // (uniform: 2-D plots have no z)
-        const int f = J.mode == 0 ? (ps >> 1) : ps;     // mode 0: 0 = (x, y), 1 = (z, row)
-        const int h = J.mode == 0 ? (ps & 1) : 0;
-        const int r0 = h * half, r1 = J.mode == 0 ? min(N, r0 + half) : N;
-        __syncthreads();  // (the sort's arrays / the previous pass are consumed)
-        for (int sub = 0; sub < (J.mode == 0 ? 2 : 1); ++sub) {  // mode 0: the two words
-            const double *col = J.mode == 0 ? (f == 0 ? (sub ? J.y : J.x) : (sub ? nullptr : J.z))
-                                            : (ps == 0 ? J.x : (ps == 1 ? J.y : (ps == 2 ? J.z : nullptr)));
-            double v[PS_R];
+    if (J.mode == 0) {
+        for (int f = 0; f < 2; ++f) {  // 0: (x, y); 1: (z, row)
+            const double *c0 = f == 0 ? J.x : J.z;  // (z nullable: 2-D layers store 0)
+            double v0[PS_R], v1[PS_R];
 #pragma unroll
             for (int u = 0; u < PS_R; ++u) {
                 const int i = t + u * PS_T;
-                v[u] = (pos[u] >= 0 && col) ? col[b + i] : 0.0;
+                v0[u] = (pos[u] >= 0 && c0) ? c0[b + i] : 0.0;
+                v1[u] = (pos[u] >= 0 && f == 0) ? J.y[b + i] : 0.0;
             }
 #pragma unroll
-            for (int u = 0; u < PS_R; ++u) {
-                if (pos[u] < 0 || pos[u] < r0 || pos[u] >= r1) continue;
-                const uint32_t row = (uint32_t)(b + t + u * PS_T);
-                if (J.mode == 0) {
-                    // (f 1: z -- 0 for 2-D layers, v = 0 -- then the row as the index word)
-                    sd[2 * (pos[u] - r0) + sub] = (f == 1 && sub == 1) ? __longlong_as_double((long long)row) : v[u];
-                } else if (ps == 3) {
-                    su[pos[u]] = row;
-                } else {
-                    sd[pos[u]] = v[u];
+            for (int h = 0; h < 2; ++h) {  // (unrolled: the halves' waits know v0 / v1 landed)
+                const int r0 = h * half, r1 = min(N, r0 + half);
+                PS_LDS_SYNC();  // (the sort's arrays / the previous half are consumed)
+#pragma unroll
+                for (int u = 0; u < PS_R; ++u) {
+                    if (pos[u] < r0 || pos[u] >= r1) continue;
+                    const uint32_t row = (uint32_t)(b + t + u * PS_T);
+                    sd[2 * (pos[u] - r0)] = v0[u];
+                    sd[2 * (pos[u] - r0) + 1] = f == 0 ? v1[u] : __longlong_as_double((long long)row);
                 }
+                PS_LDS_SYNC();
+                for (int r = r0 + t; r < r1; r += PS_T)
+                    *reinterpret_cast<double2 *>(reinterpret_cast<double *>(J.pts + b + r) + 2 * f) =
+                        make_double2(sd[2 * (r - r0)], sd[2 * (r - r0) + 1]);
             }
         }
-        __syncthreads();
-        if (J.mode == 0) {
-            for (int r = r0 + t; r < r1; r += PS_T)
-                *reinterpret_cast<double2 *>(reinterpret_cast<double *>(J.pts + b + r) + 2 * f) =
-                    make_double2(sd[2 * (r - r0)], sd[2 * (r - r0) + 1]);
-        } else {
+        return;
+    }
+    // mode 1: x and y loaded together (one round trip for both columns), then z, then the
+    // rows, each staged in full and stored coalesced
+    for (int f = 0; f < 2; ++f) {  // 0: x, y; 1: z (3-D), row
+        const double *c0 = f == 0 ? J.x : J.z;
+        double v0[PS_R], v1[PS_R];
+#pragma unroll
+        for (int u = 0; u < PS_R; ++u) {
+            const int i = t + u * PS_T;
+            v0[u] = (pos[u] >= 0 && c0) ? c0[b + i] : 0.0;
+            v1[u] = (pos[u] >= 0 && f == 0) ? J.y[b + i] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {  // x, y, z, row (unrolled, as mode 0's halves)
+            const int ps = 2 * f + q;
+            if (ps == 2 && !J.wz) continue;  // (uniform: 2-D plots have no z)
+            PS_LDS_SYNC();  // (the sort's arrays / the previous column are consumed)
+#pragma unroll
+            for (int u = 0; u < PS_R; ++u) {
+                if (pos[u] < 0) continue;
+                if (ps == 3) su[pos[u]] = (uint32_t)(b + t + u * PS_T);
+                else sd[pos[u]] = ps == 1 ? v1[u] : v0[u];
+            }
+            PS_LDS_SYNC();
             double *dst = ps == 0 ? J.wx : (ps == 1 ? J.wy : J.wz);
             for (int r = t; r < N; r += PS_T) {
                 if (ps == 3) J.worig[b + r] = su[r];

@@ -620,9 +620,11 @@ __device__ __forceinline__ double warm_d2(const NNArgs &a, int64_t i, double qx,
 template <int MD>
 __device__ __forceinline__ bool cert_try(const NNArgs &a, const GridView &g, const Stems &S,
                                          int64_t i, const double *T, unsigned long long &kmin_c,
-                                         unsigned long long &kmax, double &mv) {
+                                         unsigned long long &kmax, double &mv, double &qx,
+                                         double &qy) {
     const double ox = a.sx[i], oy = a.sy[i];
-    double qx = ox, qy = oy;
+    qx = ox;
+    qy = oy;
     if (T) {
         apply_T(T, qx, qy);
         a.sx[i] = qx;
@@ -675,11 +677,12 @@ __device__ __forceinline__ void cold_start(const GridView &g, const Stems &S, do
 // Step 2: the full scan of an uncertified query at its (already moved) position: warm
 // bound from the stored match (or the cold 3x3 start), every stem within d + pad
 // evaluated, the new bound G and the match slot stored, outputs written.
+// (qx, qy: the query's moved position, as cert_try stored it; a scan in the workgroup's
+// compacted phase takes it from LDS, not from the store another lane made)
 template <int MD, bool SKIP = false>
 __device__ __forceinline__ void cert_scan(const NNArgs &a, const GridView &g, const Stems &S,
-                                          int64_t i, bool warm, double pad,
+                                          int64_t i, double qx, double qy, bool warm, double pad,
                                           unsigned long long &kmin_c, unsigned long long &kmax) {
-    const double qx = a.sx[i], qy = a.sy[i];
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
     const double eps = cert_eps(g, qx, qy);
     Best2 b{INFINITY, 0x7fffffff, -1, INFINITY};
@@ -731,14 +734,13 @@ __device__ __forceinline__ void group_eval(const Stems &S, int p0, int p1, int l
 
 template <int MD, int GS, bool SKIP = false>
 __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView &g, const Stems &S,
-                                                int64_t i, int lg, double pad,
+                                                int64_t i, double qx, double qy, int lg, double pad,
                                                 unsigned long long &kmin_c, unsigned long long &kmax) {
-    const double qx = a.sx[i], qy = a.sy[i];
     const double qz = (MD == 3) ? a.sz[i] : 0.0;
     const double eps = cert_eps(g, qx, qy);
     const double d2w = warm_d2<MD>(a, i, qx, qy);
     if (!(d2w < INFINITY)) {  // no finite previous match: the serial cold search
-        if (lg == 0) cert_scan<MD>(a, g, S, i, false, pad, kmin_c, kmax);
+        if (lg == 0) cert_scan<MD>(a, g, S, i, qx, qy, false, pad, kmin_c, kmax);
         return;
     }
     Best2 b{d2w, 0x7fffffff, -1, INFINITY};
@@ -783,7 +785,7 @@ __device__ __forceinline__ void cert_scan_group(const NNArgs &a, const GridView 
     }
     if (lg != 0) return;
     if (b.slot < 0) {  // the stored match was not re-evaluated (not expected): cold search
-        cert_scan<MD>(a, g, S, i, false, pad, kmin_c, kmax);
+        cert_scan<MD>(a, g, S, i, qx, qy, false, pad, kmin_c, kmax);
         return;
     }
     const double gnew = fmin(sqrt(b.s2), rc - mq) - eps;
@@ -800,15 +802,18 @@ template <int MD>
 __device__ __forceinline__ bool nn_query_cert(const NNArgs &a, const GridView &g, const Stems &S,
                                               int64_t i, const double *T,
                                               unsigned long long &kmin_c, unsigned long long &kmax) {
-    double mv = 0.0;
-    if (a.warm_c && cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv)) return true;
-    if (!a.warm_c && T) {
-        double qx = a.sx[i], qy = a.sy[i];
-        apply_T(T, qx, qy);
-        a.sx[i] = qx;
-        a.sy[i] = qy;
+    double mv = 0.0, qx = 0.0, qy = 0.0;
+    if (a.warm_c && cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv, qx, qy)) return true;
+    if (!a.warm_c) {
+        qx = a.sx[i];
+        qy = a.sy[i];
+        if (T) {
+            apply_T(T, qx, qy);
+            a.sx[i] = qx;
+            a.sy[i] = qy;
+        }
     }
-    cert_scan<MD>(a, g, S, i, a.warm_c != 0, cert_pad(g, a.warm_c ? mv : INFINITY), kmin_c, kmax);
+    cert_scan<MD>(a, g, S, i, qx, qy, a.warm_c != 0, cert_pad(g, a.warm_c ? mv : INFINITY), kmin_c, kmax);
     return false;
 }
 
@@ -886,7 +891,8 @@ template <int MD, int Q>
 __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView &g, const Stems &S,
                                                  int64_t i0, const double *T,
                                                  unsigned long long &kmin_c,
-                                                 unsigned long long &kmax, double (&mv)[Q]) {
+                                                 unsigned long long &kmax, double (&mv)[Q],
+                                                 double (&mqx)[Q], double (&mqy)[Q]) {
     double ox[Q], oy[Q], wx[Q], wy[Q], wz[Q];
     float gp[Q];
 #pragma unroll
@@ -905,6 +911,7 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
     for (int q = 0; q < Q; ++q) {
         const int64_t i = i0 + (int64_t)q * 256;
         mv[q] = 0.0;
+        mqx[q] = mqy[q] = 0.0;
         if (i >= a.n) continue;
         double qx = ox[q], qy = oy[q];
         if (T) {
@@ -912,6 +919,8 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
             a.sx[i] = qx;
             a.sy[i] = qy;
         }
+        mqx[q] = qx;
+        mqy[q] = qy;
         const double eps = cert_eps(g, qx, qy);
         // the stored match's exact d2 at the moved query (eval_slot's operations)
         const double dx = qx - wx[q], dy = qy - wy[q];
@@ -941,7 +950,14 @@ __device__ __forceinline__ unsigned cert_try_qpt(const NNArgs &a, const GridView
 }
 
 
-template <int MD, bool APPLY, int Q, bool SKIP = false>
+// The compacted phase's hand-off is an LDS-only barrier: the scanning lanes take each
+// query's moved position from LDS (s_qx, s_qy) instead of loading the store another lane
+// made, so the barrier need not wait for the certified lanes' stores (__syncthreads()
+// waits for every outstanding global access, vmcnt(0)).
+#define NN_LDS_SYNC() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+// LQ: the single-plot kernels (the batch kernels keep the global hand-off: the two LDS
+// arrays cost their 5 waves per SIMD, 1,024 plots -1.4 %)
+template <int MD, bool APPLY, int Q, bool SKIP = false, bool LQ = false>
 __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g, int64_t i0) {
     // the three flags load together (the apply flag's load used to wait for the other two)
     const int sk = a.skip ? *a.skip : 0, ru = a.reuse ? *a.reuse : 0;
@@ -956,12 +972,13 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g,
         // packed densely onto its lanes (GS lanes per query when there are few of them)
         __shared__ int s_list[256 * Q];
         __shared__ double s_mv[256 * Q];
+        __shared__ double s_qx[LQ ? 256 * Q : 1], s_qy[LQ ? 256 * Q : 1];
         __shared__ int s_n;
         if (t == 0) s_n = 0;
         __syncthreads();
         const Stems S = stems_of(g.pts, g.m);
-        double mv[Q];
-        const unsigned pend = cert_try_qpt<MD, Q>(a, g, S, i0 + t, T, kmin_c, kmax, mv);
+        double mv[Q], mqx[Q], mqy[Q];
+        const unsigned pend = cert_try_qpt<MD, Q>(a, g, S, i0 + t, T, kmin_c, kmax, mv, mqx, mqy);
         const int lane = t & 63;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -974,23 +991,29 @@ __device__ __forceinline__ void nn_grid_body(const NNArgs &a, const GridView &g,
                 const int e = base + __popcll(m & ((1ULL << lane) - 1));
                 s_list[e] = q * 256 + t;
                 s_mv[e] = mv[q];
+                if constexpr (LQ) {
+                    s_qx[e] = mqx[q];
+                    s_qy[e] = mqy[q];
+                }
             }
         }
-        __syncthreads();
+        if constexpr (LQ) NN_LDS_SYNC();
+        else __syncthreads();  // (the certified lanes' moved positions land first)
         const int tot = s_n;
+#define NN_QXY(e) (LQ ? s_qx[(LQ ? (e) : 0)] : a.sx[i0 + s_list[e]]), (LQ ? s_qy[(LQ ? (e) : 0)] : a.sy[i0 + s_list[e]])
         if (a.cert_block >= 16 && tot <= 16) {
-            if (t < tot * 16) cert_scan_group<MD, 16, SKIP>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
+            if (t < tot * 16) cert_scan_group<MD, 16, SKIP>(a, g, S, i0 + s_list[t >> 4], NN_QXY(t >> 4), t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
         } else if (a.cert_block >= 8 && tot <= 32) {
-            if (t < tot * 8) cert_scan_group<MD, 8, SKIP>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
+            if (t < tot * 8) cert_scan_group<MD, 8, SKIP>(a, g, S, i0 + s_list[t >> 3], NN_QXY(t >> 3), t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
         } else if (a.cert_block >= 4 && tot <= 64) {
-            if (t < tot * 4) cert_scan_group<MD, 4, SKIP>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
+            if (t < tot * 4) cert_scan_group<MD, 4, SKIP>(a, g, S, i0 + s_list[t >> 2], NN_QXY(t >> 2), t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
         } else if (a.cert_block >= 2 && tot <= 128) {
-            if (t < tot * 2) cert_scan_group<MD, 2, SKIP>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
+            if (t < tot * 2) cert_scan_group<MD, 2, SKIP>(a, g, S, i0 + s_list[t >> 1], NN_QXY(t >> 1), t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
         } else if constexpr (Q == 1) {
-            if (t < tot) cert_scan<MD, SKIP>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
+            if (t < tot) cert_scan<MD, SKIP>(a, g, S, i0 + s_list[t], NN_QXY(t), true, cert_pad(g, s_mv[t]), kmin_c, kmax);
         } else {
             for (int e = t; e < tot; e += 256)
-                cert_scan<MD, SKIP>(a, g, S, i0 + s_list[e], true, cert_pad(g, s_mv[e]), kmin_c, kmax);
+                cert_scan<MD, SKIP>(a, g, S, i0 + s_list[e], NN_QXY(e), true, cert_pad(g, s_mv[e]), kmin_c, kmax);
         }
     } else {
         const Stems S = stems_of(g.pts, g.m);
@@ -1055,13 +1078,13 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
         // block-compacted: certificates first, then the workgroup's uncertified queries
         // packed densely onto its lanes (GS lanes per query when there are few of them)
         __shared__ int s_list[256];
-        __shared__ double s_mv[256];
+        __shared__ double s_mv[256], s_qx[256], s_qy[256];
         __shared__ int s_n;
         if (threadIdx.x == 0) s_n = 0;
         __syncthreads();
         const Stems S = stems_of(g.pts, g.m);
-        double mv = 0.0;
-        const bool pend = i < a.n && !cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv);
+        double mv = 0.0, mqx = 0.0, mqy = 0.0;
+        const bool pend = i < a.n && !cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv, mqx, mqy);
         const unsigned long long m = __ballot(pend);
         const int lane = threadIdx.x & 63;
         int base = 0;
@@ -1071,21 +1094,24 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
             const int q = base + __popcll(m & ((1ULL << lane) - 1));
             s_list[q] = (int)(i & 255);
             s_mv[q] = mv;
+            s_qx[q] = mqx;
+            s_qy[q] = mqy;
         }
-        __syncthreads();
+        NN_LDS_SYNC();  // (as nn_grid_body: the moved positions travel in LDS)
         const int tot = s_n;
         const int64_t i0 = i - threadIdx.x;
         const int t = threadIdx.x;
+        constexpr bool LQ = true;
         if (a.cert_block >= 16 && tot <= 16) {
-            if (t < tot * 16) cert_scan_group<MD, 16, SK1>(a, g, S, i0 + s_list[t >> 4], t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
+            if (t < tot * 16) cert_scan_group<MD, 16, SK1>(a, g, S, i0 + s_list[t >> 4], NN_QXY(t >> 4), t & 15, cert_pad(g, s_mv[t >> 4]), kmin_c, kmax);
         } else if (a.cert_block >= 8 && tot <= 32) {
-            if (t < tot * 8) cert_scan_group<MD, 8, SK1>(a, g, S, i0 + s_list[t >> 3], t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
+            if (t < tot * 8) cert_scan_group<MD, 8, SK1>(a, g, S, i0 + s_list[t >> 3], NN_QXY(t >> 3), t & 7, cert_pad(g, s_mv[t >> 3]), kmin_c, kmax);
         } else if (a.cert_block >= 4 && tot <= 64) {
-            if (t < tot * 4) cert_scan_group<MD, 4, SK1>(a, g, S, i0 + s_list[t >> 2], t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
+            if (t < tot * 4) cert_scan_group<MD, 4, SK1>(a, g, S, i0 + s_list[t >> 2], NN_QXY(t >> 2), t & 3, cert_pad(g, s_mv[t >> 2]), kmin_c, kmax);
         } else if (a.cert_block >= 2 && tot <= 128) {
-            if (t < tot * 2) cert_scan_group<MD, 2, SK1>(a, g, S, i0 + s_list[t >> 1], t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
+            if (t < tot * 2) cert_scan_group<MD, 2, SK1>(a, g, S, i0 + s_list[t >> 1], NN_QXY(t >> 1), t & 1, cert_pad(g, s_mv[t >> 1]), kmin_c, kmax);
         } else if (t < tot) {
-            cert_scan<MD, SK1>(a, g, S, i0 + s_list[t], true, cert_pad(g, s_mv[t]), kmin_c, kmax);
+            cert_scan<MD, SK1>(a, g, S, i0 + s_list[t], NN_QXY(t), true, cert_pad(g, s_mv[t]), kmin_c, kmax);
         }
     } else if (i < a.n) {
         if (a.gap && !a.warm_c) {
@@ -1105,7 +1131,7 @@ __global__ __launch_bounds__(256) NN_WPE void k_nn_grid(NNArgs a, GridView g) {
 
 template <int MD, bool APPLY>
 __global__ __launch_bounds__(256) NNQ_WPE void k_nn_grid_q(NNArgs a, GridView g) {
-    nn_grid_body<MD, APPLY, QPT, FICP_NN_SKIP_SINGLE != 0>(a, g, xcd_block(blockIdx.x, gridDim.x) * (256 * QPT));
+    nn_grid_body<MD, APPLY, QPT, FICP_NN_SKIP_SINGLE != 0, true>(a, g, xcd_block(blockIdx.x, gridDim.x) * (256 * QPT));
 }
 
 // Batch of plots (C4): tree i belongs to plot p = plot_of[i] and is matched against
@@ -1160,11 +1186,11 @@ __device__ __forceinline__ void nn_batch_rows(const NNArgs &a, const int32_t *__
         __shared__ int s_n;
         if (threadIdx.x == 0) s_n = 0;
         __syncthreads();
-        double mv = 0.0;
+        double mv = 0.0, mqx = 0.0, mqy = 0.0;
         bool pend = false;
         if (live) {
             const GridView g = plot_view(grids[p], pts, cell_start, m);
-            pend = !cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv);
+            pend = !cert_try<MD>(a, g, S, i, T, kmin_c, kmax, mv, mqx, mqy);
         }
         const unsigned long long msk = __ballot(pend);
         const int lane = threadIdx.x & 63;
@@ -1176,7 +1202,7 @@ __device__ __forceinline__ void nn_batch_rows(const NNArgs &a, const int32_t *__
             s_list[q] = (int)(i & 255);
             s_mv[q] = mv;
         }
-        __syncthreads();
+        __syncthreads();  // (the certified lanes' moved positions land first)
         const int tot = s_n;
         const int64_t i0 = i - threadIdx.x;
         const int t = threadIdx.x;
@@ -1190,10 +1216,11 @@ __device__ __forceinline__ void nn_batch_rows(const NNArgs &a, const int32_t *__
             const GridView gq = plot_view(grids[plot_of[iq]], pts, cell_start, m);
             const double pad = cert_pad(gq, s_mv[q]);
             constexpr bool SK = FICP_NN_SKIP_SAME != 0;
-            if (gs == 8) cert_scan_group<MD, 8, SK>(a, gq, S, iq, t & 7, pad, kmin_c, kmax);
-            else if (gs == 4) cert_scan_group<MD, 4, SK>(a, gq, S, iq, t & 3, pad, kmin_c, kmax);
-            else if (gs == 2) cert_scan_group<MD, 2, SK>(a, gq, S, iq, t & 1, pad, kmin_c, kmax);
-            else cert_scan<MD, SK>(a, gq, S, iq, true, pad, kmin_c, kmax);
+            const double qx = a.sx[iq], qy = a.sy[iq];
+            if (gs == 8) cert_scan_group<MD, 8, SK>(a, gq, S, iq, qx, qy, t & 7, pad, kmin_c, kmax);
+            else if (gs == 4) cert_scan_group<MD, 4, SK>(a, gq, S, iq, qx, qy, t & 3, pad, kmin_c, kmax);
+            else if (gs == 2) cert_scan_group<MD, 2, SK>(a, gq, S, iq, qx, qy, t & 1, pad, kmin_c, kmax);
+            else cert_scan<MD, SK>(a, gq, S, iq, qx, qy, true, pad, kmin_c, kmax);
         }
     } else if (live) {
         const GridView g = plot_view(grids[p], pts, cell_start, m);
